@@ -1,0 +1,121 @@
+/*
+ * fst_batch.h -- batched entry points of libfst_amd (new; no libfst counterpart).
+ *
+ * A batch is N linear-chain acceptors given as CSR label sequences
+ * (labels[offsets[i] .. offsets[i+1]) for string i).  Each string is the FST
+ * `fst_compile_string` would build (src/string.zig:24-50): state k --l:l/One-->
+ * k+1, final(L) = One; labels are used as given (fst_compile_string's byte+1
+ * encoding is the caller's choice).  Every string is composed against ONE
+ * frozen rhs FstHandle and reduced to its 1-best path with either
+ *   FST_SEM_LAZY : the result fst_compose_frozen_shortest_path(a, b, n) returns
+ *                  (src/ops/compose-shortest-path.zig:26-401), or
+ *   FST_SEM_EAGER: the result fst_shortest_path(fst_compose_frozen(a, b), n)
+ *                  returns (src/ops/compose.zig:29-198 then
+ *                  src/ops/shortest-path.zig:18-139) -- what the reference bench
+ *                  scenario compose_frozen_shortest_path_* measures.
+ * The two agree on weight but may pick different equal-weight paths.
+ *
+ * Per-string results use the FST_PATH_* codes; a string with FST_PATH_OK has a
+ * result chain of path_len arcs (states 0..path_len, start 0, final(path_len) =
+ * final_weight), FST_PATH_EMPTY is the reference's empty FST.
+ */
+#ifndef LIBFST_AMD_FST_BATCH_H
+#define LIBFST_AMD_FST_BATCH_H
+
+#include "fst.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    FST_SEM_LAZY = 0,
+    FST_SEM_EAGER = 1,
+} FstSemantics;
+
+typedef enum {
+    FST_PATH_OK = 0,           /* a 1-best chain */
+    FST_PATH_EMPTY = 1,        /* empty result FST (no path, n == 0, or rhs has no start) */
+    FST_PATH_ERROR_N = 2,      /* n not in {0, 1}: the reference returns FST_INVALID_HANDLE */
+    FST_PATH_CYCLE = 3,        /* back-pointer cycle; the reference would not terminate */
+    FST_PATH_OVERFLOW = 4,     /* internal: engine capacity exceeded (retried internally) */
+    FST_PATH_UNSUPPORTED = 5,  /* input outside every available engine's contract */
+    FST_PATH_OUTPUT_FULL = 6,  /* device arc arena too small */
+} FstPathStatus;
+
+/* Host-memory result of a batch (allocated by the library). */
+typedef struct {
+    uint32_t num_strings;
+    int32_t* status;          /* [num_strings] FstPathStatus */
+    uint64_t* path_offsets;   /* [num_strings + 1] CSR offsets into the arc arrays */
+    uint32_t* ilabels;        /* [total_arcs] */
+    uint32_t* olabels;        /* [total_arcs] */
+    double* weights;          /* [total_arcs] */
+    double* final_weights;    /* [num_strings] */
+    uint64_t total_arcs;
+} FstBatchResult;
+
+typedef struct {
+    int32_t device;           /* HIP device ordinal (-1: current device) */
+    uint32_t semantics;       /* FstSemantics */
+    uint32_t flags;           /* reserved, 0 */
+} FstBatchOptions;
+
+/* Host arrays in, host result out (H2D, kernels, D2H).  Returns FST_INVALID_ARG for an
+ * invalid handle or malformed offsets; per-string outcomes are in out->status. */
+FstError fst_compose_frozen_shortest_path_batch(FstHandle b, const uint32_t* labels,
+                                                const uint64_t* offsets, uint32_t num_strings,
+                                                uint32_t n, const FstBatchOptions* opts,
+                                                FstBatchResult* out);
+void fst_batch_result_free(FstBatchResult* r);
+
+/* Device-resident batch: every pointer is device memory on opts->device; the call is
+ * asynchronous on `stream` (a hipStream_t, or NULL for the null stream).  Paths are
+ * appended to the arc arena; *arc_cursor (device) is reset by the call.  `work`, if
+ * non-NULL, receives two counters per string: product states and relaxations. */
+typedef struct {
+    int32_t* status;            /* [num_strings] */
+    uint32_t* path_len;         /* [num_strings] */
+    uint64_t* path_offset;      /* [num_strings] offset of the string's first arc */
+    double* final_weight;       /* [num_strings] */
+    uint32_t* ilabels;          /* [arc_capacity] */
+    uint32_t* olabels;          /* [arc_capacity] */
+    double* weights;            /* [arc_capacity] */
+    uint64_t arc_capacity;
+    uint64_t* arc_cursor;       /* [1] */
+    uint32_t* work;             /* [2 * num_strings] or NULL */
+} FstDeviceBatch;
+
+FstError fst_device_compose_shortest_path(FstHandle b, const uint32_t* d_labels,
+                                          const uint64_t* d_offsets, uint32_t num_strings,
+                                          uint32_t max_len, uint32_t n,
+                                          const FstBatchOptions* opts, const FstDeviceBatch* out,
+                                          void* stream);
+
+/* Bring a frozen FST's device copy up on `device` (blob H2D + on-device SoA mirror). */
+FstError fst_device_prepare(FstHandle b, int32_t device);
+/* Adopt a blob that already sits in device memory on `device` (e.g. received by an
+ * RCCL broadcast): validates the header, builds the SoA mirror, returns a new handle.
+ * `host_copy` must hold the same bytes (used for host-side queries); may be NULL, in
+ * which case the bytes are copied back from the device. */
+FstHandle fst_device_adopt_blob(const void* d_blob, uint64_t len, int32_t device,
+                                const void* host_copy);
+
+/* Engine introspection for benchmarks (last device launch on this thread). */
+typedef struct {
+    double kernel_ms;           /* sum of kernel durations, HIP events on the launch stream */
+    uint32_t launches;          /* kernel launches in the call */
+    uint32_t engine;            /* 0 = eager-layered, 1 = lazy-wave, 2 = eager-general */
+    uint32_t grid;              /* workgroups of the dominant kernel */
+} FstLaunchStats;
+FstError fst_last_launch_stats(FstLaunchStats* out);
+
+/* Generators of the reference bench's synthetic rhs (bench/optimize-bench.zig:219-306),
+ * built host-side and frozen: 0 = ambiguous chain, 1 = epsilon dense, 2 = branching. */
+FstHandle fst_bench_transducer(uint32_t kind, uint32_t transducer_len, uint32_t branches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LIBFST_AMD_FST_BATCH_H */

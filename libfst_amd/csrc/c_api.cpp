@@ -1,0 +1,787 @@
+// c_api.cpp -- the fst.h / fst_batch.h C ABI of libfst_amd.
+//
+// Handle tables, snapshots and pinning follow src/c-api.zig:105-271: u64 handles
+// (generation << 32 | slot), one global mutex for table bookkeeping only, compute
+// outside the lock on a cloned lhs, the frozen rhs pinned (a shared_ptr copy here)
+// so that fst_free() during a call defers destruction.
+//
+// Every compose / shortest-path entry computes on the GPU; there is no CPU
+// fallback.  If no HIP device is usable the entry fails (FST_INVALID_HANDLE /
+// FST_INVALID_ARG) and, once per process, says why on stderr.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/fst_batch.h"
+#include "device_engine.hpp"
+#include "host_fst.hpp"
+
+using namespace fstamd;
+
+namespace {
+
+constexpr uint64_t kInvalid = UINT64_MAX;
+
+template <class T>
+class HandleTable {  // src/c-api.zig:132-271
+ public:
+  uint64_t insert(std::shared_ptr<T> p) {
+    uint32_t idx;
+    if (!free_.empty()) {
+      idx = free_.back();
+      free_.pop_back();
+      if (++gen_[idx] == 0) gen_[idx] = 1;
+      slots_[idx] = std::move(p);
+    } else {
+      idx = (uint32_t)slots_.size();
+      if (idx == 0xFFFFFFFFu) return kInvalid;
+      slots_.push_back(std::move(p));
+      gen_.push_back(1);
+    }
+    return ((uint64_t)gen_[idx] << 32) | idx;
+  }
+  // get/pin: a shared_ptr copy keeps the object alive outside the lock.
+  std::shared_ptr<T> get(uint64_t h) const {
+    if (h == kInvalid) return nullptr;
+    const uint32_t g = (uint32_t)(h >> 32), idx = (uint32_t)h;
+    if (g == 0 || idx == 0xFFFFFFFFu || idx >= slots_.size()) return nullptr;
+    if (gen_[idx] != g) return nullptr;
+    return slots_[idx];
+  }
+  bool remove(uint64_t h) {
+    if (!get(h)) return false;
+    const uint32_t idx = (uint32_t)h;
+    slots_[idx].reset();
+    if (++gen_[idx] == 0) gen_[idx] = 1;  // invalidateSlot
+    free_.push_back(idx);
+    return true;
+  }
+  void clear() {
+    slots_.clear();
+    gen_.clear();
+    free_.clear();
+  }
+
+ private:
+  std::vector<std::shared_ptr<T>> slots_;
+  std::vector<uint32_t> gen_;
+  std::vector<uint32_t> free_;
+};
+
+std::mutex g_api_mu;
+HandleTable<MutableFst> g_mut;
+HandleTable<FrozenFst> g_fst;
+
+thread_local LaunchStats t_last_stats;
+
+bool trace_enabled() {  // LIBFST_TRACE_COMPOSE, src/c-api.zig:55-64
+  static const bool on = std::getenv("LIBFST_TRACE_COMPOSE") != nullptr;
+  return on;
+}
+
+void trace(const char* tag, uint64_t a, uint64_t b, size_t in_s, size_t in_a, size_t out_s,
+           size_t out_a, double us, double kernel_ms) {
+  if (!trace_enabled()) return;
+  std::fprintf(stderr,
+               "[libfst] %s op=fst_compose_frozen a=%llu b=%llu in_states=%zu in_arcs=%zu "
+               "out_states=%zu out_arcs=%zu elapsed_us=%lld kernel_us=%lld\n",
+               tag, (unsigned long long)a, (unsigned long long)b, in_s, in_a, out_s, out_a,
+               (long long)us, (long long)(kernel_ms * 1000.0));
+}
+
+int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  return dev;
+}
+
+bool gpu_available() {
+  static int ok = -1;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (ok < 0) {
+    int n = 0;
+    ok = (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
+    if (!ok)
+      std::fprintf(stderr,
+                   "[libfst_amd] no usable HIP device: compose/shortest-path entries fail "
+                   "(there is no CPU fallback)\n");
+  }
+  return ok == 1;
+}
+
+// RAII device buffer
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(size_t n) {
+    if (hipMalloc(&p, std::max<size_t>(n, 16)) != hipSuccess) p = nullptr;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+};
+
+struct HostPaths {
+  std::vector<int32_t> status;
+  std::vector<uint32_t> len;
+  std::vector<uint64_t> off;
+  std::vector<double> fin;
+  std::vector<uint32_t> il, ol;
+  std::vector<double> w;
+};
+
+// Device outputs for `num` strings with `arc_cap` arena slots.
+struct DevOut {
+  DevBuf status, len, off, fin, il, ol, w, cursor;
+  BatchOutDev v{};
+  DevOut(uint32_t num, uint64_t arc_cap)
+      : status(num * 4ull), len(num * 4ull), off(num * 8ull), fin(num * 8ull), il(arc_cap * 4),
+        ol(arc_cap * 4), w(arc_cap * 8), cursor(8) {
+    v.status = (int32_t*)status.p;
+    v.path_len = (uint32_t*)len.p;
+    v.path_off = (uint64_t*)off.p;
+    v.final_w = (double*)fin.p;
+    v.out_il = (uint32_t*)il.p;
+    v.out_ol = (uint32_t*)ol.p;
+    v.out_w = (double*)w.p;
+    v.arc_cap = arc_cap;
+    v.cursor = (unsigned long long*)cursor.p;
+    v.work = nullptr;
+  }
+  bool ok() const {
+    return status.p && len.p && off.p && fin.p && il.p && ol.p && w.p && cursor.p;
+  }
+  bool download(uint32_t num, HostPaths* h) const {
+    h->status.resize(num);
+    h->len.resize(num);
+    h->off.resize(num);
+    h->fin.resize(num);
+    unsigned long long used = 0;
+    if (hipMemcpy(&used, cursor.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    used = std::min<unsigned long long>(used, v.arc_cap);
+    h->il.resize(used);
+    h->ol.resize(used);
+    h->w.resize(used);
+    if (num &&
+        (hipMemcpy(h->status.data(), status.p, num * 4ull, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(h->len.data(), len.p, num * 4ull, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(h->off.data(), off.p, num * 8ull, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(h->fin.data(), fin.p, num * 8ull, hipMemcpyDeviceToHost) != hipSuccess))
+      return false;
+    if (used &&
+        (hipMemcpy(h->il.data(), il.p, used * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(h->ol.data(), ol.p, used * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(h->w.data(), w.p, used * 8, hipMemcpyDeviceToHost) != hipSuccess))
+      return false;
+    return true;
+  }
+};
+
+// Result FST of one string: linear chain, or the empty FST (src/ops/*:382-400).
+MutableFst chain_result(const HostPaths& h, uint32_t i) {
+  MutableFst r;
+  if (h.status[i] != kPathOk) return r;
+  const uint32_t P = h.len[i];
+  r.add_states(P + 1);
+  r.set_start(0);
+  r.set_final(P, h.fin[i]);
+  for (uint32_t k = 0; k < P; ++k) {
+    const uint64_t o = h.off[i] + k;
+    r.add_arc(k, Arc{h.il[o], h.ol[o], h.w[o], k + 1});
+  }
+  return r;
+}
+
+// Lazy 1-best of one general lhs on the GPU (single-call C ABI path).
+int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* result,
+                    double* kernel_ms) {
+  const int dev = current_device();
+  if (dev < 0) return -1;
+  DeviceFst* D = b.device(dev);
+  if (!D) return -1;
+  // CSR of the lhs, arcs in insertion order.
+  const uint32_t ns = (uint32_t)a.num_states();
+  std::vector<uint32_t> soff(ns + 1, 0), il, ol, nx;
+  std::vector<double> w, fin(ns);
+  uint32_t maxdeg = 0;
+  for (uint32_t s = 0; s < ns; ++s) {
+    soff[s] = (uint32_t)il.size();
+    fin[s] = a.final_weight(s);
+    maxdeg = std::max<uint32_t>(maxdeg, (uint32_t)a.arcs(s).size());
+    for (const Arc& x : a.arcs(s)) {
+      il.push_back(x.ilabel);
+      ol.push_back(x.olabel);
+      w.push_back(x.weight);
+      nx.push_back(x.nextstate);
+    }
+  }
+  soff[ns] = (uint32_t)il.size();
+  const size_t na = il.size();
+  DevBuf d_off((ns + 1) * 4ull), d_il(na * 4), d_ol(na * 4), d_w(na * 8), d_nx(na * 4),
+      d_fin(ns * 8ull);
+  if (!d_off.p || !d_il.p || !d_ol.p || !d_w.p || !d_nx.p || !d_fin.p) return -1;
+  (void)hipMemcpy(d_off.p, soff.data(), (ns + 1) * 4ull, hipMemcpyHostToDevice);
+  if (na) {
+    (void)hipMemcpy(d_il.p, il.data(), na * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_ol.p, ol.data(), na * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_w.p, w.data(), na * 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_nx.p, nx.data(), na * 4, hipMemcpyHostToDevice);
+  }
+  if (ns) (void)hipMemcpy(d_fin.p, fin.data(), ns * 8ull, hipMemcpyHostToDevice);
+  GraphInput g{};
+  g.state_off = (const uint32_t*)d_off.p;
+  g.arc_il = (const uint32_t*)d_il.p;
+  g.arc_ol = (const uint32_t*)d_ol.p;
+  g.arc_w = (const double*)d_w.p;
+  g.arc_next = (const uint32_t*)d_nx.p;
+  g.final_w = (const double*)d_fin.p;
+  g.num_states = ns;
+  g.start = a.start();
+  g.max_outdeg = maxdeg;
+  DeviceEngine& E = DeviceEngine::get(dev);
+  std::lock_guard<std::mutex> lk(E.mutex());
+  // Grow the tuple capacity on overflow (the reference has no limit but memory).
+  for (uint32_t ncap = 1u << 14; ncap <= (1u << 26); ncap <<= 2) {
+    g.ncap = ncap;
+    const uint64_t arc_cap = std::max<uint64_t>(ncap, 1024);
+    DevOut out(1, arc_cap);
+    if (!out.ok()) return -1;
+    LaunchStats st;
+    if (E.run_graph(*D, g, n, 0, out.v, nullptr, &st) != hipSuccess) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    HostPaths h;
+    if (!out.download(1, &h)) return -1;
+    t_last_stats = st;
+    if (kernel_ms) *kernel_ms = st.kernel_ms;
+    const int32_t s = h.status[0];
+    if (s == kPathOverflow || s == kPathOutputFull) continue;
+    if (s == kPathErrorN) return 2;
+    if (s == kPathCycle) return 3;
+    *result = chain_result(h, 0);  // OK or EMPTY
+    return 0;
+  }
+  return -1;
+}
+
+// Chain batch on the GPU from host arrays; fills `h` in input order.
+FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
+                              uint32_t num, uint32_t n, int semantics, int dev, HostPaths* h) {
+  if (dev < 0) dev = current_device();
+  if (dev < 0) return FST_INVALID_ARG;
+  if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  DeviceFst* D = b.device(dev);
+  if (!D) return FST_OOM;
+  const uint64_t total = num ? offsets[num] - offsets[0] : 0;
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < num; ++i)
+    max_len = std::max<uint32_t>(max_len, (uint32_t)(offsets[i + 1] - offsets[i]));
+  std::vector<uint64_t> rebased(num + 1);
+  for (uint32_t i = 0; i <= num; ++i) rebased[i] = offsets[i] - offsets[0];
+  DevBuf d_lab(total * 4), d_off((num + 1) * 8ull);
+  if (!d_lab.p || !d_off.p) return FST_OOM;
+  if (total && hipMemcpy(d_lab.p, labels + offsets[0], total * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return FST_OOM;
+  if (hipMemcpy(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice) != hipSuccess)
+    return FST_OOM;
+  ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
+  // Arena: chains without rhs epsilons produce exactly L arcs per path.
+  uint64_t arc_cap = std::max<uint64_t>(total + 16, 1024);
+  DeviceEngine& E = DeviceEngine::get(dev);
+  std::lock_guard<std::mutex> lk(E.mutex());
+  for (int attempt = 0; attempt < 6; ++attempt, arc_cap *= 4) {
+    DevOut out(num, arc_cap);
+    if (!out.ok()) return FST_OOM;
+    LaunchStats st;
+    if (E.run_chain(*D, in, n, semantics, out.v, nullptr, &st) != hipSuccess) return FST_OOM;
+    if (hipDeviceSynchronize() != hipSuccess) return FST_OOM;
+    if (!out.download(num, h)) return FST_OOM;
+    t_last_stats = st;
+    bool full = false;
+    for (uint32_t i = 0; i < num; ++i) full |= h->status[i] == kPathOutputFull;
+    if (!full) return FST_OK;
+  }
+  return FST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- MutableFst lifecycle -----------------------------------------------------------
+
+FstMutableHandle fst_mutable_new(void) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_mut.insert(std::make_shared<MutableFst>());
+}
+
+FstMutableHandle fst_mutable_clone(FstMutableHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return kInvalid;
+  return g_mut.insert(std::make_shared<MutableFst>(*m));
+}
+
+void fst_mutable_free(FstMutableHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  g_mut.remove(handle);
+}
+
+uint32_t fst_mutable_add_state(FstMutableHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return FST_NO_STATE;
+  return m->add_state();
+}
+
+FstError fst_mutable_set_start(FstMutableHandle handle, uint32_t state) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return FST_INVALID_ARG;
+  if (state >= m->num_states()) return FST_INVALID_STATE;
+  m->set_start(state);
+  return FST_OK;
+}
+
+FstError fst_mutable_set_final(FstMutableHandle handle, uint32_t state, double weight) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return FST_INVALID_ARG;
+  if (state >= m->num_states()) return FST_INVALID_STATE;
+  m->set_final(state, weight);
+  return FST_OK;
+}
+
+FstError fst_mutable_add_arc(FstMutableHandle handle, uint32_t src, uint32_t ilabel,
+                             uint32_t olabel, double weight, uint32_t nextstate) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return FST_INVALID_ARG;
+  if (src >= m->num_states()) return FST_INVALID_STATE;
+  if (nextstate >= m->num_states()) return FST_INVALID_STATE;
+  m->add_arc(src, Arc{ilabel, olabel, weight, nextstate});
+  return FST_OK;
+}
+
+uint32_t fst_mutable_start(FstMutableHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  return m ? m->start() : FST_NO_STATE;
+}
+
+uint32_t fst_mutable_num_states(FstMutableHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  return m ? (uint32_t)m->num_states() : 0;
+}
+
+uint32_t fst_mutable_num_arcs(FstMutableHandle handle, uint32_t state) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m || state >= m->num_states()) return 0;
+  return (uint32_t)m->num_arcs(state);
+}
+
+double fst_mutable_final_weight(FstMutableHandle handle, uint32_t state) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m || state >= m->num_states()) return w_zero();
+  return m->final_weight(state);
+}
+
+uint32_t fst_mutable_get_arcs(FstMutableHandle handle, uint32_t state, FstArc* buf,
+                              uint32_t buf_len) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m || state >= m->num_states()) return 0;
+  const auto& arcs = m->arcs(state);
+  const uint32_t count = std::min<uint32_t>((uint32_t)arcs.size(), buf_len);
+  if (buf)
+    for (uint32_t i = 0; i < count; ++i)
+      buf[i] = FstArc{arcs[i].ilabel, arcs[i].olabel, arcs[i].weight, arcs[i].nextstate};
+  return count;
+}
+
+// ---- Freeze / frozen ----------------------------------------------------------------
+
+FstHandle fst_freeze(FstMutableHandle mutable_handle) {
+  std::shared_ptr<MutableFst> snap;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    auto m = g_mut.get(mutable_handle);
+    if (!m) return kInvalid;
+    snap = std::make_shared<MutableFst>(*m);  // clone under the lock (c-api.zig:507-517)
+  }
+  auto f = FrozenFst::from_mutable(*snap, kWeightTropical);
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
+}
+
+void fst_free(FstHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  g_fst.remove(handle);
+}
+
+uint32_t fst_start(FstHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto f = g_fst.get(handle);
+  return f ? f->start() : FST_NO_STATE;
+}
+
+uint32_t fst_num_states(FstHandle handle) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto f = g_fst.get(handle);
+  return f ? f->num_states() : 0;
+}
+
+uint32_t fst_num_arcs(FstHandle handle, uint32_t state) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto f = g_fst.get(handle);
+  if (!f || state >= f->num_states()) return 0;
+  return f->num_arcs(state);
+}
+
+double fst_final_weight(FstHandle handle, uint32_t state) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto f = g_fst.get(handle);
+  if (!f || state >= f->num_states()) return w_zero();
+  return f->final_weight(state);
+}
+
+uint32_t fst_get_arcs(FstHandle handle, uint32_t state, FstArc* buf, uint32_t buf_len) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto f = g_fst.get(handle);
+  if (!f || state >= f->num_states()) return 0;
+  const StateEntry& e = f->states()[state];
+  const uint32_t count = std::min(e.num_arcs, buf_len);
+  if (buf)
+    for (uint32_t i = 0; i < count; ++i) {
+      const PackedArc& a = f->arcs()[e.arc_offset + i];
+      buf[i] = FstArc{a.ilabel, a.olabel, a.weight, a.nextstate};
+    }
+  return count;
+}
+
+// ---- Binary I/O (src/io/binary.zig:9-36) ----------------------------------------------
+
+FstHandle fst_load(const char* path) {
+  if (!path) return kInvalid;
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return kInvalid;
+  std::vector<uint8_t> bytes;
+  if (std::fseek(fp, 0, SEEK_END) == 0) {
+    const long sz = std::ftell(fp);
+    if (sz >= 0) {
+      bytes.resize((size_t)sz);
+      std::rewind(fp);
+      if (sz > 0 && std::fread(bytes.data(), 1, (size_t)sz, fp) != (size_t)sz) bytes.clear();
+    }
+  }
+  std::fclose(fp);
+  if (bytes.size() < sizeof(Header)) return kInvalid;
+  auto f = FrozenFst::from_bytes(bytes.data(), bytes.size(), kWeightTropical, nullptr);
+  if (!f) return kInvalid;
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
+}
+
+FstError fst_save(FstHandle handle, const char* path) {
+  if (!path) return FST_INVALID_ARG;
+  std::shared_ptr<FrozenFst> f;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    f = g_fst.get(handle);
+    if (!f) return FST_INVALID_ARG;
+  }
+  FILE* fp = std::fopen(path, "wb");
+  if (!fp) return FST_IO_ERROR;
+  const bool ok = std::fwrite(f->bytes(), 1, f->size(), fp) == f->size();
+  std::fclose(fp);
+  return ok ? FST_OK : FST_IO_ERROR;
+}
+
+// ---- The hot path -----------------------------------------------------------------
+
+FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, FstHandle b_handle,
+                                                  uint32_t n) {
+  const auto t0 = std::chrono::steady_clock::now();
+  auto us = [&] {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  };
+  std::shared_ptr<MutableFst> a;
+  std::shared_ptr<FrozenFst> b;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    auto ha = g_mut.get(a_handle);
+    if (!ha) {
+      trace("sp_invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
+      return kInvalid;
+    }
+    a = std::make_shared<MutableFst>(*ha);  // snapshot (c-api.zig:754)
+    b = g_fst.get(b_handle);                // pin (c-api.zig:759)
+    if (!b) {
+      trace("sp_invalid_b", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(), 0);
+      return kInvalid;
+    }
+  }
+  MutableFst result;
+  // compose-shortest-path.zig:30-33: empty checks first, then n.
+  if (a->start() == kNoState || b->start() == kNoState || n == 0) {
+    // empty result
+  } else if (n != 1) {
+    trace("sp_compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(), 0);
+    return kInvalid;
+  } else {
+    if (!gpu_available()) return kInvalid;
+    double kms = 0;
+    const int rc = run_lazy_single(*a, *b, n, &result, &kms);
+    if (rc != 0) {
+      trace("sp_compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(),
+            kms);
+      return kInvalid;
+    }
+  }
+  trace("sp_ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
+        result.total_arcs(), us(), t_last_stats.kernel_ms);
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
+}
+
+FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handle) {
+  // Eager lattice output (src/ops/compose.zig:29-198) needs the general eager
+  // engine, which is not built yet.  Validate arguments like the
+  // reference, then report an error rather than computing on the CPU.
+  std::lock_guard<std::mutex> g(g_api_mu);
+  if (!g_mut.get(a_handle) || !g_fst.get(b_handle)) return kInvalid;
+  if (trace_enabled())
+    std::fprintf(stderr, "[libfst_amd] fst_compose_frozen: lattice output not implemented\n");
+  return kInvalid;
+}
+
+FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return kInvalid;
+  if (m->start() == kNoState || n == 0) return g_mut.insert(std::make_shared<MutableFst>());
+  if (n != 1) return kInvalid;
+  return kInvalid;  // general-lattice 1-best: see DESIGN.md §8 (next)
+}
+
+// ---- Strings ------------------------------------------------------------------------
+
+FstMutableHandle fst_compile_string(const uint8_t* input, uint32_t len) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  if (!input) return kInvalid;
+  return g_mut.insert(
+      std::make_shared<MutableFst>(MutableFst::compile_string(input, len, input, len)));
+}
+
+static int32_t print_impl(FstMutableHandle handle, uint8_t* buf, uint32_t buf_len, bool out_tape) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto m = g_mut.get(handle);
+  if (!m) return -1;
+  std::vector<uint8_t> s;
+  if (!m->print_string(out_tape, &s)) return -1;
+  if (s.size() > buf_len) return -1;
+  if (buf && !s.empty()) std::memcpy(buf, s.data(), s.size());
+  return (int32_t)s.size();
+}
+
+int32_t fst_print_string(FstMutableHandle handle, uint8_t* buf, uint32_t buf_len) {
+  return print_impl(handle, buf, buf_len, false);
+}
+
+int32_t fst_print_output_string(FstMutableHandle handle, uint8_t* buf, uint32_t buf_len) {
+  return print_impl(handle, buf, buf_len, true);
+}
+
+void fst_teardown(void) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  g_mut.clear();
+  g_fst.clear();
+}
+
+// ---- Batched entries (fst_batch.h) ----------------------------------------------------
+
+FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32_t* labels,
+                                                const uint64_t* offsets, uint32_t num_strings,
+                                                uint32_t n, const FstBatchOptions* opts,
+                                                FstBatchResult* out) {
+  if (!out || !offsets || (!labels && num_strings && offsets[num_strings] != offsets[0]))
+    return FST_INVALID_ARG;
+  std::memset(out, 0, sizeof(*out));
+  for (uint32_t i = 0; i < num_strings; ++i)
+    if (offsets[i + 1] < offsets[i]) return FST_INVALID_ARG;
+  std::shared_ptr<FrozenFst> b;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    b = g_fst.get(b_handle);
+  }
+  if (!b) return FST_INVALID_ARG;
+  if (!gpu_available()) return FST_INVALID_ARG;
+  const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
+  const int dev = opts ? opts->device : -1;
+  HostPaths h;
+  FstError e = run_chain_batch_host(*b, labels, offsets, num_strings, n, semantics, dev, &h);
+  if (e != FST_OK) return e;
+  // CSR in input order
+  out->num_strings = num_strings;
+  out->status = (int32_t*)std::malloc(std::max<size_t>(num_strings, 1) * 4);
+  out->path_offsets = (uint64_t*)std::malloc((num_strings + 1ull) * 8);
+  out->final_weights = (double*)std::malloc(std::max<size_t>(num_strings, 1) * 8);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < num_strings; ++i) {
+    out->path_offsets[i] = tot;
+    if (h.status[i] == kPathOk) tot += h.len[i];
+  }
+  out->path_offsets[num_strings] = tot;
+  out->total_arcs = tot;
+  out->ilabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
+  out->olabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
+  out->weights = (double*)std::malloc(std::max<uint64_t>(tot, 1) * 8);
+  for (uint32_t i = 0; i < num_strings; ++i) {
+    out->status[i] = h.status[i];
+    out->final_weights[i] = h.status[i] == kPathOk ? h.fin[i] : w_zero();
+    if (h.status[i] != kPathOk) continue;
+    const uint64_t o = out->path_offsets[i];
+    for (uint32_t k = 0; k < h.len[i]; ++k) {
+      out->ilabels[o + k] = h.il[h.off[i] + k];
+      out->olabels[o + k] = h.ol[h.off[i] + k];
+      out->weights[o + k] = h.w[h.off[i] + k];
+    }
+  }
+  return FST_OK;
+}
+
+void fst_batch_result_free(FstBatchResult* r) {
+  if (!r) return;
+  std::free(r->status);
+  std::free(r->path_offsets);
+  std::free(r->ilabels);
+  std::free(r->olabels);
+  std::free(r->weights);
+  std::free(r->final_weights);
+  std::memset(r, 0, sizeof(*r));
+}
+
+FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_labels,
+                                          const uint64_t* d_offsets, uint32_t num_strings,
+                                          uint32_t max_len, uint32_t n,
+                                          const FstBatchOptions* opts, const FstDeviceBatch* o,
+                                          void* stream) {
+  if (!o || !d_offsets) return FST_INVALID_ARG;
+  std::shared_ptr<FrozenFst> b;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    b = g_fst.get(b_handle);
+  }
+  if (!b) return FST_INVALID_ARG;
+  if (!gpu_available()) return FST_INVALID_ARG;
+  int dev = opts && opts->device >= 0 ? opts->device : current_device();
+  if (dev < 0 || hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  DeviceFst* D = b->device(dev);
+  if (!D) return FST_OOM;
+  BatchOutDev v{o->status, o->path_len, o->path_offset, o->final_weight, o->ilabels,
+                o->olabels, o->weights, o->arc_capacity,
+                (unsigned long long*)o->arc_cursor, o->work};
+  ChainInput in{d_labels, d_offsets, num_strings, max_len};
+  DeviceEngine& E = DeviceEngine::get(dev);
+  std::lock_guard<std::mutex> lk(E.mutex());
+  LaunchStats st;
+  const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
+  if (E.run_chain(*D, in, n, semantics, v, (hipStream_t)stream, &st) != hipSuccess) return FST_OOM;
+  t_last_stats = st;
+  return FST_OK;
+}
+
+FstError fst_device_prepare(FstHandle b_handle, int32_t device) {
+  std::shared_ptr<FrozenFst> b;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    b = g_fst.get(b_handle);
+  }
+  if (!b) return FST_INVALID_ARG;
+  if (!gpu_available()) return FST_INVALID_ARG;
+  const int dev = device >= 0 ? device : current_device();
+  return b->device(dev) ? FST_OK : FST_OOM;
+}
+
+FstHandle fst_device_adopt_blob(const void* d_blob, uint64_t len, int32_t device,
+                                const void* host_copy) {
+  if (!d_blob || len < sizeof(Header)) return kInvalid;
+  if (!gpu_available()) return kInvalid;
+  const int dev = device >= 0 ? device : current_device();
+  if (hipSetDevice(dev) != hipSuccess) return kInvalid;
+  std::vector<uint8_t> bytes(len);
+  if (host_copy) std::memcpy(bytes.data(), host_copy, len);
+  else if (hipMemcpy(bytes.data(), d_blob, len, hipMemcpyDeviceToHost) != hipSuccess)
+    return kInvalid;
+  Header h;
+  std::memcpy(&h, bytes.data(), sizeof(h));
+  auto f = FrozenFst::from_bytes(bytes.data(), len, h.weight_type, nullptr);
+  if (!f) return kInvalid;
+  DeviceFst* D = DeviceFst::adopt(d_blob, *f, dev);
+  if (!D) return kInvalid;
+  f->adopt_device(dev, D);
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
+}
+
+FstError fst_last_launch_stats(FstLaunchStats* out) {
+  if (!out) return FST_INVALID_ARG;
+  out->kernel_ms = t_last_stats.kernel_ms;
+  out->launches = t_last_stats.launches;
+  out->engine = t_last_stats.engine;
+  out->grid = t_last_stats.grid;
+  return FST_OK;
+}
+
+// Reference bench rhs generators (bench/optimize-bench.zig:219-306).
+FstHandle fst_bench_transducer(uint32_t kind, uint32_t T, uint32_t B) {
+  MutableFst m;
+  if (kind == 0) {  // buildAmbiguousChainTransducer, :250-277
+    m.add_states(T + 1);
+    m.set_start(0);
+    for (uint32_t i = 0; i <= T; ++i) m.set_final(i, w_one());
+    const uint32_t fan = std::max<uint32_t>(1, std::min<uint32_t>(B, 4));
+    for (uint32_t i = 0; i <= T; ++i) {
+      m.add_arc(i, Arc{1, 1, w_one(), i});
+      for (uint32_t b = 0; b < fan; ++b)
+        m.add_arc(i, Arc{1, ((i + b) % 255) + 1, (double)b, std::min(i + b + 1, T)});
+    }
+  } else if (kind == 1) {  // buildEpsilonDenseTransducer, :219-248
+    m.add_states(T + 1);
+    m.set_start(0);
+    for (uint32_t i = 0; i <= T; ++i) m.set_final(i, w_one());
+    for (uint32_t i = 0; i < T; ++i) {
+      m.add_arc(i, Arc{0, 0, w_one(), i + 1});
+      for (uint32_t b = 0; b < B; ++b)
+        m.add_arc(i, Arc{1, ((i + b) % 255) + 1, (double)b, std::min(i + (b % 4) + 1, T)});
+    }
+  } else if (kind == 2) {  // transducer_for_freeze, :290-306
+    if (T == 0) return kInvalid;
+    m.add_states(T);
+    m.set_start(0);
+    for (uint32_t i = 0; i < T; ++i) {
+      m.set_final(i, w_one());
+      for (uint32_t b = 0; b < B; ++b)
+        m.add_arc(i, Arc{(b % 255) + 1, ((i + b) % 255) + 1, (double)b,
+                         (uint32_t)(((uint64_t)i + b + 1) % T)});
+    }
+  } else {
+    return kInvalid;
+  }
+  auto f = FrozenFst::from_mutable(m, kWeightTropical);
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
+}
+
+}  // extern "C"

@@ -1,0 +1,356 @@
+// device_engine.hip -- device copies of frozen FSTs and the batch engine launches.
+#include "device_engine.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+
+#include "host_fst.hpp"
+#include "kernels/eager_layered.hpp"
+#include "kernels/lazy_wave.hpp"
+
+#define HIP_TRY(x)                              \
+  do {                                          \
+    hipError_t e_ = (x);                        \
+    if (e_ != hipSuccess) return e_;            \
+  } while (0)
+
+namespace fstamd {
+
+// ---------------------------------------------------------------------------------
+// Frozen FST on the device: the blob itself (byte-identical, the HBM-resident
+// Fst(W) layout) plus an SoA mirror derived from it on the device.
+// ---------------------------------------------------------------------------------
+
+__global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t na, uint2* span,
+                                    double* fin, uint32_t* il, ArcRec* rec) {
+  const StateEntry* se = reinterpret_cast<const StateEntry*>(blob + sizeof(Header));
+  const PackedArc* pa =
+      reinterpret_cast<const PackedArc*>(blob + sizeof(Header) + (size_t)ns * sizeof(StateEntry));
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    const StateEntry e = se[i];
+    span[i] = make_uint2(e.arc_offset, e.num_arcs);
+    fin[i] = e.final_weight;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
+    const PackedArc a = pa[i];
+    il[i] = a.ilabel;
+    ArcRec r;
+    r.next = a.nextstate;
+    r.olabel = a.olabel;
+    r.weight = a.weight;
+    rec[i] = r;
+  }
+}
+
+// Eager batch on an rhs no eager engine covers yet: per-string UNSUPPORTED
+// (after the reference's empty / n checks, which need no search).
+__global__ void mark_status_kernel(uint32_t num, uint32_t n_best, uint32_t rhs_start,
+                                   BatchOutDev out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= num) return;
+  int32_t st = kPathUnsupported;
+  if (rhs_start == kNoState || n_best == 0) st = kPathEmpty;
+  else if (n_best != 1) st = kPathErrorN;
+  out.status[i] = st;
+  out.path_len[i] = 0;
+  out.path_off[i] = 0;
+  out.final_w[i] = w_zero();
+  if (out.work) {
+    out.work[2 * i] = 0;
+    out.work[2 * i + 1] = 0;
+  }
+}
+
+static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
+  const Header& h = f.header();
+  const uint32_t ns = h.num_states, na = h.num_arcs;
+  bool ok = hipMalloc(&d->span, sizeof(uint2) * std::max<uint32_t>(ns, 1)) == hipSuccess &&
+            hipMalloc(&d->final_w, sizeof(double) * std::max<uint32_t>(ns, 1)) == hipSuccess &&
+            hipMalloc(&d->il, sizeof(uint32_t) * std::max<uint32_t>(na, 1)) == hipSuccess &&
+            hipMalloc(&d->rec, sizeof(ArcRec) * std::max<uint32_t>(na, 1)) == hipSuccess;
+  if (!ok) {
+    DeviceFst::destroy(d);
+    return nullptr;
+  }
+  const uint32_t work = std::max(ns, na);
+  const uint32_t blocks = std::min<uint32_t>((work + 255) / 256, 4096);
+  if (work > 0) {
+    build_mirror_kernel<<<std::max<uint32_t>(blocks, 1), 256>>>(d->blob, ns, na, d->span,
+                                                                d->final_w, d->il, d->rec);
+  }
+  if (hipDeviceSynchronize() != hipSuccess) {
+    DeviceFst::destroy(d);
+    return nullptr;
+  }
+  uint32_t max_span = 0;
+  const StateEntry* se = f.states();
+  for (uint32_t i = 0; i < ns; ++i) max_span = std::max(max_span, se[i].num_arcs);
+  d->view = RhsView{d->span, d->final_w, d->il, d->rec, ns, na, h.start_state, max_span};
+  d->has_eps = f.has_epsilon_input();
+  d->nonneg = f.weights_nonnegative();
+  d->weight_type = f.weight_type();
+  return d;
+}
+
+DeviceFst* DeviceFst::create(const FrozenFst& f, int dev) {
+  if (hipSetDevice(dev) != hipSuccess) return nullptr;
+  DeviceFst* d = new DeviceFst();
+  d->dev = dev;
+  d->blob_size = f.size();
+  if (hipMalloc(&d->blob, d->blob_size) != hipSuccess ||
+      hipMemcpy(d->blob, f.bytes(), d->blob_size, hipMemcpyHostToDevice) != hipSuccess) {
+    destroy(d);
+    return nullptr;
+  }
+  return finish_device(d, f);
+}
+
+DeviceFst* DeviceFst::adopt(const void* d_blob, const FrozenFst& f, int dev) {
+  if (hipSetDevice(dev) != hipSuccess) return nullptr;
+  DeviceFst* d = new DeviceFst();
+  d->dev = dev;
+  d->blob_size = f.size();
+  if (hipMalloc(&d->blob, d->blob_size) != hipSuccess ||
+      hipMemcpy(d->blob, d_blob, d->blob_size, hipMemcpyDeviceToDevice) != hipSuccess) {
+    destroy(d);
+    return nullptr;
+  }
+  return finish_device(d, f);
+}
+
+void DeviceFst::destroy(DeviceFst* d) {
+  if (!d) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(d->dev);
+  if (d->blob) (void)hipFree(d->blob);
+  if (d->span) (void)hipFree(d->span);
+  if (d->final_w) (void)hipFree(d->final_w);
+  if (d->il) (void)hipFree(d->il);
+  if (d->rec) (void)hipFree(d->rec);
+  (void)hipSetDevice(cur);
+  delete d;
+}
+
+// ---------------------------------------------------------------------------------
+// Engine
+// ---------------------------------------------------------------------------------
+
+namespace {
+// eager-layered geometry: 256 threads (4 waves) per string, <= 512 tuples per layer.
+constexpr int kElWG = 256;
+constexpr int kElFcap = 512;
+constexpr int kElHcap = 1024;
+
+enum Scratch : size_t {
+  kCounter = 0,
+  kElBack,
+  kLzHash,
+  kLzNkey,
+  kLzNdist,
+  kLzNback,
+  kLzNbw,
+  kLzQd,
+  kLzQid,
+  kLzG,
+  kItems,
+  kNumScratch
+};
+
+uint32_t next_pow2(uint64_t x) {
+  uint32_t p = 1;
+  while (p < x && p < 0x80000000u) p <<= 1;
+  return p;
+}
+}  // namespace
+
+DeviceEngine& DeviceEngine::get(int dev) {
+  static std::mutex mu;
+  static std::vector<std::unique_ptr<DeviceEngine>> engines;
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)engines.size() <= dev) engines.resize(dev + 1);
+  if (!engines[dev]) engines[dev].reset(new DeviceEngine(dev));
+  return *engines[dev];
+}
+
+DeviceEngine::DeviceEngine(int dev) : dev_(dev) {
+  (void)hipSetDevice(dev);
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) == hipSuccess) num_cus_ = p.multiProcessorCount;
+  if (num_cus_ <= 0) num_cus_ = 256;
+  bufs_.assign(kNumScratch, nullptr);
+  sizes_.assign(kNumScratch, 0);
+  (void)hipEventCreate(&ev0_);
+  (void)hipEventCreate(&ev1_);
+}
+
+void* DeviceEngine::scratch(size_t idx, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (sizes_[idx] >= bytes) return bufs_[idx];
+  if (bufs_[idx]) (void)hipFree(bufs_[idx]);
+  bufs_[idx] = nullptr;
+  sizes_[idx] = 0;
+  if (hipMalloc(&bufs_[idx], bytes) != hipSuccess) {
+    bufs_[idx] = nullptr;
+    return nullptr;
+  }
+  sizes_[idx] = bytes;
+  return bufs_[idx];
+}
+
+static hipError_t finish_stats(hipEvent_t e0, hipEvent_t e1, LaunchStats* stats) {
+  if (!stats) return hipSuccess;
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  stats->kernel_ms = ms;
+  return hipSuccess;
+}
+
+hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                   int semantics, const BatchOutDev& out, hipStream_t stream,
+                                   LaunchStats* stats) {
+  HIP_TRY(hipSetDevice(dev_));
+  unsigned int* counter = (unsigned int*)scratch(kCounter, 64);
+  if (!counter) return hipErrorOutOfMemory;
+  HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
+  HIP_TRY(hipMemsetAsync(out.cursor, 0, sizeof(unsigned long long), stream));
+  if (in.num_strings == 0) return hipSuccess;
+
+  // Eager semantics on a layered lattice -> eager-layered engine.
+  if (semantics == 1) {
+    if (rhs.has_eps || !rhs.nonneg) {
+      // Not layered (rhs epsilon arcs), or negative weights (Dijkstra on the
+      // lattice is then not the exact SSSP the layered kernel computes).
+      mark_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(in.num_strings, n,
+                                                                           rhs.view.start, out);
+      return hipGetLastError();
+    }
+    const uint64_t back_cap64 = (uint64_t)(in.max_len + 1) * kElFcap;
+    const uint32_t back_cap = (uint32_t)std::min<uint64_t>(back_cap64, 1u << 22);
+    int occ = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, eager_layered_kernel<kElWG, kElFcap, kElHcap>, kElWG, 0));
+    occ = std::max(occ, 1);
+    uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)occ * num_cus_, in.num_strings);
+    // keep the back-pointer slabs within 4 GiB
+    while (grid > 1 && (uint64_t)grid * back_cap * sizeof(uint2) > (4ull << 30)) grid /= 2;
+    uint2* back = (uint2*)scratch(kElBack, (size_t)grid * back_cap * sizeof(uint2));
+    if (!back) return hipErrorOutOfMemory;
+    if (stats) {
+      stats->engine = 0;
+      stats->grid = grid;
+      stats->launches = 1;
+      HIP_TRY(hipEventRecord(ev0_, stream));
+    }
+    const RhsView view = rhs.view;
+    eager_layered_kernel<kElWG, kElFcap, kElHcap>
+        <<<grid, kElWG, 0, stream>>>(view, in, n, counter, back, back_cap, out);
+    HIP_TRY(hipGetLastError());
+    if (stats) {
+      HIP_TRY(hipEventRecord(ev1_, stream));
+      HIP_TRY(finish_stats(ev0_, ev1_, stats));
+    }
+    return hipSuccess;
+  }
+
+  // Lazy semantics -> exact replay, one wavefront per string.
+  LazyWs ws{};
+  const uint64_t want_nodes = std::max<uint64_t>(4096, (uint64_t)256 * (in.max_len + 1));
+  ws.ncap = next_pow2(want_nodes);
+  ws.hcap = ws.ncap * 2;
+  ws.qcap = ws.ncap * 4;
+  ws.gcap = 64;
+  const uint64_t per_wave = (uint64_t)ws.hcap * sizeof(uint4) +
+                            (uint64_t)ws.ncap * (8 + 8 + 16 + 8) +
+                            (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
+  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 16, in.num_strings);
+  while (grid > 1 && (uint64_t)grid * per_wave > (6ull << 30)) grid /= 2;
+  ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
+  ws.nkey = (unsigned long long*)scratch(kLzNkey, (size_t)grid * ws.ncap * 8);
+  ws.ndist = (double*)scratch(kLzNdist, (size_t)grid * ws.ncap * 8);
+  ws.nback = (uint4*)scratch(kLzNback, (size_t)grid * ws.ncap * 16);
+  ws.nbw = (double*)scratch(kLzNbw, (size_t)grid * ws.ncap * 8);
+  ws.qd = (double*)scratch(kLzQd, (size_t)grid * ws.qcap * 8);
+  ws.qid = (uint32_t*)scratch(kLzQid, (size_t)grid * ws.qcap * 4);
+  ws.gscratch = (uint4*)scratch(kLzG, (size_t)grid * ws.gcap * sizeof(uint4));
+  if (!ws.hslot || !ws.nkey || !ws.ndist || !ws.nback || !ws.nbw || !ws.qd || !ws.qid ||
+      !ws.gscratch)
+    return hipErrorOutOfMemory;
+  // Stamps: zero the table whenever it was (re)allocated or the stamp would wrap.
+  if (lazy_hash_bytes_ != (size_t)grid * ws.hcap * sizeof(uint4) ||
+      (uint64_t)lazy_stamp_ + in.num_strings + 2 > 0xFFFFFFF0ull) {
+    HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
+    lazy_hash_bytes_ = (size_t)grid * ws.hcap * sizeof(uint4);
+    lazy_stamp_ = 0;
+  }
+  ws.stamp_base = lazy_stamp_;
+  lazy_stamp_ += in.num_strings + 1;
+  if (stats) {
+    stats->engine = 1;
+    stats->grid = grid;
+    stats->launches = 1;
+    HIP_TRY(hipEventRecord(ev0_, stream));
+  }
+  GraphInput none{};
+  lazy_wave_kernel<false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, counter, nullptr,
+                                                   in.num_strings, ws, out);
+  HIP_TRY(hipGetLastError());
+  if (stats) {
+    HIP_TRY(hipEventRecord(ev1_, stream));
+    HIP_TRY(finish_stats(ev0_, ev1_, stats));
+  }
+  return hipSuccess;
+}
+
+hipError_t DeviceEngine::run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n,
+                                   int semantics, const BatchOutDev& out, hipStream_t stream,
+                                   LaunchStats* stats) {
+  HIP_TRY(hipSetDevice(dev_));
+  if (semantics != 0) return hipErrorInvalidValue;
+  unsigned int* counter = (unsigned int*)scratch(kCounter, 64);
+  if (!counter) return hipErrorOutOfMemory;
+  HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
+  HIP_TRY(hipMemsetAsync(out.cursor, 0, sizeof(unsigned long long), stream));
+  LazyWs ws{};
+  ws.ncap = next_pow2(std::max<uint32_t>(in.ncap, 1024));
+  ws.hcap = ws.ncap * 2;
+  ws.qcap = ws.ncap * 4;
+  ws.gcap = next_pow2(std::max<uint32_t>(64, 2 * in.max_outdeg + 2));
+  const uint32_t grid = 1;
+  ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
+  ws.nkey = (unsigned long long*)scratch(kLzNkey, (size_t)grid * ws.ncap * 8);
+  ws.ndist = (double*)scratch(kLzNdist, (size_t)grid * ws.ncap * 8);
+  ws.nback = (uint4*)scratch(kLzNback, (size_t)grid * ws.ncap * 16);
+  ws.nbw = (double*)scratch(kLzNbw, (size_t)grid * ws.ncap * 8);
+  ws.qd = (double*)scratch(kLzQd, (size_t)grid * ws.qcap * 8);
+  ws.qid = (uint32_t*)scratch(kLzQid, (size_t)grid * ws.qcap * 4);
+  ws.gscratch = (uint4*)scratch(kLzG, (size_t)grid * ws.gcap * sizeof(uint4));
+  if (!ws.hslot || !ws.nkey || !ws.ndist || !ws.nback || !ws.nbw || !ws.qd || !ws.qid ||
+      !ws.gscratch)
+    return hipErrorOutOfMemory;
+  HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
+  lazy_hash_bytes_ = 0;  // force a clear before the next chain launch
+  ws.stamp_base = 0;
+  if (stats) {
+    stats->engine = 1;
+    stats->grid = grid;
+    stats->launches = 1;
+    HIP_TRY(hipEventRecord(ev0_, stream));
+  }
+  ChainInput none{};
+  none.num_strings = 1;
+  lazy_wave_kernel<true><<<grid, 64, 0, stream>>>(rhs.view, none, in, n, counter, nullptr, 1, ws,
+                                                  out);
+  HIP_TRY(hipGetLastError());
+  if (stats) {
+    HIP_TRY(hipEventRecord(ev1_, stream));
+    HIP_TRY(finish_stats(ev0_, ev1_, stats));
+  }
+  return hipSuccess;
+}
+
+}  // namespace fstamd

@@ -1,0 +1,126 @@
+// device_engine.hpp -- device-resident frozen FSTs and the batch engines.
+//
+// Engines:
+//   eager-layered : FST_SEM_EAGER on lattices that are layered by input position
+//                   (rhs without epsilon input arcs, inputs without label 0).
+//                   One workgroup per string, per-layer LDS hash tables; ids,
+//                   distances and back-pointers reproduce compose.zig's BFS ids and
+//                   shortest-path.zig's tie rules.
+//   lazy-wave     : FST_SEM_LAZY, exact replay of composeShortestPath's Dijkstra
+//                   (one wavefront per string, workspace in HBM).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "fst_core.hpp"
+
+namespace fstamd {
+
+class FrozenFst;
+
+// Read-only view of a device-resident rhs (the kernels' only rhs interface).
+struct RhsView {
+  const uint2* span;        // [num_states] (arc_offset, num_arcs)
+  const double* final_w;    // [num_states]
+  const uint32_t* il;       // [num_arcs] sorted ilabels per state span
+  const ArcRec* rec;        // [num_arcs] {nextstate, olabel, weight}
+  uint32_t num_states;
+  uint32_t num_arcs;
+  uint32_t start;
+  uint32_t max_span;        // largest per-state arc count
+};
+
+struct DeviceFst {
+  int dev = 0;
+  uint8_t* blob = nullptr;  // the frozen blob itself, byte-identical to the host copy
+  size_t blob_size = 0;
+  uint2* span = nullptr;
+  double* final_w = nullptr;
+  uint32_t* il = nullptr;
+  ArcRec* rec = nullptr;
+  RhsView view{};
+  bool has_eps = false;
+  bool nonneg = true;
+  uint8_t weight_type = 0;
+
+  static DeviceFst* create(const FrozenFst& f, int dev);
+  // Blob already in device memory on `dev` (e.g. after an RCCL broadcast).
+  static DeviceFst* adopt(const void* d_blob, const FrozenFst& host_view, int dev);
+  static void destroy(DeviceFst* d);
+};
+
+// Device pointers of one batch's outputs (mirrors FstDeviceBatch in fst_batch.h).
+struct BatchOutDev {
+  int32_t* status;
+  uint32_t* path_len;
+  uint64_t* path_off;
+  double* final_w;
+  uint32_t* out_il;
+  uint32_t* out_ol;
+  double* out_w;
+  uint64_t arc_cap;
+  unsigned long long* cursor;
+  uint32_t* work;
+};
+
+// Chain inputs (batch API) or one general lhs FST (single-call C ABI).
+struct ChainInput {
+  const uint32_t* labels;
+  const uint64_t* offsets;
+  uint32_t num_strings;
+  uint32_t max_len;
+};
+struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
+  const uint32_t* state_off;   // [ns + 1]
+  const uint32_t* arc_il;
+  const uint32_t* arc_ol;
+  const double* arc_w;
+  const uint32_t* arc_next;
+  const double* final_w;   // [ns]
+  uint32_t num_states;
+  uint32_t start;
+  uint32_t max_outdeg;     // largest lhs out-degree (sizes the per-pop table)
+  uint32_t ncap;           // product-tuple capacity for this run (power of two)
+};
+
+struct LaunchStats {
+  double kernel_ms = 0;
+  uint32_t launches = 0;
+  uint32_t engine = 0;
+  uint32_t grid = 0;
+};
+
+// Per-device engine state: persistent workspaces (grown on demand) and a lock,
+// since the C ABI may be called from several threads.
+class DeviceEngine {
+ public:
+  static DeviceEngine& get(int dev);
+
+  // All launches are asynchronous on `stream`; stats are filled when `stats` is
+  // non-null (this synchronises on the stream's end event).
+  hipError_t run_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n, int semantics,
+                       const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
+  hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
+                       const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
+
+  int dev() const { return dev_; }
+  std::mutex& mutex() { return mu_; }
+
+ private:
+  explicit DeviceEngine(int dev);
+  void* scratch(size_t idx, size_t bytes);
+  int dev_;
+  int num_cus_ = 0;
+  std::mutex mu_;
+  std::vector<void*> bufs_;
+  std::vector<size_t> sizes_;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  size_t lazy_hash_bytes_ = 0;   // hash table stamps are valid for this allocation
+  uint32_t lazy_stamp_ = 0;      // next stamp base (bumped per launch)
+};
+
+}  // namespace fstamd

@@ -1,0 +1,89 @@
+// device_common.hpp -- device helpers shared by the gfx950 batch kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../device_engine.hpp"
+#include "../fst_core.hpp"
+
+namespace fstamd {
+
+constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;
+constexpr unsigned long long kMaxU64 = ~0ull;
+
+// Fst.arcsByIlabel (src/fst.zig:112-136): global arc range [lo, hi) of the arcs of
+// state `s` whose ilabel == label.  Spans of <= 8 arcs are counted with independent
+// loads (no dependent binary-search chain); longer spans use the two binary searches.
+__device__ __forceinline__ void span_by_ilabel(const RhsView& r, uint32_t s, uint32_t label,
+                                               uint32_t& lo, uint32_t& hi) {
+  const uint2 sp = r.span[s];
+  const uint32_t off = sp.x, n = sp.y;
+  if (n <= 8) {
+    uint32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (uint32_t)i < n ? r.il[off + i] : 0xFFFFFFFFu;
+    uint32_t cl = 0, ch = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool v = (uint32_t)i < n;
+      cl += (v && x[i] < label) ? 1u : 0u;
+      ch += (v && x[i] <= label) ? 1u : 0u;
+    }
+    lo = off + cl;
+    hi = off + ch;
+    return;
+  }
+  uint32_t a = 0, b = n;
+  while (a < b) {
+    const uint32_t m = a + ((b - a) >> 1);
+    if (r.il[off + m] < label) a = m + 1;
+    else b = m;
+  }
+  const uint32_t first = a;
+  b = n;
+  while (a < b) {
+    const uint32_t m = a + ((b - a) >> 1);
+    if (r.il[off + m] <= label) a = m + 1;
+    else b = m;
+  }
+  lo = off + first;
+  hi = off + a;
+}
+
+// Wavefront inclusive prefix sum (64 lanes).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// Workgroup exclusive scan in thread order; `scratch` holds WG/64 words.
+template <int WG>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch,
+                                                    uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(v);
+  if constexpr (WG == 64) {
+    total = __shfl(inc, 63, 64);
+    return inc - v;
+  } else {
+    if (lane == 63) scratch[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < WG / 64; ++i) {
+      const uint32_t t = scratch[i];
+      base += (i < w) ? t : 0u;
+      tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return base + inc - v;
+  }
+}
+
+}  // namespace fstamd

@@ -1,0 +1,679 @@
+// lazy_wave.hpp -- batched composeShortestPath (FST_SEM_LAZY), exact replay.
+//
+// Replaces src/ops/compose-shortest-path.zig:26-401 (and the arcsByIlabel inner
+// loop src/fst.zig:112-136) for many lhs at once: one wavefront per string.
+//
+// The lazy algorithm's answer depends on the id each product tuple receives at
+// FIRST TOUCH (getOrCreate, :70-89) in Dijkstra pop order, so it is replayed
+// exactly rather than re-derived:
+//  * priority queue: a 64-ary min-heap on (dist, id) in HBM; pop = one coalesced
+//    64-child load + a wave argmin per level.  Pop order equals the reference's
+//    binary heap with lazy deletion because (dist, id) is a total order and stale
+//    or settled entries are skipped identically (:159-163).
+//  * one pop's candidates (4 fixed phases, :181-365) are enumerated across lanes in
+//    reference order, 64 at a time; hash lookups run in parallel; NEW tuples get
+//    ids by first occurrence in lane order (ballot + popcount), exactly getOrCreate.
+//  * relaxations that hit the same tuple inside a chunk are folded in lane order
+//    by the group's first lane with the reference rule (:110-128), which is the
+//    sequential result; one push per (pop, tuple) is equivalent to the
+//    reference's push-per-take because earlier entries become stale.
+//  * a candidate that targets the popped tuple itself (self-loop) switches the
+//    chunk to a one-lane sequential path, since it may rewrite dist[curr].
+#pragma once
+
+#include "device_common.hpp"
+
+namespace fstamd {
+
+struct LazyWs {
+  uint4* hslot;                  // [waves * hcap] {key lo, key hi, id, stamp}
+  unsigned long long* nkey;      // [waves * ncap] (s2 << 32) | (s1 << 2) | filter
+  double* ndist;                 // [waves * ncap]
+  uint4* nback;                  // [waves * ncap] {prev, ilabel, olabel, flags}
+  double* nbw;                   // [waves * ncap] back-pointer edge weight
+  double* qd;                    // [waves * qcap] heap dist
+  uint32_t* qid;                 // [waves * qcap] heap id
+  uint4* gscratch;               // [waves * gcap] graph-lhs enumeration table
+  uint32_t hcap, ncap, qcap, gcap;
+  uint32_t stamp_base;
+};
+
+constexpr uint32_t kSettled = 1u;
+constexpr uint32_t kHasBack = 2u;
+
+__device__ __forceinline__ unsigned long long tuple_key(uint32_t s1, uint32_t s2, uint32_t f) {
+  return ((unsigned long long)s2 << 32) | ((unsigned long long)s1 << 2) | f;
+}
+__device__ __forceinline__ uint32_t hmix(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// (dist, id) order of queueCompare (compose-shortest-path.zig:55-61); NaN out of contract.
+__device__ __forceinline__ bool qless(double da, uint32_t ia, double db, uint32_t ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const uint32_t l = lane_id();
+  return l ? (~0ull >> (64 - l)) : 0ull;
+}
+
+// ---- lhs accessors -------------------------------------------------------------
+
+// One linear-chain acceptor of the batch (src/string.zig:24-50 semantics).
+struct ChainLhs {
+  const uint32_t* labels;
+  uint32_t L;
+  __device__ uint32_t start() const { return 0; }
+  __device__ double final_w(uint32_t s1) const { return s1 == L ? w_one() : w_zero(); }
+};
+
+// Per-pop candidate enumeration state, uniform across the wave.
+struct PopCands {
+  uint32_t s1, s2, f;
+  uint32_t n1, n2, n3, n4;   // phase sizes
+  uint32_t lo1, lo3;         // chain: phase-1 span start, rhs-epsilon span start
+  uint32_t label;            // chain: the lhs arc label (if s1 < L)
+  uint32_t deg;              // graph: lhs out-degree of s1
+  uint32_t e_cnt;            // graph: number of epsilon-output lhs arcs
+};
+
+struct Cand {
+  unsigned long long key;
+  uint32_t il, ol;
+  double w;
+};
+
+// Chain: phase sizes in closed form (at most one lhs arc per state).
+__device__ __forceinline__ void prepare_chain(const RhsView& rhs, const ChainLhs& lhs,
+                                              PopCands& P) {
+  const bool has_arc = P.s1 < lhs.L;
+  P.label = has_arc ? lhs.labels[P.s1] : 0u;
+  uint32_t lo3, hi3;
+  span_by_ilabel(rhs, P.s2, kEpsilon, lo3, hi3);
+  P.lo3 = lo3;
+  const uint32_t ne = hi3 - lo3;
+  P.n1 = 0;
+  P.lo1 = 0;
+  if (has_arc && P.label != kEpsilon) {  // :182-224
+    uint32_t lo1, hi1;
+    span_by_ilabel(rhs, P.s2, P.label, lo1, hi1);
+    P.lo1 = lo1;
+    P.n1 = hi1 - lo1;
+  }
+  P.n2 = (has_arc && P.label == kEpsilon && P.f != 1) ? 1u : 0u;       // :227-252
+  P.n3 = (P.f != 2) ? ne : 0u;                                          // :254-305
+  P.n4 = (has_arc && P.label == kEpsilon && P.f == 0) ? ne : 0u;       // :307-365
+}
+
+__device__ __forceinline__ Cand chain_cand(const RhsView& rhs, const PopCands& P, uint32_t c) {
+  Cand x;
+  if (c < P.n1) {
+    const ArcRec r = rhs.rec[P.lo1 + c];
+    x.key = tuple_key(P.s1 + 1, r.next, 0);
+    x.il = P.label;
+    x.ol = r.olabel;
+    x.w = w_times(w_one(), r.weight);
+    return x;
+  }
+  c -= P.n1;
+  if (c < P.n2) {
+    x.key = tuple_key(P.s1 + 1, P.s2, P.f == 0 ? 2u : P.f);
+    x.il = P.label;
+    x.ol = kEpsilon;
+    x.w = w_one();
+    return x;
+  }
+  c -= P.n2;
+  if (c < P.n3) {
+    const ArcRec r = rhs.rec[P.lo3 + c];
+    x.key = tuple_key(P.s1, r.next, P.f == 0 ? 1u : P.f);
+    x.il = kEpsilon;
+    x.ol = r.olabel;
+    x.w = r.weight;
+    return x;
+  }
+  c -= P.n3;
+  const ArcRec r = rhs.rec[P.lo3 + c];
+  x.key = tuple_key(P.s1 + 1, r.next, 0);
+  x.il = P.label;
+  x.ol = r.olabel;
+  x.w = w_times(w_one(), r.weight);
+  return x;
+}
+
+// Graph: per-pop table over the lhs arcs of s1 in gscratch:
+//   tbl[i] = {phase-1 base, phase-1 span lo, phase-1 count, arc index} for i < deg
+//   tbl[deg + e].w = arc index of the e-th epsilon-output lhs arc.
+__device__ void prepare_graph(const RhsView& rhs, const GraphInput& g, uint4* tbl, PopCands& P) {
+  const uint32_t a0 = g.state_off[P.s1];
+  P.deg = g.state_off[P.s1 + 1] - a0;
+  uint32_t base1 = 0, ebase = 0;
+  for (uint32_t i0 = 0; i0 < P.deg; i0 += 64) {
+    const uint32_t i = i0 + lane_id();
+    const bool v = i < P.deg;
+    uint32_t lo = 0, cnt = 0;
+    bool eps_out = false;
+    if (v) {
+      const uint32_t ol = g.arc_ol[a0 + i];
+      eps_out = ol == kEpsilon;
+      if (!eps_out) {
+        uint32_t hi;
+        span_by_ilabel(rhs, P.s2, ol, lo, hi);
+        cnt = hi - lo;
+      }
+    }
+    const uint32_t inc = wave_incl_scan(cnt);
+    const unsigned long long em = __ballot(v && eps_out);
+    const uint32_t erank = __popcll(em & lanemask_lt());
+    if (v) {
+      tbl[i] = make_uint4(base1 + inc - cnt, lo, cnt, a0 + i);
+      if (eps_out) tbl[P.deg + ebase + erank].w = a0 + i;
+    }
+    base1 += __shfl(inc, 63, 64);
+    ebase += __popcll(em);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  uint32_t lo3, hi3;
+  span_by_ilabel(rhs, P.s2, kEpsilon, lo3, hi3);
+  P.lo3 = lo3;
+  const uint32_t ne = hi3 - lo3;
+  P.e_cnt = ebase;
+  P.n1 = base1;
+  P.n2 = (P.f != 1) ? ebase : 0u;
+  P.n3 = (P.f != 2) ? ne : 0u;
+  P.n4 = (P.f == 0) ? ebase * ne : 0u;
+}
+
+__device__ __forceinline__ Cand graph_cand(const RhsView& rhs, const GraphInput& g,
+                                           const uint4* tbl, const PopCands& P, uint32_t c) {
+  Cand x;
+  if (c < P.n1) {  // find the lhs arc whose phase-1 range holds c
+    uint32_t a = 0, b = P.deg;
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (tbl[m].x <= c) a = m;
+      else b = m;
+    }
+    while (tbl[a].z == 0 || c >= tbl[a].x + tbl[a].z) ++a;  // skip empty ranges
+    const uint4 t = tbl[a];
+    const ArcRec r = rhs.rec[t.y + (c - t.x)];
+    x.key = tuple_key(g.arc_next[t.w], r.next, 0);
+    x.il = g.arc_il[t.w];
+    x.ol = r.olabel;
+    x.w = w_times(g.arc_w[t.w], r.weight);
+    return x;
+  }
+  c -= P.n1;
+  if (c < P.n2) {
+    const uint32_t ai = tbl[P.deg + c].w;
+    x.key = tuple_key(g.arc_next[ai], P.s2, P.f == 0 ? 2u : P.f);
+    x.il = g.arc_il[ai];
+    x.ol = kEpsilon;
+    x.w = g.arc_w[ai];
+    return x;
+  }
+  c -= P.n2;
+  if (c < P.n3) {
+    const ArcRec r = rhs.rec[P.lo3 + c];
+    x.key = tuple_key(P.s1, r.next, P.f == 0 ? 1u : P.f);
+    x.il = kEpsilon;
+    x.ol = r.olabel;
+    x.w = r.weight;
+    return x;
+  }
+  c -= P.n3;
+  const uint32_t ne = P.n3 ? P.n3 : (P.n4 / (P.e_cnt ? P.e_cnt : 1));
+  const uint32_t ai = tbl[P.deg + c / ne].w;
+  const ArcRec r = rhs.rec[P.lo3 + c % ne];
+  x.key = tuple_key(g.arc_next[ai], r.next, 0);
+  x.il = g.arc_il[ai];
+  x.ol = r.olabel;
+  x.w = w_times(g.arc_w[ai], r.weight);
+  return x;
+}
+
+// ---- the kernel ----------------------------------------------------------------
+
+struct LazyLds {
+  double nd[64];
+  double w[64];
+  uint32_t il[64];
+  uint32_t ol[64];
+  uint32_t id[64];
+};
+
+template <bool kGraph>
+__global__ void __launch_bounds__(64)
+lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_best,
+                 unsigned int* next_item, const uint32_t* items, uint32_t num_items, LazyWs ws,
+                 BatchOutDev out) {
+  __shared__ LazyLds S;
+  const uint32_t lane = lane_id();
+  const size_t w = blockIdx.x;
+  uint4* hslot = ws.hslot + w * ws.hcap;
+  unsigned long long* nkey = ws.nkey + w * ws.ncap;
+  double* ndist = ws.ndist + w * ws.ncap;
+  uint4* nback = ws.nback + w * ws.ncap;
+  double* nbw = ws.nbw + w * ws.ncap;
+  double* qd = ws.qd + w * ws.qcap;
+  uint32_t* qid = ws.qid + w * ws.qcap;
+  uint4* tbl = ws.gscratch + w * ws.gcap;
+  const uint32_t hmask = ws.hcap - 1;
+
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(next_item, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= num_items) break;
+    const uint32_t si = items ? items[item] : item;
+    const uint32_t stamp = ws.stamp_base + item + 1;
+
+    ChainLhs cl{nullptr, 0};
+    uint32_t start1;
+    if constexpr (kGraph) {
+      start1 = graph.start;
+    } else {
+      const uint64_t off = chain.offsets[si];
+      cl.labels = chain.labels + off;
+      cl.L = (uint32_t)(chain.offsets[si + 1] - off);
+      start1 = 0;
+    }
+    auto lhs_final = [&](uint32_t s1) -> double {
+      if constexpr (kGraph) return graph.final_w[s1];
+      else return cl.final_w(s1);
+    };
+
+    // compose-shortest-path.zig:30-33
+    if (start1 == kNoState || rhs.start == kNoState || n_best == 0 || n_best != 1) {
+      if (lane == 0) {
+        const bool empty = start1 == kNoState || rhs.start == kNoState || n_best == 0;
+        out.status[si] = empty ? kPathEmpty : kPathErrorN;
+        out.path_len[si] = 0;
+        out.path_off[si] = 0;
+        out.final_w[si] = w_zero();
+        if (out.work) {
+          out.work[2 * si] = 0;
+          out.work[2 * si + 1] = 0;
+        }
+      }
+      continue;
+    }
+
+    // init tuple, id 0 (:146-153)
+    uint32_t nn = 1, qn = 1;
+    if (lane == 0) {
+      const unsigned long long k0 = tuple_key(start1, rhs.start, 0);
+      nkey[0] = k0;
+      ndist[0] = w_one();
+      nback[0] = make_uint4(0, 0, 0, 0);
+      uint32_t h = hmix(k0) & hmask;
+      hslot[h] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), 0u, stamp);
+      qd[0] = w_one();
+      qid[0] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+
+    uint32_t best_id = kNoState;
+    double best_fw = w_zero(), best_total = w_zero();
+    uint32_t relax_count = 0;
+    int32_t fail = kPathOk;
+
+    while (qn > 0) {
+      // ---- pop (64-ary heap, wave-cooperative sift-down) ----
+      const double pd = qd[0];
+      const uint32_t pid = qid[0];
+      --qn;
+      if (qn > 0) {
+        const double xd = qd[qn];
+        const uint32_t xi = qid[qn];
+        uint32_t i = 0;
+        for (;;) {
+          const uint32_t c0 = i * 64 + 1;
+          if (c0 >= qn) break;
+          const uint32_t cc = c0 + lane;
+          const bool v = cc < qn;
+          double md = v ? qd[cc] : 0.0;
+          uint32_t mi = v ? qid[cc] : 0u;
+          uint32_t mp = cc;
+          bool mv = v;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(md, o, 64);
+            const uint32_t oi = __shfl_xor(mi, o, 64);
+            const uint32_t op = __shfl_xor(mp, o, 64);
+            const bool ov = __shfl_xor((int)mv, o, 64) != 0;
+            const bool take = ov && (!mv || qless(od, oi, md, mi));
+            if (take) {
+              md = od;
+              mi = oi;
+              mp = op;
+              mv = true;
+            }
+          }
+          // all lanes now hold the minimum child
+          if (qless(md, mi, xd, xi)) {
+            if (lane == 0) {
+              qd[i] = md;
+              qid[i] = mi;
+            }
+            i = mp;
+          } else {
+            break;
+          }
+        }
+        if (lane == 0) {
+          qd[i] = xd;
+          qid[i] = xi;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+
+      // ---- settled / stale (:161-163) ----
+      const uint4 pb = nback[pid];
+      const double pdist = ndist[pid];
+      if (pb.w & kSettled) continue;
+      if (!(pd == pdist)) continue;
+      if (lane == 0) nback[pid].w = pb.w | kSettled;
+      const unsigned long long pk = nkey[pid];
+      PopCands P;
+      P.s1 = (uint32_t)(pk & 0xFFFFFFFFull) >> 2;
+      P.f = (uint32_t)pk & 3u;
+      P.s2 = (uint32_t)(pk >> 32);
+
+      // ---- best final (:165-179) ----
+      const double fw1 = lhs_final(P.s1);
+      const double fw2 = rhs.final_w[P.s2];
+      if (!w_is_zero(fw1) && !w_is_zero(fw2)) {
+        const double fw = w_times(fw1, fw2);
+        const double total = w_times(pdist, fw);
+        if (best_id == kNoState || total < best_total || (total == best_total && pid < best_id)) {
+          best_id = pid;
+          best_fw = fw;
+          best_total = total;
+        }
+      }
+
+      // ---- candidates of the 4 phases in reference order ----
+      if constexpr (kGraph) prepare_graph(rhs, graph, tbl, P);
+      else prepare_chain(rhs, cl, P);
+      const uint32_t C = P.n1 + P.n2 + P.n3 + P.n4;
+      relax_count += C;
+      double cur_dist = pdist;  // dist[curr_id]; changes only through a self-loop
+
+      for (uint32_t cb = 0; cb < C; cb += 64) {
+        const uint32_t c = cb + lane;
+        const bool act = c < C;
+        Cand x{0, 0, 0, 0.0};
+        if (act) {
+          if constexpr (kGraph) x = graph_cand(rhs, graph, tbl, P, c);
+          else x = chain_cand(rhs, P, c);
+        }
+        // lookup (getOrCreate's get)
+        uint32_t tid = kNoState;
+        uint32_t slot = hmix(x.key) & hmask;
+        if (act) {
+          for (uint32_t probe = 0; probe <= hmask; ++probe) {
+            const uint4 s = hslot[slot];
+            if (s.w != stamp) break;
+            if (s.x == (uint32_t)x.key && s.y == (uint32_t)(x.key >> 32)) {
+              tid = s.z;
+              break;
+            }
+            slot = (slot + 1) & hmask;
+          }
+        }
+        // first-occurrence dedup of new tuples in lane order
+        bool need = act && tid == kNoState;
+        uint32_t leader = lane;
+        unsigned long long pending = __ballot(need);
+        while (pending) {
+          const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
+          const unsigned long long lk = __shfl(x.key, (int)l, 64);
+          const bool same = need && x.key == lk;
+          const unsigned long long m = __ballot(same);
+          if (same) leader = l;
+          pending &= ~m;
+        }
+        const bool is_new_leader = need && leader == lane;
+        const unsigned long long nlm = __ballot(is_new_leader);
+        const uint32_t n_new = (uint32_t)__popcll(nlm);
+        if (nn + n_new > ws.ncap || 2 * (nn + n_new) > ws.hcap) {
+          fail = kPathOverflow;
+          break;
+        }
+        if (is_new_leader) {
+          tid = nn + (uint32_t)__popcll(nlm & lanemask_lt());
+          // claim a slot (the table is private to this wave)
+          uint32_t s = slot;
+          for (;;) {
+            const uint32_t old = atomicExch(&hslot[s].w, stamp);
+            if (old != stamp) break;
+            s = (s + 1) & hmask;
+          }
+          hslot[s] = make_uint4((uint32_t)x.key, (uint32_t)(x.key >> 32), tid, stamp);
+          nkey[tid] = x.key;
+          ndist[tid] = w_zero();
+          nback[tid] = make_uint4(0, 0, 0, 0);
+        }
+        const uint32_t lt = __shfl(tid, (int)leader, 64);
+        if (need) tid = lt;
+        nn += n_new;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+
+        // self-loop onto the popped tuple: rare, exact one-lane path
+        const unsigned long long selfm = __ballot(act && tid == pid);
+        if (selfm) {
+          S.id[lane] = tid;
+          S.w[lane] = x.w;
+          S.il[lane] = x.il;
+          S.ol[lane] = x.ol;
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          const uint32_t cnt = C - cb < 64 ? C - cb : 64;
+          if (lane == 0) {
+            for (uint32_t i = 0; i < cnt; ++i) {
+              const uint32_t t = S.id[i];
+              const double nd = w_times(cur_dist, S.w[i]);
+              const double od = ndist[t];
+              uint4 b = nback[t];
+              bool take = w_is_zero(od) || nd < od;
+              if (!take && nd == od) {
+                take = !(b.w & kHasBack) || pid < b.x ||
+                       (pid == b.x && (S.il[i] < b.y || (S.il[i] == b.y && S.ol[i] < b.z)));
+              }
+              if (take) {
+                ndist[t] = nd;
+                nbw[t] = S.w[i];
+                nback[t] = make_uint4(pid, S.il[i], S.ol[i], b.w | kHasBack);
+                if (t == pid) cur_dist = nd;
+                if (!(b.w & kSettled)) {
+                  if (qn >= ws.qcap) {
+                    fail = kPathOverflow;
+                  } else {  // push + sift-up
+                    uint32_t q = qn++;
+                    while (q > 0) {
+                      const uint32_t pq = (q - 1) >> 6;
+                      const double qpd = qd[pq];
+                      const uint32_t qpi = qid[pq];
+                      if (!qless(nd, t, qpd, qpi)) break;
+                      qd[q] = qpd;
+                      qid[q] = qpi;
+                      q = pq;
+                    }
+                    qd[q] = nd;
+                    qid[q] = t;
+                  }
+                }
+              }
+            }
+          }
+          cur_dist = __shfl(cur_dist, 0, 64);
+          qn = __shfl(qn, 0, 64);
+          fail = __shfl(fail, 0, 64);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          if (fail != kPathOk) break;
+          continue;
+        }
+
+        // group by target: the first lane of each group folds its members in lane order
+        const double nd = w_times(cur_dist, x.w);
+        S.nd[lane] = nd;
+        S.w[lane] = x.w;
+        S.il[lane] = x.il;
+        S.ol[lane] = x.ol;
+        S.id[lane] = act ? tid : kNoState;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        unsigned long long gmask = 0;
+        {
+          unsigned long long pend = __ballot(act);
+          while (pend) {
+            const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
+            const uint32_t lt2 = __shfl(tid, (int)l, 64);
+            const bool same = act && tid == lt2;
+            const unsigned long long m = __ballot(same);
+            if (lane == l) gmask = m;
+            pend &= ~m;
+          }
+        }
+        bool push = false;
+        double push_d = 0.0;
+        if (gmask) {  // group leader
+          const uint32_t t = tid;
+          double od = ndist[t];
+          uint4 b = nback[t];
+          double bw = 0.0;
+          bool took = false;
+          unsigned long long m = gmask;
+          while (m) {
+            const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
+            m &= m - 1;
+            const double cnd = S.nd[i];
+            const uint32_t cil = S.il[i], col = S.ol[i];
+            bool take = w_is_zero(od) || cnd < od;
+            if (!take && cnd == od) {
+              take = !(b.w & kHasBack) || pid < b.x ||
+                     (pid == b.x && (cil < b.y || (cil == b.y && col < b.z)));
+            }
+            if (take) {
+              od = cnd;
+              b = make_uint4(pid, cil, col, b.w | kHasBack);
+              bw = S.w[i];
+              took = true;
+            }
+          }
+          if (took) {
+            ndist[t] = od;
+            nback[t] = b;
+            nbw[t] = bw;
+            if (!(b.w & kSettled)) {
+              push = true;
+              push_d = od;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        // pushes in lane order, one lane at a time (sift-up is short in practice)
+        unsigned long long pm = __ballot(push);
+        while (pm) {
+          const uint32_t l = (uint32_t)__ffsll((long long)pm) - 1;
+          pm &= pm - 1;
+          const double xd = __shfl(push_d, (int)l, 64);
+          const uint32_t xi = __shfl(tid, (int)l, 64);
+          if (qn >= ws.qcap) {
+            fail = kPathOverflow;
+            break;
+          }
+          if (lane == 0) {
+            uint32_t q = qn;
+            while (q > 0) {
+              const uint32_t pq = (q - 1) >> 6;
+              const double qpd = qd[pq];
+              const uint32_t qpi = qid[pq];
+              if (!qless(xd, xi, qpd, qpi)) break;
+              qd[q] = qpd;
+              qid[q] = qpi;
+              q = pq;
+            }
+            qd[q] = xd;
+            qid[q] = xi;
+          }
+          ++qn;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (fail != kPathOk) break;
+      }
+      if (fail != kPathOk) break;
+    }
+
+    // ---- result (:368-400) ----
+    if (lane == 0) {
+      int32_t st = fail;
+      uint32_t P = 0;
+      unsigned long long o = 0;
+      double fin = w_zero();
+      if (st == kPathOk) {
+        if (best_id == kNoState) {
+          st = kPathEmpty;
+        } else {
+          uint32_t cur = best_id;
+          bool empty = false;
+          while (cur != 0) {  // init_id == 0
+            const uint4 b = nback[cur];
+            if (!(b.w & kHasBack)) {
+              empty = true;
+              break;
+            }
+            if (++P > nn) {
+              st = kPathCycle;
+              break;
+            }
+            cur = b.x;
+          }
+          if (st == kPathOk && empty) {
+            st = kPathEmpty;
+            P = 0;
+          }
+          if (st == kPathOk) {
+            o = atomicAdd(out.cursor, (unsigned long long)P);
+            if (o + P > out.arc_cap) {
+              st = kPathOutputFull;
+            } else {
+              uint32_t k = P;
+              cur = best_id;
+              while (cur != 0) {
+                const uint4 b = nback[cur];
+                --k;
+                out.out_il[o + k] = b.y;
+                out.out_ol[o + k] = b.z;
+                out.out_w[o + k] = nbw[cur];
+                cur = b.x;
+              }
+              fin = best_fw;
+            }
+          }
+        }
+      }
+      if (st != kPathOk) {
+        P = 0;
+        o = 0;
+        fin = w_zero();
+      }
+      out.status[si] = st;
+      out.path_len[si] = P;
+      out.path_off[si] = o;
+      out.final_w[si] = fin;
+      if (out.work) {
+        out.work[2 * si] = nn;
+        out.work[2 * si + 1] = relax_count;
+      }
+    }
+  }
+}
+
+}  // namespace fstamd
