@@ -41,6 +41,7 @@ typedef enum {
     FST_PATH_OVERFLOW = 4,     /* internal: engine capacity exceeded (retried internally) */
     FST_PATH_UNSUPPORTED = 5,  /* input outside every available engine's contract */
     FST_PATH_OUTPUT_FULL = 6,  /* device arc arena too small */
+    FST_PATH_INTERNAL = 7,     /* engine invariant violated (a bug), reported, never silent */
 } FstPathStatus;
 
 /* Host-memory result of a batch (allocated by the library). */

@@ -157,8 +157,31 @@ enum Scratch : size_t {
   kLzQid,
   kLzG,
   kItems,
+  kDebug,
   kNumScratch
 };
+
+// Lazy-engine watchdog: 60 s of s_memrealtime (100 MHz) per wave, far beyond any
+// legitimate string; it exists so that no bug can leave a wave resident forever.
+constexpr unsigned long long kWatchdogTicks = 6000000000ull;
+
+unsigned long long watchdog_ticks() {
+  const char* e = std::getenv("FSTAMD_WATCHDOG_MS");  // test/debug override
+  if (e && *e) return (unsigned long long)std::strtoull(e, nullptr, 10) * 100000ull;
+  return kWatchdogTicks;
+}
+
+void dump_debug(const uint32_t* d_dbg, uint32_t grid, hipStream_t stream) {
+  std::vector<uint32_t> h((size_t)grid * 8);
+  if (hipStreamSynchronize(stream) != hipSuccess) return;
+  if (hipMemcpy(h.data(), d_dbg, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return;
+  for (uint32_t w = 0; w < grid; ++w)
+    if (h[w * 8])
+      std::fprintf(stderr,
+                   "[fstamd lazy dbg] wave %u: watchdog at site %u pops=%u cb=%u C=%u qn=%u nn=%u\n",
+                   w, h[w * 8], h[w * 8 + 1], h[w * 8 + 2], h[w * 8 + 3], h[w * 8 + 4],
+                   h[w * 8 + 5]);
+}
 
 uint32_t next_pow2(uint64_t x) {
   uint32_t p = 1;
@@ -288,6 +311,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     lazy_stamp_ = 0;
   }
   ws.stamp_base = lazy_stamp_;
+  ws.max_pops = ws.qcap + 1;
   lazy_stamp_ += in.num_strings + 1;
   if (stats) {
     stats->engine = 1;
@@ -296,9 +320,14 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     HIP_TRY(hipEventRecord(ev0_, stream));
   }
   GraphInput none{};
+  ws.wd_ticks = watchdog_ticks();
+  const bool debug = std::getenv("FSTAMD_LAZY_DEBUG") != nullptr;
+  ws.dbg = debug ? (uint32_t*)scratch(kDebug, (size_t)grid * 8 * 4) : nullptr;
+  if (ws.dbg) HIP_TRY(hipMemsetAsync(ws.dbg, 0, (size_t)grid * 8 * 4, stream));
   lazy_wave_kernel<false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, counter, nullptr,
                                                    in.num_strings, ws, out);
   HIP_TRY(hipGetLastError());
+  if (debug) dump_debug(ws.dbg, grid, stream);
   if (stats) {
     HIP_TRY(hipEventRecord(ev1_, stream));
     HIP_TRY(finish_stats(ev0_, ev1_, stats));
@@ -335,6 +364,9 @@ hipError_t DeviceEngine::run_graph(const DeviceFst& rhs, const GraphInput& in, u
   HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
   lazy_hash_bytes_ = 0;  // force a clear before the next chain launch
   ws.stamp_base = 0;
+  ws.max_pops = ws.qcap + 1;
+  ws.wd_ticks = watchdog_ticks();
+  ws.dbg = nullptr;
   if (stats) {
     stats->engine = 1;
     stats->grid = grid;

@@ -104,7 +104,7 @@ enum PathStatus : int32_t {
   kPathOverflow = 4,     // engine capacity exceeded (host retries on a larger engine)
   kPathUnsupported = 5,  // input outside this engine's contract (host reroutes)
   kPathOutputFull = 6,   // output arc arena exhausted
-  kPathPending = 7,      // not processed yet
+  kPathInternal = 7,     // engine invariant violated (a bug); never silently wrong
 };
 
 }  // namespace fstamd

@@ -36,7 +36,16 @@ struct LazyWs {
   uint4* gscratch;               // [waves * gcap] graph-lhs enumeration table
   uint32_t hcap, ncap, qcap, gcap;
   uint32_t stamp_base;
+  uint32_t max_pops;             // hard bound per string: pops <= pushes <= qcap
+  unsigned long long wd_ticks;   // wall-clock watchdog (s_memrealtime, 100 MHz ticks)
+  uint32_t* dbg;                 // optional [waves * 8] diagnostics, may be null
 };
+
+// Every loop of the kernel polls this: no input, bug or corruption can keep a
+// wave resident longer than wd_ticks.
+__device__ __forceinline__ bool wd_expired(unsigned long long t0, unsigned long long lim) {
+  return __builtin_amdgcn_s_memrealtime() - t0 > lim;
+}
 
 constexpr uint32_t kSettled = 1u;
 constexpr uint32_t kHasBack = 2u;
@@ -266,6 +275,22 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
   uint32_t* qid = ws.qid + w * ws.qcap;
   uint4* tbl = ws.gscratch + w * ws.gcap;
   const uint32_t hmask = ws.hcap - 1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool dead = false;  // watchdog fired: drain the remaining items as INTERNAL
+  uint32_t dbg_pops = 0, dbg_cb = 0, dbg_C = 0, dbg_qn = 0, dbg_nn = 0;
+#define LZ_WD(code)                                                                  \
+  if (!dead && wd_expired(t0, ws.wd_ticks)) {                                        \
+    dead = true;                                                                     \
+    if (ws.dbg && lane == 0) {                                                       \
+      uint32_t* d_ = ws.dbg + w * 8;                                                 \
+      d_[0] = (code);                                                                \
+      d_[1] = dbg_pops;                                                              \
+      d_[2] = dbg_cb;                                                                \
+      d_[3] = dbg_C;                                                                 \
+      d_[4] = dbg_qn;                                                                \
+      d_[5] = dbg_nn;                                                                \
+    }                                                                                \
+  }
 
   for (;;) {
     uint32_t item = 0;
@@ -273,6 +298,15 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
     item = __shfl(item, 0, 64);
     if (item >= num_items) break;
     const uint32_t si = items ? items[item] : item;
+    if (dead) {
+      if (lane == 0) {
+        out.status[si] = kPathInternal;
+        out.path_len[si] = 0;
+        out.path_off[si] = 0;
+        out.final_w[si] = w_zero();
+      }
+      continue;
+    }
     const uint32_t stamp = ws.stamp_base + item + 1;
 
     ChainLhs cl{nullptr, 0};
@@ -325,7 +359,16 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
     uint32_t relax_count = 0;
     int32_t fail = kPathOk;
 
+    uint32_t pops = 0, pushes = 1;
     while (qn > 0) {
+      dbg_pops = pops;
+      dbg_qn = qn;
+      dbg_nn = nn;
+      LZ_WD(1);
+      if (dead || ++pops > ws.max_pops) {  // a heap yields only as many items as were pushed
+        fail = kPathInternal;
+        break;
+      }
       // ---- pop (64-ary heap, wave-cooperative sift-down) ----
       const double pd = qd[0];
       const uint32_t pid = qid[0];
@@ -337,6 +380,8 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         for (;;) {
           const uint32_t c0 = i * 64 + 1;
           if (c0 >= qn) break;
+          LZ_WD(2);
+          if (dead) break;
           const uint32_t cc = c0 + lane;
           const bool v = cc < qn;
           double md = v ? qd[cc] : 0.0;
@@ -349,7 +394,10 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             const uint32_t oi = __shfl_xor(mi, o, 64);
             const uint32_t op = __shfl_xor(mp, o, 64);
             const bool ov = __shfl_xor((int)mv, o, 64) != 0;
-            const bool take = ov && (!mv || qless(od, oi, md, mi));
+            // duplicates of one (dist, id) exist (equal-dist tie takes push again):
+            // break ties by heap position so every lane agrees on the winner
+            const bool take =
+                ov && (!mv || qless(od, oi, md, mi) || (od == md && oi == mi && op < mp));
             if (take) {
               md = od;
               mi = oi;
@@ -375,6 +423,10 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 
+      if (pid >= nn) {  // cannot happen on a consistent heap; never spin on garbage
+        fail = kPathInternal;
+        break;
+      }
       // ---- settled / stale (:161-163) ----
       const uint4 pb = nback[pid];
       const double pdist = ndist[pid];
@@ -386,6 +438,10 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       P.s1 = (uint32_t)(pk & 0xFFFFFFFFull) >> 2;
       P.f = (uint32_t)pk & 3u;
       P.s2 = (uint32_t)(pk >> 32);
+      if (P.s2 >= rhs.num_states) {  // invariant guard (see pid check above)
+        fail = kPathInternal;
+        break;
+      }
 
       // ---- best final (:165-179) ----
       const double fw1 = lhs_final(P.s1);
@@ -407,7 +463,14 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       relax_count += C;
       double cur_dist = pdist;  // dist[curr_id]; changes only through a self-loop
 
+      dbg_C = C;
       for (uint32_t cb = 0; cb < C; cb += 64) {
+        dbg_cb = cb;
+        LZ_WD(3);
+        if (dead) {
+          fail = kPathInternal;
+          break;
+        }
         const uint32_t c = cb + lane;
         const bool act = c < C;
         Cand x{0, 0, 0, 0.0};
@@ -434,12 +497,18 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         uint32_t leader = lane;
         unsigned long long pending = __ballot(need);
         while (pending) {
+          LZ_WD(4);
+          if (dead) break;
           const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
           const unsigned long long lk = __shfl(x.key, (int)l, 64);
           const bool same = need && x.key == lk;
           const unsigned long long m = __ballot(same);
           if (same) leader = l;
           pending &= ~m;
+        }
+        if (dead) {
+          fail = kPathInternal;
+          break;
         }
         const bool is_new_leader = need && leader == lane;
         const unsigned long long nlm = __ballot(is_new_leader);
@@ -452,7 +521,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           tid = nn + (uint32_t)__popcll(nlm & lanemask_lt());
           // claim a slot (the table is private to this wave)
           uint32_t s = slot;
-          for (;;) {
+          for (uint32_t probe = 0; probe <= hmask; ++probe) {  // load <= 1/2: always ends
             const uint32_t old = atomicExch(&hslot[s].w, stamp);
             if (old != stamp) break;
             s = (s + 1) & hmask;
@@ -497,6 +566,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
                     fail = kPathOverflow;
                   } else {  // push + sift-up
                     uint32_t q = qn++;
+                    ++pushes;
                     while (q > 0) {
                       const uint32_t pq = (q - 1) >> 6;
                       const double qpd = qd[pq];
@@ -533,6 +603,8 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         {
           unsigned long long pend = __ballot(act);
           while (pend) {
+            LZ_WD(5);
+            if (dead) break;
             const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
             const uint32_t lt2 = __shfl(tid, (int)l, 64);
             const bool same = act && tid == lt2;
@@ -540,6 +612,10 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             if (lane == l) gmask = m;
             pend &= ~m;
           }
+        }
+        if (dead) {
+          fail = kPathInternal;
+          break;
         }
         bool push = false;
         double push_d = 0.0;
@@ -581,6 +657,11 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         // pushes in lane order, one lane at a time (sift-up is short in practice)
         unsigned long long pm = __ballot(push);
         while (pm) {
+          LZ_WD(6);
+          if (dead) {
+            fail = kPathInternal;
+            break;
+          }
           const uint32_t l = (uint32_t)__ffsll((long long)pm) - 1;
           pm &= pm - 1;
           const double xd = __shfl(push_d, (int)l, 64);
@@ -604,6 +685,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             qid[q] = xi;
           }
           ++qn;
+          ++pushes;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         if (fail != kPathOk) break;
@@ -665,8 +747,8 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         fin = w_zero();
       }
       out.status[si] = st;
-      out.path_len[si] = P;
-      out.path_off[si] = o;
+      out.path_len[si] = st == kPathInternal ? pops : P;  // diagnostics on a bug path
+      out.path_off[si] = st == kPathInternal ? pushes : o;
       out.final_w[si] = fin;
       if (out.work) {
         out.work[2 * si] = nn;
@@ -675,5 +757,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
     }
   }
 }
+#undef LZ_WD
 
 }  // namespace fstamd

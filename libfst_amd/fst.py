@@ -25,7 +25,7 @@ FST_INVALID_HANDLE = 0xFFFFFFFFFFFFFFFF
 FST_OK, FST_OOM, FST_INVALID_ARG, FST_INVALID_STATE, FST_IO_ERROR = range(5)
 FST_SEM_LAZY, FST_SEM_EAGER = 0, 1
 (FST_PATH_OK, FST_PATH_EMPTY, FST_PATH_ERROR_N, FST_PATH_CYCLE, FST_PATH_OVERFLOW,
- FST_PATH_UNSUPPORTED, FST_PATH_OUTPUT_FULL) = range(7)
+ FST_PATH_UNSUPPORTED, FST_PATH_OUTPUT_FULL, FST_PATH_INTERNAL) = range(8)
 
 BENCH_AMBIGUOUS, BENCH_EPS_DENSE, BENCH_BRANCHING = 0, 1, 2
 
