@@ -158,6 +158,8 @@ enum Scratch : size_t {
   kLzG,
   kItems,
   kDebug,
+  kElSlab,
+  kElBack2,
   kNumScratch
 };
 
@@ -252,27 +254,57 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                                                                            rhs.view.start, out);
       return hipGetLastError();
     }
+    // Tier 1: LDS tables, layers of <= kElFcap tuples (the metric's layers have <= 257).
     const uint64_t back_cap64 = (uint64_t)(in.max_len + 1) * kElFcap;
     const uint32_t back_cap = (uint32_t)std::min<uint64_t>(back_cap64, 1u << 22);
+    auto k1 = eager_layered_kernel<kElWG, kElFcap, kElHcap, true>;
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, eager_layered_kernel<kElWG, kElFcap, kElHcap>, kElWG, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k1, kElWG, 0));
     occ = std::max(occ, 1);
     uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)occ * num_cus_, in.num_strings);
-    // keep the back-pointer slabs within 4 GiB
     while (grid > 1 && (uint64_t)grid * back_cap * sizeof(uint2) > (4ull << 30)) grid /= 2;
     uint2* back = (uint2*)scratch(kElBack, (size_t)grid * back_cap * sizeof(uint2));
     if (!back) return hipErrorOutOfMemory;
+
+    // Tier 2 (HBM tables) takes the strings tier 1 reports as OVERFLOW.  A layer of a
+    // layered lattice holds at most one tuple per rhs state, so fcap = num_states can
+    // only overflow the back-pointer slab.  Skipped when tier 1 cannot overflow.
+    const bool may_overflow =
+        (uint64_t)rhs.view.num_states > (uint64_t)kElFcap || back_cap64 > back_cap;
+    uint32_t* list = nullptr;
+    uint32_t* count = counter + 2;
+    uint32_t grid2 = 0, fcap2 = 0, hcap2 = 0, back_cap2 = 0;
+    uint8_t* slab = nullptr;
+    uint2* back2 = nullptr;
+    if (may_overflow) {
+      list = (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4);
+      fcap2 = std::max<uint32_t>(rhs.view.num_states, 1);
+      hcap2 = next_pow2(2ull * fcap2);
+      back_cap2 = (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * fcap2, 1u << 28);
+      const uint64_t per_wg = layer_slab_bytes(fcap2, hcap2) + (uint64_t)back_cap2 * 8;
+      grid2 = (uint32_t)std::min<uint64_t>(num_cus_, std::max<uint64_t>(1, (8ull << 30) / per_wg));
+      slab = (uint8_t*)scratch(kElSlab, (size_t)grid2 * layer_slab_bytes(fcap2, hcap2));
+      back2 = (uint2*)scratch(kElBack2, (size_t)grid2 * back_cap2 * sizeof(uint2));
+      if (!list || !slab || !back2) return hipErrorOutOfMemory;
+    }
     if (stats) {
       stats->engine = 0;
       stats->grid = grid;
-      stats->launches = 1;
+      stats->launches = may_overflow ? 3 : 1;
       HIP_TRY(hipEventRecord(ev0_, stream));
     }
-    const RhsView view = rhs.view;
-    eager_layered_kernel<kElWG, kElFcap, kElHcap>
-        <<<grid, kElWG, 0, stream>>>(view, in, n, counter, back, back_cap, out);
+    EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back, back_cap,
+                   watchdog_ticks()};
+    k1<<<grid, kElWG, 0, stream>>>(rhs.view, in, n, counter, lp, out);
     HIP_TRY(hipGetLastError());
+    if (may_overflow) {
+      collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
+          out.status, in.num_strings, kPathOverflow, list, count);
+      EagerLaunch lp2{list, count, 0, slab, fcap2, hcap2, back2, back_cap2, watchdog_ticks()};
+      eager_layered_kernel<kElWG, kElFcap, kElHcap, false>
+          <<<grid2, kElWG, 0, stream>>>(rhs.view, in, n, counter + 1, lp2, out);
+      HIP_TRY(hipGetLastError());
+    }
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));

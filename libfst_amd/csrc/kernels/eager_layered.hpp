@@ -23,109 +23,202 @@
 //  * Best final (shortest-path.zig:88-104): lexmin (total, id) over finite nodes.
 //
 // Layout: one workgroup owns one string at a time (persistent, atomic work
-// counter).  The current layer (s2, dist) and the next layer's open-addressing
-// hash table live in LDS; back-pointers of every layer go to a per-workgroup
-// HBM slab that the final backtrace walks.
+// counter).  The current layer (s2, dist, span) and the next layer's open-
+// addressing hash table live either in LDS (fast tier, <= FCAP tuples per layer)
+// or in a per-workgroup HBM slab (overflow tier, capacity chosen at launch).
+// Back-pointers of every layer go to a per-workgroup HBM slab that the final
+// backtrace walks.
 #pragma once
 
 #include "device_common.hpp"
 
 namespace fstamd {
 
-template <int WG, int FCAP, int HCAP>
-struct LayeredLds {
+// Pointers to one workgroup's layer tables (LDS or HBM).
+struct LayerTables {
+  uint32_t* s2[2];
+  double* d[2];
+  uint32_t* lo;                  // current layer: first matching rhs arc
+  uint32_t* cnt;                 // current layer: number of matching rhs arcs
+  uint32_t* h_key;               // next layer hash: rhs state (kEmptyKey = free)
+  uint32_t* h_first;             // first candidate index that reached the key, then
+                                 // 0x80000000 | rank of the tuple in the next layer
+  unsigned long long* h_dmin;    // minimum distance (order-preserving bits)
+  uint32_t* h_bmin;              // minimum tight candidate index (back-pointer)
+  uint32_t* nslot;               // next layer rank -> slot
+  uint32_t fcap, hcap, hbits;
+};
+
+template <int FCAP, int HCAP>
+struct LayerLds {
   uint32_t s2[2][FCAP];
   double d[2][FCAP];
+  uint32_t lo[FCAP];
+  uint32_t cnt[FCAP];
   uint32_t h_key[HCAP];
   uint32_t h_first[HCAP];
   unsigned long long h_dmin[HCAP];
   uint32_t h_bmin[HCAP];
-  uint32_t h_pos[HCAP];
   uint32_t nslot[FCAP];
-  uint32_t scan[WG / 64];
-  uint32_t str;
+};
+
+// Bytes of one workgroup's HBM table slab for the overflow tier.
+__host__ __device__ inline size_t layer_slab_bytes(uint32_t fcap, uint32_t hcap) {
+  return (size_t)fcap * (2 * 4 + 2 * 8 + 4 + 4 + 4) + (size_t)hcap * (4 + 4 + 8 + 4) + 256;
+}
+
+__device__ inline LayerTables carve_slab(uint8_t* base, uint32_t fcap, uint32_t hcap) {
+  LayerTables t;
+  uint8_t* p = base;
+  auto take = [&](size_t bytes) {
+    uint8_t* r = p;
+    p += (bytes + 15) & ~(size_t)15;
+    return r;
+  };
+  t.d[0] = (double*)take((size_t)fcap * 8);
+  t.d[1] = (double*)take((size_t)fcap * 8);
+  t.h_dmin = (unsigned long long*)take((size_t)hcap * 8);
+  t.s2[0] = (uint32_t*)take((size_t)fcap * 4);
+  t.s2[1] = (uint32_t*)take((size_t)fcap * 4);
+  t.lo = (uint32_t*)take((size_t)fcap * 4);
+  t.cnt = (uint32_t*)take((size_t)fcap * 4);
+  t.nslot = (uint32_t*)take((size_t)fcap * 4);
+  t.h_key = (uint32_t*)take((size_t)hcap * 4);
+  t.h_first = (uint32_t*)take((size_t)hcap * 4);
+  t.h_bmin = (uint32_t*)take((size_t)hcap * 4);
+  t.fcap = fcap;
+  t.hcap = hcap;
+  t.hbits = __builtin_ctz(hcap);
+  return t;
+}
+
+__device__ __forceinline__ uint32_t lhash(uint32_t k, uint32_t hbits) {
+  return (k * 2654435761u) >> (32 - hbits);
+}
+
+// Insert-or-find `k`; returns the slot or kEmptyKey if the probe bound is hit.
+__device__ __forceinline__ uint32_t tbl_insert(const LayerTables& T, uint32_t k, bool& created) {
+  uint32_t i = lhash(k, T.hbits);
+  created = false;
+  for (uint32_t probe = 0; probe < T.hcap; ++probe) {
+    const uint32_t old = atomicCAS(&T.h_key[i], kEmptyKey, k);
+    if (old == kEmptyKey) {
+      created = true;
+      return i;
+    }
+    if (old == k) return i;
+    i = (i + 1) & (T.hcap - 1);
+  }
+  return kEmptyKey;
+}
+
+__device__ __forceinline__ uint32_t tbl_find(const LayerTables& T, uint32_t k) {
+  uint32_t i = lhash(k, T.hbits);
+  for (uint32_t probe = 0; probe < T.hcap; ++probe) {
+    if (T.h_key[i] == k) return i;
+    i = (i + 1) & (T.hcap - 1);
+  }
+  return kEmptyKey;
+}
+
+__device__ __forceinline__ void tbl_clear_slot(const LayerTables& T, uint32_t s) {
+  T.h_key[s] = kEmptyKey;
+  T.h_first[s] = kEmptyKey;
+  T.h_dmin[s] = kMaxU64;
+  T.h_bmin[s] = kEmptyKey;
+}
+
+struct LayerShared {
+  uint32_t scan[16];
+  uint32_t item;
   uint32_t nnext;
   uint32_t flag;
   uint32_t bestp;
   unsigned long long best;
 };
 
-template <int HCAP>
-__device__ __forceinline__ uint32_t lhash(uint32_t k) {
-  constexpr int bits = __builtin_ctz(HCAP);
-  return (k * 2654435761u) >> (32 - bits);
-}
+struct EagerLaunch {
+  const uint32_t* items;         // null: item i is string i
+  const uint32_t* num_items_dev; // null: use num_items
+  uint32_t num_items;
+  uint8_t* slab;                 // HBM tier tables (null for the LDS tier)
+  uint32_t fcap, hcap;           // HBM tier capacities
+  uint2* back_ws;                // [grid * back_cap] {source id, rhs arc}
+  uint32_t back_cap;
+  unsigned long long wd_ticks;   // wall-clock watchdog (s_memrealtime ticks)
+};
 
-// Insert-or-find `k`; returns the slot or kEmptyKey if the probe bound is hit.
-template <int HCAP>
-__device__ __forceinline__ uint32_t lds_insert(uint32_t* keys, uint32_t k, bool& created) {
-  uint32_t i = lhash<HCAP>(k);
-  created = false;
-  for (int probe = 0; probe < HCAP; ++probe) {
-    const uint32_t old = atomicCAS(&keys[i], kEmptyKey, k);
-    if (old == kEmptyKey) {
-      created = true;
-      return i;
-    }
-    if (old == k) return i;
-    i = (i + 1) & (HCAP - 1);
+__device__ __forceinline__ void write_status(const BatchOutDev& out, uint32_t si, int32_t st,
+                                             uint32_t tuples, uint32_t relax) {
+  out.status[si] = st;
+  out.path_len[si] = 0;
+  out.path_off[si] = 0;
+  out.final_w[si] = w_zero();
+  if (out.work) {
+    out.work[2 * si] = tuples;
+    out.work[2 * si + 1] = relax;
   }
-  return kEmptyKey;
 }
 
-template <int HCAP>
-__device__ __forceinline__ uint32_t lds_find(const uint32_t* keys, uint32_t k) {
-  uint32_t i = lhash<HCAP>(k);
-  for (int probe = 0; probe < HCAP; ++probe) {
-    if (keys[i] == k) return i;
-    i = (i + 1) & (HCAP - 1);
-  }
-  return kEmptyKey;
-}
-
-template <int WG, int FCAP, int HCAP>
+template <int WG, int FCAP, int HCAP, bool kLds>
 __global__ void __launch_bounds__(WG)
-eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_string,
-                     uint2* back_ws, uint32_t back_cap, BatchOutDev out) {
-  constexpr int EMAX = (FCAP + WG - 1) / WG;
-  __shared__ LayeredLds<WG, FCAP, HCAP> S;
-  const uint32_t tid = threadIdx.x;
-  uint2* back = back_ws + (size_t)blockIdx.x * back_cap;
-
-  for (uint32_t i = tid; i < HCAP; i += WG) {
-    S.h_key[i] = kEmptyKey;
-    S.h_first[i] = kEmptyKey;
-    S.h_dmin[i] = kMaxU64;
-    S.h_bmin[i] = kEmptyKey;
+eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
+                     EagerLaunch lp, BatchOutDev out) {
+  __shared__ LayerShared SH;
+  LayerTables T;
+  if constexpr (kLds) {
+    __shared__ LayerLds<FCAP, HCAP> L;
+    T.s2[0] = L.s2[0];
+    T.s2[1] = L.s2[1];
+    T.d[0] = L.d[0];
+    T.d[1] = L.d[1];
+    T.lo = L.lo;
+    T.cnt = L.cnt;
+    T.h_key = L.h_key;
+    T.h_first = L.h_first;
+    T.h_dmin = L.h_dmin;
+    T.h_bmin = L.h_bmin;
+    T.nslot = L.nslot;
+    T.fcap = FCAP;
+    T.hcap = HCAP;
+    T.hbits = __builtin_ctz(HCAP);
+  } else {
+    T = carve_slab(lp.slab + (size_t)blockIdx.x * layer_slab_bytes(lp.fcap, lp.hcap), lp.fcap,
+                   lp.hcap);
   }
+  const uint32_t tid = threadIdx.x;
+  uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
+  const uint32_t num_items = lp.num_items_dev ? *lp.num_items_dev : lp.num_items;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+  for (uint32_t i = tid; i < T.hcap; i += WG) tbl_clear_slot(T, i);
 
   for (;;) {
     __syncthreads();
-    if (tid == 0) S.str = atomicAdd(next_string, 1u);
+    if (tid == 0) SH.item = atomicAdd(next_item, 1u);
     __syncthreads();
-    const uint32_t si = S.str;
-    if (si >= in.num_strings) break;
+    const uint32_t item = SH.item;
+    if (item >= num_items) break;
+    const uint32_t si = lp.items ? lp.items[item] : item;
     const uint64_t off = in.offsets[si];
     const uint32_t L = (uint32_t)(in.offsets[si + 1] - off);
 
     // compose.zig:33-35 / shortest-path.zig:21-24 (n checked after the empty checks)
-    if (rhs.start == kNoState || n_best == 0 || n_best != 1) {
-      if (tid == 0) {
-        out.status[si] = (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN;
-        out.path_len[si] = 0;
-        out.path_off[si] = 0;
-        out.final_w[si] = w_zero();
-        if (out.work) {
-          out.work[2 * si] = 0;
-          out.work[2 * si + 1] = 0;
-        }
-      }
+    if (rhs.start == kNoState || n_best != 1) {
+      if (tid == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+    // Watchdog: no bug may keep a workgroup resident forever (status INTERNAL).
+    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+      if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
       continue;
     }
 
     if (tid == 0) {
-      S.s2[0][0] = rhs.start;
-      S.d[0][0] = w_one();
+      T.s2[0][0] = rhs.start;
+      T.d[0][0] = w_one();
     }
     uint32_t cur = 0, n_cur = 1, cur_base = 0;
     uint32_t tuples = 1, relax = 0;
@@ -138,56 +231,50 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
         fail = kPathUnsupported;
         break;
       }
-      // ---- (A) spans of this thread's contiguous chunk of the layer ----
+      // Each thread owns a contiguous chunk of the layer: candidate order, i.e.
+      // (source id, arc index), equals thread order then chunk order.
       const uint32_t E = (n_cur + WG - 1) / WG;
-      const uint32_t p0 = tid * E;
-      uint32_t lo[EMAX], cnt[EMAX];
-      double dd[EMAX];
+      const uint32_t p0 = min(tid * E, n_cur), p1 = min(p0 + E, n_cur);
+
+      // ---- (A) rhs spans (arcsByIlabel) of the chunk ----
       uint32_t tsum = 0;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        lo[e] = 0;
-        cnt[e] = 0;
-        dd[e] = 0.0;
-        const uint32_t p = p0 + e;
-        if ((uint32_t)e < E && p < n_cur) {
-          uint32_t a, b;
-          span_by_ilabel(rhs, S.s2[cur][p], label, a, b);
-          lo[e] = a;
-          cnt[e] = b - a;
-          dd[e] = S.d[cur][p];
-          tsum += b - a;
-        }
+      for (uint32_t p = p0; p < p1; ++p) {
+        uint32_t a, b;
+        span_by_ilabel(rhs, T.s2[cur][p], label, a, b);
+        T.lo[p] = a;
+        T.cnt[p] = b - a;
+        tsum += b - a;
       }
       if (tid == 0) {
-        S.nnext = 0;
-        S.flag = 0;
+        SH.nnext = 0;
+        SH.flag = 0;
       }
       uint32_t ctot;
-      const uint32_t cbase = block_excl_scan<WG>(tsum, S.scan, ctot);
+      const uint32_t cbase = block_excl_scan<WG>(tsum, SH.scan, ctot);
       relax += ctot;
 
       // ---- (B) dedup targets, first occurrence, minimum distance ----
       uint32_t c = cbase;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        for (uint32_t j = 0; j < cnt[e]; ++j, ++c) {
-          const ArcRec r = rhs.rec[lo[e] + j];
-          const double nd = w_times(dd[e], w_times(w_one(), r.weight));
+      for (uint32_t p = p0; p < p1; ++p) {
+        const double dp = T.d[cur][p];
+        const uint32_t a0 = T.lo[p], n = T.cnt[p];
+        for (uint32_t j = 0; j < n; ++j, ++c) {
+          const ArcRec r = rhs.rec[a0 + j];
+          const double nd = w_times(dp, w_times(w_one(), r.weight));  // compose.zig:104
           bool created;
-          const uint32_t slot = lds_insert<HCAP>(S.h_key, r.next, created);
+          const uint32_t slot = tbl_insert(T, r.next, created);
           if (slot == kEmptyKey) {
-            S.flag = 1;
+            SH.flag = 1;
             continue;
           }
-          if (created && atomicAdd(&S.nnext, 1u) >= (uint32_t)FCAP) S.flag = 1;
-          atomicMin(&S.h_first[slot], c);
-          atomicMin(&S.h_dmin[slot], (unsigned long long)okey(nd));
+          if (created && atomicAdd(&SH.nnext, 1u) >= T.fcap) SH.flag = 1;
+          atomicMin(&T.h_first[slot], c);
+          atomicMin(&T.h_dmin[slot], (unsigned long long)okey(nd));
         }
       }
       __syncthreads();
-      const uint32_t n_next = S.nnext;
-      if (S.flag || (uint64_t)cur_base + n_cur + n_next > back_cap) {
+      const uint32_t n_next = SH.nnext;
+      if (SH.flag || (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
         fail = kPathOverflow;
         break;
       }
@@ -199,31 +286,34 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       // ---- (C) tight candidates -> back-pointer; count first occurrences ----
       uint32_t nf = 0;
       c = cbase;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        for (uint32_t j = 0; j < cnt[e]; ++j, ++c) {
-          const ArcRec r = rhs.rec[lo[e] + j];
-          const double nd = w_times(dd[e], w_times(w_one(), r.weight));
-          const uint32_t slot = lds_find<HCAP>(S.h_key, r.next);
-          if (okey(nd) == S.h_dmin[slot]) atomicMin(&S.h_bmin[slot], c);
-          if (S.h_first[slot] == c) ++nf;
+      for (uint32_t p = p0; p < p1; ++p) {
+        const double dp = T.d[cur][p];
+        const uint32_t a0 = T.lo[p], n = T.cnt[p];
+        for (uint32_t j = 0; j < n; ++j, ++c) {
+          const ArcRec r = rhs.rec[a0 + j];
+          const double nd = w_times(dp, w_times(w_one(), r.weight));
+          const uint32_t slot = tbl_find(T, r.next);
+          if (okey(nd) == T.h_dmin[slot]) atomicMin(&T.h_bmin[slot], c);
+          if (T.h_first[slot] == c) ++nf;
         }
       }
       uint32_t nftot;
-      uint32_t rank = block_excl_scan<WG>(nf, S.scan, nftot);
+      uint32_t rank = block_excl_scan<WG>(nf, SH.scan, nftot);
 
       // ---- (D) ids of the next layer in first-occurrence order ----
       const uint32_t nxt = cur ^ 1;
       c = cbase;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        for (uint32_t j = 0; j < cnt[e]; ++j, ++c) {
-          const uint32_t t = rhs.rec[lo[e] + j].next;
-          const uint32_t slot = lds_find<HCAP>(S.h_key, t);
-          if (S.h_first[slot] == c) {
-            S.h_pos[slot] = rank;
-            S.nslot[rank] = slot;
-            S.s2[nxt][rank] = t;
+      for (uint32_t p = p0; p < p1; ++p) {
+        const uint32_t a0 = T.lo[p], n = T.cnt[p];
+        for (uint32_t j = 0; j < n; ++j, ++c) {
+          const uint32_t t = rhs.rec[a0 + j].next;
+          const uint32_t slot = tbl_find(T, t);
+          if (T.h_first[slot] == c) {
+            // the slot's rank replaces its first-candidate index (tag bit 31: candidate
+            // indices are < 2^31, so no other candidate can match it any more)
+            T.h_first[slot] = 0x80000000u | rank;
+            T.nslot[rank] = slot;
+            T.s2[nxt][rank] = t;
             ++rank;
           }
         }
@@ -233,25 +323,22 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       // ---- (E) back-pointer records of the next layer ----
       const uint32_t next_base = cur_base + n_cur;
       c = cbase;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        for (uint32_t j = 0; j < cnt[e]; ++j, ++c) {
-          const uint32_t t = rhs.rec[lo[e] + j].next;
-          const uint32_t slot = lds_find<HCAP>(S.h_key, t);
-          if (S.h_bmin[slot] == c)
-            back[next_base + S.h_pos[slot]] = make_uint2(cur_base + p0 + e, lo[e] + j);
+      for (uint32_t p = p0; p < p1; ++p) {
+        const uint32_t a0 = T.lo[p], n = T.cnt[p];
+        for (uint32_t j = 0; j < n; ++j, ++c) {
+          const uint32_t t = rhs.rec[a0 + j].next;
+          const uint32_t slot = tbl_find(T, t);
+          if (T.h_bmin[slot] == c)
+            back[next_base + (T.h_first[slot] & 0x7FFFFFFFu)] = make_uint2(cur_base + p, a0 + j);
         }
       }
       __syncthreads();
 
       // ---- (F) next-layer distances, clear the used slots ----
       for (uint32_t r = tid; r < n_next; r += WG) {
-        const uint32_t slot = S.nslot[r];
-        S.d[nxt][r] = from_okey(S.h_dmin[slot]);
-        S.h_key[slot] = kEmptyKey;
-        S.h_first[slot] = kEmptyKey;
-        S.h_dmin[slot] = kMaxU64;
-        S.h_bmin[slot] = kEmptyKey;
+        const uint32_t slot = T.nslot[r];
+        T.d[nxt][r] = from_okey(T.h_dmin[slot]);
+        tbl_clear_slot(T, slot);
       }
       __syncthreads();
       cur = nxt;
@@ -263,67 +350,45 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     if (fail != kPathOk) {
       // Leave the tables clean for the next string.
       __syncthreads();
-      for (uint32_t i = tid; i < HCAP; i += WG) {
-        S.h_key[i] = kEmptyKey;
-        S.h_first[i] = kEmptyKey;
-        S.h_dmin[i] = kMaxU64;
-        S.h_bmin[i] = kEmptyKey;
-      }
-      if (tid == 0) {
-        out.status[si] = fail;
-        out.path_len[si] = 0;
-        out.path_off[si] = 0;
-        out.final_w[si] = w_zero();
-        if (out.work) {
-          out.work[2 * si] = tuples;
-          out.work[2 * si + 1] = relax;
-        }
-      }
+      for (uint32_t i = tid; i < T.hcap; i += WG) tbl_clear_slot(T, i);
+      if (tid == 0) write_status(out, si, fail, tuples, relax);
       continue;
     }
 
     // ---- best final over the last layer (only final(L) is non-Zero on a chain) ----
     if (tid == 0) {
-      S.best = kMaxU64;
-      S.bestp = kEmptyKey;
+      SH.best = kMaxU64;
+      SH.bestp = kEmptyKey;
     }
     __syncthreads();
     for (uint32_t p = tid; p < n_cur; p += WG) {
-      const double d = S.d[cur][p];
-      const double fw2 = rhs.final_w[S.s2[cur][p]];
-      if (!w_is_zero(d) && !w_is_zero(fw2)) {
-        const double total = w_times(d, w_times(w_one(), fw2));
-        atomicMin(&S.best, (unsigned long long)okey(total));
-      }
+      const double d = T.d[cur][p];
+      const double fw2 = rhs.final_w[T.s2[cur][p]];
+      if (!w_is_zero(d) && !w_is_zero(fw2))
+        atomicMin(&SH.best, (unsigned long long)okey(w_times(d, w_times(w_one(), fw2))));
     }
     __syncthreads();
-    const unsigned long long best = S.best;
+    const unsigned long long best = SH.best;
     if (best != kMaxU64) {
       for (uint32_t p = tid; p < n_cur; p += WG) {
-        const double d = S.d[cur][p];
-        const double fw2 = rhs.final_w[S.s2[cur][p]];
+        const double d = T.d[cur][p];
+        const double fw2 = rhs.final_w[T.s2[cur][p]];
         if (!w_is_zero(d) && !w_is_zero(fw2) &&
             okey(w_times(d, w_times(w_one(), fw2))) == best)
-          atomicMin(&S.bestp, p);
+          atomicMin(&SH.bestp, p);
       }
     }
     __syncthreads();
 
     if (tid == 0) {
-      const uint32_t bp = S.bestp;
+      const uint32_t bp = SH.bestp;
       if (n_cur == 0 || best == kMaxU64 || bp == kEmptyKey) {
-        out.status[si] = kPathEmpty;
-        out.path_len[si] = 0;
-        out.path_off[si] = 0;
-        out.final_w[si] = w_zero();
+        write_status(out, si, kPathEmpty, tuples, relax);
       } else {
-        const double fw = w_times(w_one(), rhs.final_w[S.s2[cur][bp]]);
+        const double fw = w_times(w_one(), rhs.final_w[T.s2[cur][bp]]);  // compose.zig:73
         const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
         if (o + L > out.arc_cap) {
-          out.status[si] = kPathOutputFull;
-          out.path_len[si] = 0;
-          out.path_off[si] = 0;
-          out.final_w[si] = w_zero();
+          write_status(out, si, kPathOutputFull, tuples, relax);
         } else {
           // shortest-path.zig:109-136: walk back-pointers, one layer per hop.
           uint32_t id = cur_base + bp;
@@ -339,14 +404,21 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
           out.path_len[si] = L;
           out.path_off[si] = o;
           out.final_w[si] = fw;
+          if (out.work) {
+            out.work[2 * si] = tuples;
+            out.work[2 * si + 1] = relax;
+          }
         }
-      }
-      if (out.work) {
-        out.work[2 * si] = tuples;
-        out.work[2 * si + 1] = relax;
       }
     }
   }
+}
+
+// Appends every string whose status is `code` to a device list (retry tier input).
+__global__ void collect_status_kernel(const int32_t* status, uint32_t num, int32_t code,
+                                      uint32_t* list, uint32_t* count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < num && status[i] == code) list[atomicAdd(count, 1u)] = i;
 }
 
 }  // namespace fstamd
