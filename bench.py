@@ -26,6 +26,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import libfst_amd as F  # noqa: E402
+from libfst_amd import dist as D  # noqa: E402
 from libfst_amd import fst as FF  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -164,27 +165,14 @@ def main():
     # ---- rhs: built on rank 0, broadcast once over xGMI (RCCL), adopted on every rank ----
     blob_host = None
     if rank == 0:
-        src = F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, args.transducer_len, args.branches)
-        path = f"/tmp/libfst_bench_{os.getpid()}.fst"
-        src.save(path)
-        blob_host = open(path, "rb").read()
-        os.unlink(path)
+        blob_host = D.blob_bytes(
+            F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, args.transducer_len, args.branches))
     if world > 1:
-        n = torch.tensor([len(blob_host) if rank == 0 else 0], dtype=torch.int64, device=dev)
-        dist.broadcast(n, src=0)
-        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
-        if rank == 0:
-            buf.copy_(torch.frombuffer(bytearray(blob_host), dtype=torch.uint8))
-        dist.broadcast(buf, src=0)
-        torch.cuda.synchronize()
-        h = F.lib().fst_device_adopt_blob(dev_ptr(buf), buf.numel(), local, None)
-        rhs = F.Fst(h)
-        del buf
+        buf = D.broadcast_blob(blob_host, rank, dev)
     else:
-        h = F.lib().fst_device_adopt_blob(
-            dev_ptr(torch.frombuffer(bytearray(blob_host), dtype=torch.uint8).to(dev)),
-            len(blob_host), local, None)
-        rhs = F.Fst(h)
+        buf = torch.frombuffer(bytearray(blob_host), dtype=torch.uint8).to(dev)
+    rhs = D.adopt_on_device(buf, local)
+    del buf
 
     L = args.len
     lengths = np.full(args.batch, L, np.int64)
