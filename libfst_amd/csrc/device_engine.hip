@@ -144,6 +144,7 @@ namespace {
 constexpr int kElWG = 256;
 constexpr int kElFcap = 512;
 constexpr int kElHcap = 1024;
+constexpr int kElKmax = 8;  // candidates per tuple kept in registers across phases
 
 enum Scratch : size_t {
   kCounter = 0,
@@ -257,7 +258,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     // Tier 1: LDS tables, layers of <= kElFcap tuples (the metric's layers have <= 257).
     const uint64_t back_cap64 = (uint64_t)(in.max_len + 1) * kElFcap;
     const uint32_t back_cap = (uint32_t)std::min<uint64_t>(back_cap64, 1u << 22);
-    auto k1 = eager_layered_kernel<kElWG, kElFcap, kElHcap, true>;
+    auto k1 = eager_layered_lds_kernel<kElWG, kElFcap, kElHcap, kElKmax>;
     int occ = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k1, kElWG, 0));
     occ = std::max(occ, 1);

@@ -47,6 +47,9 @@ struct LayerTables {
   uint32_t* h_bmin;              // minimum tight candidate index (back-pointer)
   uint32_t* nslot;               // next layer rank -> slot
   uint32_t fcap, hcap, hbits;
+  // select, not index: a dynamically indexed pointer array would live in scratch
+  __device__ __forceinline__ uint32_t* s2p(uint32_t i) const { return i ? s2[1] : s2[0]; }
+  __device__ __forceinline__ double* dp(uint32_t i) const { return i ? d[1] : d[0]; }
 };
 
 template <int FCAP, int HCAP>
@@ -240,7 +243,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       uint32_t tsum = 0;
       for (uint32_t p = p0; p < p1; ++p) {
         uint32_t a, b;
-        span_by_ilabel(rhs, T.s2[cur][p], label, a, b);
+        span_by_ilabel(rhs, T.s2p(cur)[p], label, a, b);
         T.lo[p] = a;
         T.cnt[p] = b - a;
         tsum += b - a;
@@ -256,7 +259,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       // ---- (B) dedup targets, first occurrence, minimum distance ----
       uint32_t c = cbase;
       for (uint32_t p = p0; p < p1; ++p) {
-        const double dp = T.d[cur][p];
+        const double dp = T.dp(cur)[p];
         const uint32_t a0 = T.lo[p], n = T.cnt[p];
         for (uint32_t j = 0; j < n; ++j, ++c) {
           const ArcRec r = rhs.rec[a0 + j];
@@ -287,7 +290,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       uint32_t nf = 0;
       c = cbase;
       for (uint32_t p = p0; p < p1; ++p) {
-        const double dp = T.d[cur][p];
+        const double dp = T.dp(cur)[p];
         const uint32_t a0 = T.lo[p], n = T.cnt[p];
         for (uint32_t j = 0; j < n; ++j, ++c) {
           const ArcRec r = rhs.rec[a0 + j];
@@ -313,7 +316,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
             // indices are < 2^31, so no other candidate can match it any more)
             T.h_first[slot] = 0x80000000u | rank;
             T.nslot[rank] = slot;
-            T.s2[nxt][rank] = t;
+            T.s2p(nxt)[rank] = t;
             ++rank;
           }
         }
@@ -337,7 +340,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       // ---- (F) next-layer distances, clear the used slots ----
       for (uint32_t r = tid; r < n_next; r += WG) {
         const uint32_t slot = T.nslot[r];
-        T.d[nxt][r] = from_okey(T.h_dmin[slot]);
+        T.dp(nxt)[r] = from_okey(T.h_dmin[slot]);
         tbl_clear_slot(T, slot);
       }
       __syncthreads();
@@ -362,8 +365,8 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     }
     __syncthreads();
     for (uint32_t p = tid; p < n_cur; p += WG) {
-      const double d = T.d[cur][p];
-      const double fw2 = rhs.final_w[T.s2[cur][p]];
+      const double d = T.dp(cur)[p];
+      const double fw2 = rhs.final_w[T.s2p(cur)[p]];
       if (!w_is_zero(d) && !w_is_zero(fw2))
         atomicMin(&SH.best, (unsigned long long)okey(w_times(d, w_times(w_one(), fw2))));
     }
@@ -371,8 +374,8 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     const unsigned long long best = SH.best;
     if (best != kMaxU64) {
       for (uint32_t p = tid; p < n_cur; p += WG) {
-        const double d = T.d[cur][p];
-        const double fw2 = rhs.final_w[T.s2[cur][p]];
+        const double d = T.dp(cur)[p];
+        const double fw2 = rhs.final_w[T.s2p(cur)[p]];
         if (!w_is_zero(d) && !w_is_zero(fw2) &&
             okey(w_times(d, w_times(w_one(), fw2))) == best)
           atomicMin(&SH.bestp, p);
@@ -385,7 +388,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       if (n_cur == 0 || best == kMaxU64 || bp == kEmptyKey) {
         write_status(out, si, kPathEmpty, tuples, relax);
       } else {
-        const double fw = w_times(w_one(), rhs.final_w[T.s2[cur][bp]]);  // compose.zig:73
+        const double fw = w_times(w_one(), rhs.final_w[T.s2p(cur)[bp]]);  // compose.zig:73
         const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
         if (o + L > out.arc_cap) {
           write_status(out, si, kPathOutputFull, tuples, relax);
@@ -402,6 +405,324 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
           }
           out.status[si] = kPathOk;
           out.path_len[si] = L;
+          out.path_off[si] = o;
+          out.final_w[si] = fw;
+          if (out.work) {
+            out.work[2 * si] = tuples;
+            out.work[2 * si + 1] = relax;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// LDS tier, v2: same phases and the same results as the generic kernel above, with
+// the per-layer latency cut down:
+//  * each thread owns <= EMAX = FCAP/WG tuples of a layer; the distance and hash
+//    slot of each of their first KMAX candidates stay in registers from phase B to
+//    E (no re-reads of rhs arcs, no re-probing of the hash);
+//  * the next layer's arcsByIlabel spans are computed while the layer is finished
+//    (span loads issued in E, ilabel search in F), so a layer starts with its
+//    spans already in LDS.
+// Per layer the critical path holds two global round trips (arc records in B,
+// ilabels in F) instead of six.
+// ---------------------------------------------------------------------------------
+template <int WG, int FCAP, int HCAP, int KMAX>
+__global__ void __launch_bounds__(WG)
+eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
+                         EagerLaunch lp, BatchOutDev out) {
+  constexpr int EMAX = FCAP / WG;
+  static_assert(FCAP % WG == 0, "FCAP must be a multiple of WG");
+  __shared__ LayerShared SH;
+  __shared__ LayerLds<FCAP, HCAP> L;
+  LayerTables T;
+  T.s2[0] = L.s2[0];
+  T.s2[1] = L.s2[1];
+  T.d[0] = L.d[0];
+  T.d[1] = L.d[1];
+  T.lo = L.lo;
+  T.cnt = L.cnt;
+  T.h_key = L.h_key;
+  T.h_first = L.h_first;
+  T.h_dmin = L.h_dmin;
+  T.h_bmin = L.h_bmin;
+  T.nslot = L.nslot;
+  T.fcap = FCAP;
+  T.hcap = HCAP;
+  T.hbits = __builtin_ctz(HCAP);
+  const uint32_t tid = threadIdx.x;
+  uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+  for (uint32_t i = tid; i < HCAP; i += WG) tbl_clear_slot(T, i);
+
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) SH.item = atomicAdd(next_item, 1u);
+    __syncthreads();
+    const uint32_t item = SH.item;
+    if (item >= lp.num_items) break;
+    const uint32_t si = item;
+    const uint64_t off = in.offsets[si];
+    const uint32_t Lk = (uint32_t)(in.offsets[si + 1] - off);
+
+    if (rhs.start == kNoState || n_best != 1) {  // compose.zig:33-35, shortest-path.zig:21-24
+      if (tid == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+      if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
+      continue;
+    }
+    if (tid == 0) {
+      T.s2[0][0] = rhs.start;
+      T.d[0][0] = w_one();
+      if (Lk > 0) {
+        uint32_t a, b;
+        span_by_ilabel(rhs, rhs.start, in.labels[off], a, b);
+        T.lo[0] = a;
+        T.cnt[0] = b - a;
+      }
+    }
+    uint32_t cur = 0, n_cur = 1, cur_base = 0;
+    uint32_t tuples = 1, relax = 0;
+    int32_t fail = kPathOk;
+    __syncthreads();
+
+    for (uint32_t k = 0; k < Lk; ++k) {
+      const uint32_t label = in.labels[off + k];
+      if (label == kEpsilon) {  // lhs epsilon output: not a layered lattice
+        fail = kPathUnsupported;
+        break;
+      }
+      const uint32_t E = (n_cur + WG - 1) / WG;  // <= EMAX because n_cur <= FCAP
+      const uint32_t p0 = min(tid * E, n_cur);
+      uint32_t lo[EMAX], cnt[EMAX];
+      double dd[EMAX];
+      uint32_t tsum = 0;
+      bool too_long = false;  // > KMAX arcs with one label: HBM tier handles the string
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        const uint32_t p = p0 + e;
+        const bool v = (uint32_t)e < E && p < n_cur;
+        lo[e] = v ? T.lo[p] : 0u;
+        cnt[e] = v ? T.cnt[p] : 0u;
+        dd[e] = v ? T.dp(cur)[p] : 0.0;
+        too_long |= cnt[e] > (uint32_t)KMAX;
+        tsum += cnt[e];
+      }
+      if (tid == 0) {
+        SH.nnext = 0;
+        SH.flag = 0;
+      }
+      uint32_t ctot;
+      const uint32_t cbase = block_excl_scan<WG>(tsum, SH.scan, ctot);
+      relax += ctot;
+      if (too_long) SH.flag = 1;  // after the scan's barriers: the reset above is done
+
+      // ---- (B) dedup targets, first occurrence, minimum distance ----
+      double rnd[EMAX][KMAX];
+      uint32_t rslot[EMAX][KMAX];
+      uint32_t c = cbase;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        const double dp = dd[e];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          rslot[e][j] = kEmptyKey;
+          rnd[e][j] = 0.0;
+          if ((uint32_t)j < cnt[e]) {
+            const ArcRec r = rhs.rec[lo[e] + j];
+            const double nd = w_times(dp, w_times(w_one(), r.weight));  // compose.zig:104
+            bool created;
+            const uint32_t slot = tbl_insert(T, r.next, created);
+            if (slot == kEmptyKey) {
+              SH.flag = 1;
+            } else {
+              if (created && atomicAdd(&SH.nnext, 1u) >= (uint32_t)FCAP) SH.flag = 1;
+              atomicMin(&T.h_first[slot], c + j);
+              atomicMin(&T.h_dmin[slot], (unsigned long long)okey(nd));
+            }
+            rslot[e][j] = slot;
+            rnd[e][j] = nd;
+          }
+        }
+        c += cnt[e];
+      }
+      __syncthreads();
+      const uint32_t n_next = SH.nnext;
+      if (SH.flag || (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
+        fail = kPathOverflow;
+        break;
+      }
+      if (n_next == 0) {
+        n_cur = 0;
+        break;
+      }
+
+      // ---- (C) tight candidates -> back-pointer; count first occurrences ----
+      uint32_t nf = 0;
+      c = cbase;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if ((uint32_t)j < cnt[e]) {
+            const uint32_t slot = rslot[e][j];
+            if (okey(rnd[e][j]) == T.h_dmin[slot]) atomicMin(&T.h_bmin[slot], c + j);
+            if (T.h_first[slot] == c + j) ++nf;
+          }
+        }
+        c += cnt[e];
+      }
+      uint32_t nftot;
+      uint32_t rank = block_excl_scan<WG>(nf, SH.scan, nftot);
+
+      // ---- (D) ids of the next layer in first-occurrence order ----
+      const uint32_t nxt = cur ^ 1;
+      c = cbase;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if ((uint32_t)j < cnt[e]) {
+            const uint32_t slot = rslot[e][j];
+            if (T.h_first[slot] == c + j) {
+              T.h_first[slot] = 0x80000000u | rank;
+              T.nslot[rank] = slot;
+              T.s2p(nxt)[rank] = T.h_key[slot];
+              ++rank;
+            }
+          }
+        }
+        c += cnt[e];
+      }
+      __syncthreads();
+
+      // ---- (E) back-pointer records; start loading the next layer's spans ----
+      const uint32_t next_base = cur_base + n_cur;
+      c = cbase;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if ((uint32_t)j < cnt[e]) {
+            const uint32_t slot = rslot[e][j];
+            if (T.h_bmin[slot] == c + j)
+              back[next_base + (T.h_first[slot] & 0x7FFFFFFFu)] =
+                  make_uint2(cur_base + p0 + e, lo[e] + j);
+          }
+        }
+        c += cnt[e];
+      }
+      const bool more = k + 1 < Lk;
+      const uint32_t next_label = more ? in.labels[off + k + 1] : 0u;
+      uint2 sp[EMAX];
+#pragma unroll
+      for (int i = 0; i < EMAX; ++i) {
+        const uint32_t r = tid + i * WG;
+        sp[i] = (more && r < n_next) ? rhs.span[T.s2p(nxt)[r]] : make_uint2(0, 0);
+      }
+      __syncthreads();
+
+      // ---- (F) next-layer distances, clear used slots, next-layer spans ----
+#pragma unroll
+      for (int i = 0; i < EMAX; ++i) {
+        const uint32_t r = tid + i * WG;
+        if (r < n_next) {
+          const uint32_t slot = T.nslot[r];
+          T.dp(nxt)[r] = from_okey(T.h_dmin[slot]);
+          tbl_clear_slot(T, slot);
+          if (more) {
+            // Fst.arcsByIlabel over [sp.x, sp.x + sp.y) (src/fst.zig:112-136)
+            const uint32_t o = sp[i].x, n = sp[i].y;
+            uint32_t a, b;
+            if (n <= 8) {
+              uint32_t cl = 0, ch = 0;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const uint32_t x = (uint32_t)q < n ? rhs.il[o + q] : 0xFFFFFFFFu;
+                cl += ((uint32_t)q < n && x < next_label) ? 1u : 0u;
+                ch += ((uint32_t)q < n && x <= next_label) ? 1u : 0u;
+              }
+              a = o + cl;
+              b = o + ch;
+            } else {
+              span_by_ilabel(rhs, T.s2p(nxt)[r], next_label, a, b);
+            }
+            T.lo[r] = a;
+            T.cnt[r] = b - a;
+          }
+        }
+      }
+      __syncthreads();
+      cur = nxt;
+      cur_base = next_base;
+      n_cur = n_next;
+      tuples += n_next;
+    }
+
+    if (fail != kPathOk) {
+      __syncthreads();
+      for (uint32_t i = tid; i < HCAP; i += WG) tbl_clear_slot(T, i);
+      if (tid == 0) write_status(out, si, fail, tuples, relax);
+      continue;
+    }
+
+    // ---- best final over the last layer (shortest-path.zig:88-104) ----
+    if (tid == 0) {
+      SH.best = kMaxU64;
+      SH.bestp = kEmptyKey;
+    }
+    __syncthreads();
+    unsigned long long mykey = kMaxU64;
+    uint32_t myp = kEmptyKey;
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      const uint32_t p = tid + i * WG;
+      if (p < n_cur) {
+        const double d = T.dp(cur)[p];
+        const double fw2 = rhs.final_w[T.s2p(cur)[p]];
+        if (!w_is_zero(d) && !w_is_zero(fw2)) {
+          const unsigned long long kk = okey(w_times(d, w_times(w_one(), fw2)));
+          if (kk < mykey) {
+            mykey = kk;
+            myp = p;
+          }
+        }
+      }
+    }
+    if (mykey != kMaxU64) atomicMin(&SH.best, mykey);
+    __syncthreads();
+    const unsigned long long best = SH.best;
+    if (best != kMaxU64 && mykey == best) atomicMin(&SH.bestp, myp);
+    __syncthreads();
+
+    if (tid == 0) {
+      const uint32_t bp = SH.bestp;
+      if (n_cur == 0 || best == kMaxU64 || bp == kEmptyKey) {
+        write_status(out, si, kPathEmpty, tuples, relax);
+      } else {
+        const double fw = w_times(w_one(), rhs.final_w[T.s2p(cur)[bp]]);  // compose.zig:73
+        const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)Lk);
+        if (o + Lk > out.arc_cap) {
+          write_status(out, si, kPathOutputFull, tuples, relax);
+        } else {
+          uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
+          for (uint32_t k = Lk; k > 0; --k) {
+            const uint2 b = back[id];
+            const ArcRec r = rhs.rec[b.y];
+            out.out_il[o + k - 1] = in.labels[off + k - 1];
+            out.out_ol[o + k - 1] = r.olabel;
+            out.out_w[o + k - 1] = w_times(w_one(), r.weight);
+            id = b.x;
+          }
+          out.status[si] = kPathOk;
+          out.path_len[si] = Lk;
           out.path_off[si] = o;
           out.final_w[si] = fw;
           if (out.work) {
