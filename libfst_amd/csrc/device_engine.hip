@@ -270,8 +270,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     // Tier 2 (HBM tables) takes the strings tier 1 reports as OVERFLOW.  A layer of a
     // layered lattice holds at most one tuple per rhs state, so fcap = num_states can
     // only overflow the back-pointer slab.  Skipped when tier 1 cannot overflow.
-    const bool may_overflow =
-        (uint64_t)rhs.view.num_states > (uint64_t)kElFcap || back_cap64 > back_cap;
+    const bool may_overflow = (uint64_t)rhs.view.num_states > (uint64_t)kElFcap ||
+                              back_cap64 > back_cap || rhs.view.max_span > (uint32_t)kElKmax;
     uint32_t* list = nullptr;
     uint32_t* count = counter + 2;
     uint32_t grid2 = 0, fcap2 = 0, hcap2 = 0, back_cap2 = 0;

@@ -50,6 +50,16 @@ __device__ __forceinline__ bool wd_expired(unsigned long long t0, unsigned long 
 constexpr uint32_t kSettled = 1u;
 constexpr uint32_t kHasBack = 2u;
 
+// The kernel runs one wavefront per workgroup and all of a string's state is
+// private to that wave.  A wave's vector memory and LDS operations execute in
+// program order, so its own stores are visible to its later loads (LLVM AMDGPU
+// memory model: wavefront scope needs no cache or counter synchronisation).  The
+// fence below therefore only stops the compiler from reordering accesses across
+// phases -- no s_waitcnt for store acknowledgements on the critical path.
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 __device__ __forceinline__ unsigned long long tuple_key(uint32_t s1, uint32_t s2, uint32_t f) {
   return ((unsigned long long)s2 << 32) | ((unsigned long long)s1 << 2) | f;
 }
@@ -188,7 +198,7 @@ __device__ void prepare_graph(const RhsView& rhs, const GraphInput& g, uint4* tb
     base1 += __shfl(inc, 63, 64);
     ebase += __popcll(em);
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  wave_fence();
   uint32_t lo3, hi3;
   span_by_ilabel(rhs, P.s2, kEpsilon, lo3, hi3);
   P.lo3 = lo3;
@@ -352,7 +362,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       qd[0] = w_one();
       qid[0] = 0;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wave_fence();
 
     uint32_t best_id = kNoState;
     double best_fw = w_zero(), best_total = w_zero();
@@ -421,7 +431,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           qid[i] = xi;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      wave_fence();
 
       if (pid >= nn) {  // cannot happen on a consistent heap; never spin on garbage
         fail = kPathInternal;
@@ -534,7 +544,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         const uint32_t lt = __shfl(tid, (int)leader, 64);
         if (need) tid = lt;
         nn += n_new;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
 
         // self-loop onto the popped tuple: rare, exact one-lane path
         const unsigned long long selfm = __ballot(act && tid == pid);
@@ -543,7 +553,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           S.w[lane] = x.w;
           S.il[lane] = x.il;
           S.ol[lane] = x.ol;
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          wave_fence();
           const uint32_t cnt = C - cb < 64 ? C - cb : 64;
           if (lane == 0) {
             for (uint32_t i = 0; i < cnt; ++i) {
@@ -586,7 +596,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           cur_dist = __shfl(cur_dist, 0, 64);
           qn = __shfl(qn, 0, 64);
           fail = __shfl(fail, 0, 64);
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+          wave_fence();
           if (fail != kPathOk) break;
           continue;
         }
@@ -598,7 +608,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         S.il[lane] = x.il;
         S.ol[lane] = x.ol;
         S.id[lane] = act ? tid : kNoState;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         unsigned long long gmask = 0;
         {
           unsigned long long pend = __ballot(act);
@@ -653,7 +663,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             }
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         // pushes in lane order, one lane at a time (sift-up is short in practice)
         unsigned long long pm = __ballot(push);
         while (pm) {
@@ -687,7 +697,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           ++qn;
           ++pushes;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_fence();
         if (fail != kPathOk) break;
       }
       if (fail != kPathOk) break;
