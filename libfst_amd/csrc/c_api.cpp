@@ -301,8 +301,12 @@ FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64
     DevOut out(num, arc_cap);
     if (!out.ok()) return FST_OOM;
     LaunchStats st;
-    if (E.run_chain(*D, in, n, semantics, out.v, nullptr, &st) != hipSuccess) return FST_OOM;
-    if (hipDeviceSynchronize() != hipSuccess) return FST_OOM;
+    hipError_t err = E.run_chain(*D, in, n, semantics, out.v, nullptr, &st);
+    if (err == hipSuccess) err = hipDeviceSynchronize();
+    if (err != hipSuccess) {
+      std::fprintf(stderr, "[libfst_amd] batch engine failed: %s\n", hipGetErrorString(err));
+      return FST_OOM;
+    }
     if (!out.download(num, h)) return FST_OOM;
     t_last_stats = st;
     bool full = false;

@@ -298,13 +298,39 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                    watchdog_ticks()};
     k1<<<grid, kElWG, 0, stream>>>(rhs.view, in, n, counter, lp, out);
     HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_DEBUG_BOUNDS
+    std::fprintf(stderr, "[fstamd dbg] tier1 sync: %s\n", hipGetErrorString(hipStreamSynchronize(stream)));
+#endif
     if (may_overflow) {
       collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
           out.status, in.num_strings, kPathOverflow, list, count);
       EagerLaunch lp2{list, count, 0, slab, fcap2, hcap2, back2, back_cap2, watchdog_ticks()};
+#ifdef FSTAMD_DEBUG_BOUNDS
+      static uint32_t* h_trace = nullptr;
+      if (!h_trace) {
+        HIP_TRY(hipHostMalloc((void**)&h_trace, 4096 * 16, hipHostMallocCoherent));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_fst_trace), &h_trace, sizeof(h_trace)));
+      }
+      std::memset(h_trace, 0xEE, 4096 * 16);
+      std::fprintf(stderr, "[fstamd dbg] tier2 grid=%u fcap=%u hcap=%u back_cap=%u slab=%p back=%p\n",
+                   grid2, fcap2, hcap2, back_cap2, (void*)slab, (void*)back2);
+#endif
       eager_layered_kernel<kElWG, kElFcap, kElHcap, false>
           <<<grid2, kElWG, 0, stream>>>(rhs.view, in, n, counter + 1, lp2, out);
       HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_DEBUG_BOUNDS
+      {
+        const hipError_t e = hipStreamSynchronize(stream);
+        std::fprintf(stderr, "[fstamd dbg] tier2 sync: %s\n", hipGetErrorString(e));
+        for (uint32_t b = 0; b < grid2; ++b) {
+          const uint32_t* w = h_trace + b * 4;
+          if (w[0] != 0xEEEEEEEEu)
+            std::fprintf(stderr, "[fstamd dbg] wg %u item %u si %d k %u phase %u\n", b, w[0],
+                         (int)w[1], w[2], w[3]);
+        }
+        if (e != hipSuccess) return e;
+      }
+#endif
     }
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));

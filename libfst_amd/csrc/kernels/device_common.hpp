@@ -11,17 +11,48 @@ namespace fstamd {
 constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;
 constexpr unsigned long long kMaxU64 = ~0ull;
 
+// Debug builds (make DEBUG_BOUNDS=1) check every indexed access FB(i, cap, site):
+// an out-of-range index is reported with device printf and clamped to 0, so a bug
+// shows up as a message instead of a GPU memory fault.  Release builds: no-op.
+#ifdef FSTAMD_DEBUG_BOUNDS
+__device__ __forceinline__ uint64_t fst_bound(uint64_t i, uint64_t cap, int site) {
+  if (i >= cap) {
+    printf("[fstamd OOB] site %d index %llu cap %llu block %u thread %u\n", site,
+           (unsigned long long)i, (unsigned long long)cap, blockIdx.x, threadIdx.x);
+    return 0;
+  }
+  return i;
+}
+#define FB(i, cap, site) fst_bound((uint64_t)(i), (uint64_t)(cap), (site))
+// Progress trace into fine-grained host memory (survives a queue abort): thread 0 of
+// each workgroup records (item, string, layer, phase) before every phase.
+__device__ uint32_t* g_fst_trace;
+__device__ __forceinline__ void fst_trace(uint32_t item, uint32_t si, uint32_t k, uint32_t ph) {
+  uint32_t* t = g_fst_trace;
+  if (t && threadIdx.x == 0) {
+    volatile uint32_t* w = t + blockIdx.x * 4;
+    w[0] = item; w[1] = si; w[2] = k; w[3] = ph;
+    __threadfence_system();
+  }
+}
+#define FT(item, si, k, ph) fst_trace((item), (si), (k), (ph))
+#else
+#define FB(i, cap, site) (i)
+#define FT(item, si, k, ph) ((void)0)
+#endif
+
 // Fst.arcsByIlabel (src/fst.zig:112-136): global arc range [lo, hi) of the arcs of
 // state `s` whose ilabel == label.  Spans of <= 8 arcs are counted with independent
 // loads (no dependent binary-search chain); longer spans use the two binary searches.
 __device__ __forceinline__ void span_by_ilabel(const RhsView& r, uint32_t s, uint32_t label,
                                                uint32_t& lo, uint32_t& hi) {
-  const uint2 sp = r.span[s];
+  const uint2 sp = r.span[FB(s, r.num_states, 1)];
   const uint32_t off = sp.x, n = sp.y;
   if (n <= 8) {
     uint32_t x[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = (uint32_t)i < n ? r.il[off + i] : 0xFFFFFFFFu;
+    for (int i = 0; i < 8; ++i)
+      x[i] = (uint32_t)i < n ? r.il[FB(off + i, r.num_arcs, 2)] : 0xFFFFFFFFu;
     uint32_t cl = 0, ch = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -36,14 +67,14 @@ __device__ __forceinline__ void span_by_ilabel(const RhsView& r, uint32_t s, uin
   uint32_t a = 0, b = n;
   while (a < b) {
     const uint32_t m = a + ((b - a) >> 1);
-    if (r.il[off + m] < label) a = m + 1;
+    if (r.il[FB(off + m, r.num_arcs, 3)] < label) a = m + 1;
     else b = m;
   }
   const uint32_t first = a;
   b = n;
   while (a < b) {
     const uint32_t m = a + ((b - a) >> 1);
-    if (r.il[off + m] <= label) a = m + 1;
+    if (r.il[FB(off + m, r.num_arcs, 4)] <= label) a = m + 1;
     else b = m;
   }
   lo = off + first;

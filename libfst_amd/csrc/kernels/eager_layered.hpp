@@ -66,8 +66,12 @@ struct LayerLds {
 };
 
 // Bytes of one workgroup's HBM table slab for the overflow tier.
+// Rounded to 256 B: workgroup slabs are carved at blockIdx * this stride, and the
+// 64-bit atomics on h_dmin fault on a misaligned address.
 __host__ __device__ inline size_t layer_slab_bytes(uint32_t fcap, uint32_t hcap) {
-  return (size_t)fcap * (2 * 4 + 2 * 8 + 4 + 4 + 4) + (size_t)hcap * (4 + 4 + 8 + 4) + 256;
+  const size_t raw =
+      (size_t)fcap * (2 * 4 + 2 * 8 + 4 + 4 + 4) + (size_t)hcap * (4 + 4 + 8 + 4) + 256;
+  return (raw + 255) & ~(size_t)255;
 }
 
 __device__ inline LayerTables carve_slab(uint8_t* base, uint32_t fcap, uint32_t hcap) {
@@ -121,10 +125,11 @@ __device__ __forceinline__ uint32_t tbl_find(const LayerTables& T, uint32_t k) {
     if (T.h_key[i] == k) return i;
     i = (i + 1) & (T.hcap - 1);
   }
-  return kEmptyKey;
+  return (uint32_t)FB(kEmptyKey, T.hcap, 10);  // a key inserted in phase B must be found
 }
 
 __device__ __forceinline__ void tbl_clear_slot(const LayerTables& T, uint32_t s) {
+  s = (uint32_t)FB(s, T.hcap, 19);
   T.h_key[s] = kEmptyKey;
   T.h_first[s] = kEmptyKey;
   T.h_dmin[s] = kMaxU64;
@@ -202,6 +207,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     __syncthreads();
     const uint32_t item = SH.item;
     if (item >= num_items) break;
+    FT(item, 0xFFFFFFFFu, 0, 0);
     const uint32_t si = lp.items ? lp.items[item] : item;
     const uint64_t off = in.offsets[si];
     const uint32_t L = (uint32_t)(in.offsets[si + 1] - off);
@@ -239,6 +245,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       const uint32_t E = (n_cur + WG - 1) / WG;
       const uint32_t p0 = min(tid * E, n_cur), p1 = min(p0 + E, n_cur);
 
+      FT(item, si, k, 1);
       // ---- (A) rhs spans (arcsByIlabel) of the chunk ----
       uint32_t tsum = 0;
       for (uint32_t p = p0; p < p1; ++p) {
@@ -256,13 +263,14 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       const uint32_t cbase = block_excl_scan<WG>(tsum, SH.scan, ctot);
       relax += ctot;
 
+      FT(item, si, k, 2);
       // ---- (B) dedup targets, first occurrence, minimum distance ----
       uint32_t c = cbase;
       for (uint32_t p = p0; p < p1; ++p) {
         const double dp = T.dp(cur)[p];
         const uint32_t a0 = T.lo[p], n = T.cnt[p];
         for (uint32_t j = 0; j < n; ++j, ++c) {
-          const ArcRec r = rhs.rec[a0 + j];
+          const ArcRec r = rhs.rec[FB(a0 + j, rhs.num_arcs, 14)];
           const double nd = w_times(dp, w_times(w_one(), r.weight));  // compose.zig:104
           bool created;
           const uint32_t slot = tbl_insert(T, r.next, created);
@@ -286,6 +294,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
         break;
       }
 
+      FT(item, si, k, 3);
       // ---- (C) tight candidates -> back-pointer; count first occurrences ----
       uint32_t nf = 0;
       c = cbase;
@@ -303,6 +312,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       uint32_t nftot;
       uint32_t rank = block_excl_scan<WG>(nf, SH.scan, nftot);
 
+      FT(item, si, k, 4);
       // ---- (D) ids of the next layer in first-occurrence order ----
       const uint32_t nxt = cur ^ 1;
       c = cbase;
@@ -315,14 +325,15 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
             // the slot's rank replaces its first-candidate index (tag bit 31: candidate
             // indices are < 2^31, so no other candidate can match it any more)
             T.h_first[slot] = 0x80000000u | rank;
-            T.nslot[rank] = slot;
-            T.s2p(nxt)[rank] = t;
+            T.nslot[FB(rank, T.fcap, 17)] = slot;
+            T.s2p(nxt)[FB(rank, T.fcap, 18)] = t;
             ++rank;
           }
         }
       }
       __syncthreads();
 
+      FT(item, si, k, 5);
       // ---- (E) back-pointer records of the next layer ----
       const uint32_t next_base = cur_base + n_cur;
       c = cbase;
@@ -332,15 +343,17 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
           const uint32_t t = rhs.rec[a0 + j].next;
           const uint32_t slot = tbl_find(T, t);
           if (T.h_bmin[slot] == c)
-            back[next_base + (T.h_first[slot] & 0x7FFFFFFFu)] = make_uint2(cur_base + p, a0 + j);
+            back[FB(next_base + (T.h_first[slot] & 0x7FFFFFFFu), lp.back_cap, 11)] =
+                make_uint2(cur_base + p, a0 + j);
         }
       }
       __syncthreads();
 
+      FT(item, si, k, 6);
       // ---- (F) next-layer distances, clear the used slots ----
       for (uint32_t r = tid; r < n_next; r += WG) {
-        const uint32_t slot = T.nslot[r];
-        T.dp(nxt)[r] = from_okey(T.h_dmin[slot]);
+        const uint32_t slot = T.nslot[FB(r, T.fcap, 15)];
+        T.dp(nxt)[r] = from_okey(T.h_dmin[FB(slot, T.hcap, 16)]);
         tbl_clear_slot(T, slot);
       }
       __syncthreads();
@@ -358,6 +371,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       continue;
     }
 
+    FT(item, si, L, 7);
     // ---- best final over the last layer (only final(L) is non-Zero on a chain) ----
     if (tid == 0) {
       SH.best = kMaxU64;
@@ -366,7 +380,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     __syncthreads();
     for (uint32_t p = tid; p < n_cur; p += WG) {
       const double d = T.dp(cur)[p];
-      const double fw2 = rhs.final_w[T.s2p(cur)[p]];
+      const double fw2 = rhs.final_w[FB(T.s2p(cur)[p], rhs.num_states, 20)];
       if (!w_is_zero(d) && !w_is_zero(fw2))
         atomicMin(&SH.best, (unsigned long long)okey(w_times(d, w_times(w_one(), fw2))));
     }
@@ -375,7 +389,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     if (best != kMaxU64) {
       for (uint32_t p = tid; p < n_cur; p += WG) {
         const double d = T.dp(cur)[p];
-        const double fw2 = rhs.final_w[T.s2p(cur)[p]];
+        const double fw2 = rhs.final_w[FB(T.s2p(cur)[p], rhs.num_states, 20)];
         if (!w_is_zero(d) && !w_is_zero(fw2) &&
             okey(w_times(d, w_times(w_one(), fw2))) == best)
           atomicMin(&SH.bestp, p);
@@ -393,11 +407,12 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
         if (o + L > out.arc_cap) {
           write_status(out, si, kPathOutputFull, tuples, relax);
         } else {
+          FT(item, si, L, 8);
           // shortest-path.zig:109-136: walk back-pointers, one layer per hop.
           uint32_t id = cur_base + bp;
           for (uint32_t k = L; k > 0; --k) {
-            const uint2 b = back[id];
-            const ArcRec r = rhs.rec[b.y];
+            const uint2 b = back[FB(id, lp.back_cap, 12)];
+            const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 13)];
             out.out_il[o + k - 1] = in.labels[off + k - 1];
             out.out_ol[o + k - 1] = r.olabel;
             out.out_w[o + k - 1] = w_times(w_one(), r.weight);
@@ -536,7 +551,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
           rslot[e][j] = kEmptyKey;
           rnd[e][j] = 0.0;
           if ((uint32_t)j < cnt[e]) {
-            const ArcRec r = rhs.rec[lo[e] + j];
+            const ArcRec r = rhs.rec[FB(lo[e] + j, rhs.num_arcs, 24)];
             const double nd = w_times(dp, w_times(w_one(), r.weight));  // compose.zig:104
             bool created;
             const uint32_t slot = tbl_insert(T, r.next, created);
@@ -613,7 +628,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
           if ((uint32_t)j < cnt[e]) {
             const uint32_t slot = rslot[e][j];
             if (T.h_bmin[slot] == c + j)
-              back[next_base + (T.h_first[slot] & 0x7FFFFFFFu)] =
+              back[FB(next_base + (T.h_first[slot] & 0x7FFFFFFFu), lp.back_cap, 21)] =
                   make_uint2(cur_base + p0 + e, lo[e] + j);
           }
         }
@@ -686,7 +701,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
       const uint32_t p = tid + i * WG;
       if (p < n_cur) {
         const double d = T.dp(cur)[p];
-        const double fw2 = rhs.final_w[T.s2p(cur)[p]];
+        const double fw2 = rhs.final_w[FB(T.s2p(cur)[p], rhs.num_states, 20)];
         if (!w_is_zero(d) && !w_is_zero(fw2)) {
           const unsigned long long kk = okey(w_times(d, w_times(w_one(), fw2)));
           if (kk < mykey) {
@@ -714,8 +729,8 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
         } else {
           uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
           for (uint32_t k = Lk; k > 0; --k) {
-            const uint2 b = back[id];
-            const ArcRec r = rhs.rec[b.y];
+            const uint2 b = back[FB(id, lp.back_cap, 22)];
+            const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 23)];
             out.out_il[o + k - 1] = in.labels[off + k - 1];
             out.out_ol[o + k - 1] = r.olabel;
             out.out_w[o + k - 1] = w_times(w_one(), r.weight);
