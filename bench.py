@@ -30,6 +30,20 @@ from libfst_amd import dist as D  # noqa: E402
 from libfst_amd import fst as FF  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# Measured HBM traffic of the metric kernel: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+# over this same command (scripts/profile_r01.sh), reduced by scripts/pmc_summary.py.
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def measured_traffic(args, sem):
+    """Per-launch HBM bytes from the committed PMC summary (metric config only), else None."""
+    if sem != F.FST_SEM_EAGER or (args.len, args.transducer_len, args.branches) != (64, 4096, 12):
+        return None, None
+    try:
+        t = json.load(open(TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    return t["traffic_per_string"] * args.batch, t.get("source", TRAFFIC_FILE)
 
 
 def parse():
@@ -220,6 +234,7 @@ def main():
                          "note": "fst_compose_frozen_shortest_path semantics (exact Dijkstra replay)"}
 
     if rank == 0:
+        traffic, traffic_src = measured_traffic(args, sem)
         cpu = None
         if not args.no_cpu:
             cpu = cpu_baseline(args, blob_host, 1 if sem == F.FST_SEM_EAGER else 0)
@@ -244,9 +259,10 @@ def main():
                        "global_batch": args.batch * world,
                        "parallelism": f"dp{world} (string shards, rhs replicated via RCCL broadcast)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel_ms": avg_k, "b_alg_per_string": balg / args.batch,
-                         "kernel": "eager_layered_kernel" if sem else "lazy_wave_kernel"},
+                         "kernel": "eager_layered_lds_kernel" if sem else "lazy_wave_kernel"},
             "cpu_baseline": cpu,
         }
         line.update(extra)
