@@ -4,10 +4,14 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
+#include <cstdlib>
 #include <memory>
+#include <thread>
 
 #include "host_fst.hpp"
 #include "kernels/eager_layered.hpp"
+#include "kernels/eager_wave.hpp"
 #include "kernels/lazy_wave.hpp"
 
 #define HIP_TRY(x)                              \
@@ -24,7 +28,7 @@ namespace fstamd {
 // ---------------------------------------------------------------------------------
 
 __global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t na, uint2* span,
-                                    double* fin, uint32_t* il, ArcRec* rec) {
+                                    double* fin, uint32_t* il, ArcRec* rec, uint4* sspan) {
   const StateEntry* se = reinterpret_cast<const StateEntry*>(blob + sizeof(Header));
   const PackedArc* pa =
       reinterpret_cast<const PackedArc*>(blob + sizeof(Header) + (size_t)ns * sizeof(StateEntry));
@@ -33,6 +37,13 @@ __global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t n
     const StateEntry e = se[i];
     span[i] = make_uint2(e.arc_offset, e.num_arcs);
     fin[i] = e.final_weight;
+    // arcs are sorted by ilabel (fst.zig:258-265): first == last <=> one shared ilabel
+    uint32_t uniq = kSpanNone;
+    if (e.num_arcs > 0) {
+      const uint32_t a = pa[e.arc_offset].ilabel, z = pa[e.arc_offset + e.num_arcs - 1].ilabel;
+      uniq = a == z ? a : kSpanMixed;
+    }
+    sspan[i] = make_uint4(e.arc_offset, e.num_arcs, uniq, 0u);
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
     const PackedArc a = pa[i];
@@ -70,7 +81,9 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   bool ok = hipMalloc(&d->span, sizeof(uint2) * std::max<uint32_t>(ns, 1)) == hipSuccess &&
             hipMalloc(&d->final_w, sizeof(double) * std::max<uint32_t>(ns, 1)) == hipSuccess &&
             hipMalloc(&d->il, sizeof(uint32_t) * std::max<uint32_t>(na, 1)) == hipSuccess &&
-            hipMalloc(&d->rec, sizeof(ArcRec) * std::max<uint32_t>(na, 1)) == hipSuccess;
+            hipMalloc(&d->rec, sizeof(ArcRec) * ((size_t)na + kRecPad)) == hipSuccess &&
+            hipMemset(d->rec + na, 0, sizeof(ArcRec) * kRecPad) == hipSuccess &&
+            hipMalloc(&d->sspan, sizeof(uint4) * std::max<uint32_t>(ns, 1)) == hipSuccess;
   if (!ok) {
     DeviceFst::destroy(d);
     return nullptr;
@@ -79,7 +92,8 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   const uint32_t blocks = std::min<uint32_t>((work + 255) / 256, 4096);
   if (work > 0) {
     build_mirror_kernel<<<std::max<uint32_t>(blocks, 1), 256>>>(d->blob, ns, na, d->span,
-                                                                d->final_w, d->il, d->rec);
+                                                                d->final_w, d->il, d->rec,
+                                                                d->sspan);
   }
   if (hipDeviceSynchronize() != hipSuccess) {
     DeviceFst::destroy(d);
@@ -88,7 +102,7 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   uint32_t max_span = 0;
   const StateEntry* se = f.states();
   for (uint32_t i = 0; i < ns; ++i) max_span = std::max(max_span, se[i].num_arcs);
-  d->view = RhsView{d->span, d->final_w, d->il, d->rec, ns, na, h.start_state, max_span};
+  d->view = RhsView{d->span, d->final_w, d->il, d->rec, d->sspan, ns, na, h.start_state, max_span};
   d->has_eps = f.has_epsilon_input();
   d->nonneg = f.weights_nonnegative();
   d->weight_type = f.weight_type();
@@ -131,6 +145,7 @@ void DeviceFst::destroy(DeviceFst* d) {
   if (d->final_w) (void)hipFree(d->final_w);
   if (d->il) (void)hipFree(d->il);
   if (d->rec) (void)hipFree(d->rec);
+  if (d->sspan) (void)hipFree(d->sspan);
   (void)hipSetDevice(cur);
   delete d;
 }
@@ -145,6 +160,12 @@ constexpr int kElWG = 256;
 constexpr int kElFcap = 512;
 constexpr int kElHcap = 1024;
 constexpr int kElKmax = 8;  // candidates per tuple kept in registers across phases
+// eager-wave geometry (tier 1): one wavefront per string, <= 320 tuples per layer
+// (5 per lane), <= 8 same-label arcs per tuple, 512-slot LDS hash.
+constexpr int kEwEmax = 5;
+constexpr int kEwFcap = 64 * kEwEmax;
+constexpr int kEwHcap = 512;
+constexpr int kEwKmax = 5;
 
 enum Scratch : size_t {
   kCounter = 0,
@@ -185,6 +206,52 @@ void dump_debug(const uint32_t* d_dbg, uint32_t grid, hipStream_t stream) {
                    w, h[w * 8], h[w * 8 + 1], h[w * 8 + 2], h[w * 8 + 3], h[w * 8 + 4],
                    h[w * 8 + 5]);
 }
+
+#ifdef FSTAMD_DEBUG_WAIT
+// Debug builds: kernels record per-workgroup progress (FT) into fine-grained host memory,
+// which the host can read while a kernel runs or after its queue aborted.
+uint32_t* g_host_trace = nullptr;
+constexpr size_t kTraceWords = 65536 * 4;
+
+hipError_t debug_trace_arm() {
+  if (!g_host_trace) {
+    HIP_TRY(hipHostMalloc((void**)&g_host_trace, kTraceWords * 4, hipHostMallocCoherent));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_fst_trace), &g_host_trace, sizeof(g_host_trace)));
+  }
+  std::memset(g_host_trace, 0xEE, kTraceWords * 4);
+  return hipSuccess;
+}
+
+// Waits up to FSTAMD_DEBUG_WAIT_S (default 20) seconds; on a fault or a timeout prints the
+// progress of every workgroup and (timeout) exits the process, so a hang becomes a report.
+hipError_t debug_wait(hipStream_t stream, uint32_t grid, const char* what) {
+  const char* ws = std::getenv("FSTAMD_DEBUG_WAIT_S");
+  const double limit = ws ? std::atof(ws) : 20.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t e;
+  bool timed_out = false;
+  while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+      timed_out = true;
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  std::fprintf(stderr, "[fstamd dbg] %s: %s\n", what,
+               timed_out ? "TIMEOUT" : hipGetErrorString(e));
+  if (timed_out || e != hipSuccess) {
+    for (uint32_t b = 0; b < grid && b < 65536; ++b) {
+      const uint32_t* w = g_host_trace + b * 4;
+      if (w[0] != 0xEEEEEEEEu)
+        std::fprintf(stderr, "[fstamd dbg]   wg %u item %u si %d k %u phase %u\n", b, w[0],
+                     (int)w[1], w[2], w[3]);
+    }
+    std::fflush(stderr);
+    if (timed_out) std::_Exit(3);
+  }
+  return e == hipErrorNotReady ? hipSuccess : e;
+}
+#endif
 
 uint32_t next_pow2(uint64_t x) {
   uint32_t p = 1;
@@ -245,6 +312,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
   HIP_TRY(hipMemsetAsync(out.cursor, 0, sizeof(unsigned long long), stream));
   if (in.num_strings == 0) return hipSuccess;
+  // every string starts as INTERNAL: a string no kernel finished can never read as a result
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)out.status, kPathInternal, in.num_strings, stream));
 
   // Eager semantics on a layered lattice -> eager-layered engine.
   if (semantics == 1) {
@@ -255,12 +324,21 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                                                                            rhs.view.start, out);
       return hipGetLastError();
     }
-    // Tier 1: LDS tables, layers of <= kElFcap tuples (the metric's layers have <= 257).
-    const uint64_t back_cap64 = (uint64_t)(in.max_len + 1) * kElFcap;
+    // Tier 1: the 256-thread LDS kernel (layers of <= kElFcap tuples), or with
+    // FSTAMD_EAGER_TIER1=wave the one-wavefront-per-string kernel (<= kEwFcap tuples;
+    // opt-in until it is validated on hardware).
+    const char* t1 = std::getenv("FSTAMD_EAGER_TIER1");
+    const bool wg_tier = !(t1 && std::strcmp(t1, "wave") == 0);
+    const uint32_t fcap1 = wg_tier ? kElFcap : kEwFcap;
+    const uint32_t kmax1 = wg_tier ? kElKmax : kEwKmax;
+    const uint64_t back_cap64 = (uint64_t)(in.max_len + 1) * fcap1;
     const uint32_t back_cap = (uint32_t)std::min<uint64_t>(back_cap64, 1u << 22);
-    auto k1 = eager_layered_lds_kernel<kElWG, kElFcap, kElHcap, kElKmax>;
+    auto k_wg = eager_layered_lds_kernel<kElWG, kElFcap, kElHcap, kElKmax>;
+    auto k_wave = eager_wave_kernel<kEwFcap, kEwHcap, kEwEmax, kEwKmax>;
+    const int block1 = wg_tier ? kElWG : 64;
     int occ = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k1, kElWG, 0));
+    if (wg_tier) HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_wg, block1, 0));
+    else HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_wave, block1, 0));
     occ = std::max(occ, 1);
     uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)occ * num_cus_, in.num_strings);
     while (grid > 1 && (uint64_t)grid * back_cap * sizeof(uint2) > (4ull << 30)) grid /= 2;
@@ -270,8 +348,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     // Tier 2 (HBM tables) takes the strings tier 1 reports as OVERFLOW.  A layer of a
     // layered lattice holds at most one tuple per rhs state, so fcap = num_states can
     // only overflow the back-pointer slab.  Skipped when tier 1 cannot overflow.
-    const bool may_overflow = (uint64_t)rhs.view.num_states > (uint64_t)kElFcap ||
-                              back_cap64 > back_cap || rhs.view.max_span > (uint32_t)kElKmax;
+    const bool may_overflow = (uint64_t)rhs.view.num_states > (uint64_t)fcap1 ||
+                              back_cap64 > back_cap || rhs.view.max_span > kmax1;
     uint32_t* list = nullptr;
     uint32_t* count = counter + 2;
     uint32_t grid2 = 0, fcap2 = 0, hcap2 = 0, back_cap2 = 0;
@@ -296,40 +374,29 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back, back_cap,
                    watchdog_ticks()};
-    k1<<<grid, kElWG, 0, stream>>>(rhs.view, in, n, counter, lp, out);
+#ifdef FSTAMD_DEBUG_WAIT
+    HIP_TRY(debug_trace_arm());
+#endif
+    if (wg_tier) k_wg<<<grid, block1, 0, stream>>>(rhs.view, in, n, counter, lp, out);
+    else k_wave<<<grid, block1, 0, stream>>>(rhs.view, in, n, counter, lp, out);
     HIP_TRY(hipGetLastError());
-#ifdef FSTAMD_DEBUG_BOUNDS
-    std::fprintf(stderr, "[fstamd dbg] tier1 sync: %s\n", hipGetErrorString(hipStreamSynchronize(stream)));
+#ifdef FSTAMD_DEBUG_WAIT
+    HIP_TRY(debug_wait(stream, grid, "tier1"));
 #endif
     if (may_overflow) {
       collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
           out.status, in.num_strings, kPathOverflow, list, count);
       EagerLaunch lp2{list, count, 0, slab, fcap2, hcap2, back2, back_cap2, watchdog_ticks()};
-#ifdef FSTAMD_DEBUG_BOUNDS
-      static uint32_t* h_trace = nullptr;
-      if (!h_trace) {
-        HIP_TRY(hipHostMalloc((void**)&h_trace, 4096 * 16, hipHostMallocCoherent));
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_fst_trace), &h_trace, sizeof(h_trace)));
-      }
-      std::memset(h_trace, 0xEE, 4096 * 16);
-      std::fprintf(stderr, "[fstamd dbg] tier2 grid=%u fcap=%u hcap=%u back_cap=%u slab=%p back=%p\n",
-                   grid2, fcap2, hcap2, back_cap2, (void*)slab, (void*)back2);
+#ifdef FSTAMD_DEBUG_WAIT
+      HIP_TRY(debug_trace_arm());
+      std::fprintf(stderr, "[fstamd dbg] tier2 grid=%u fcap=%u hcap=%u back_cap=%u\n", grid2,
+                   fcap2, hcap2, back_cap2);
 #endif
       eager_layered_kernel<kElWG, kElFcap, kElHcap, false>
           <<<grid2, kElWG, 0, stream>>>(rhs.view, in, n, counter + 1, lp2, out);
       HIP_TRY(hipGetLastError());
-#ifdef FSTAMD_DEBUG_BOUNDS
-      {
-        const hipError_t e = hipStreamSynchronize(stream);
-        std::fprintf(stderr, "[fstamd dbg] tier2 sync: %s\n", hipGetErrorString(e));
-        for (uint32_t b = 0; b < grid2; ++b) {
-          const uint32_t* w = h_trace + b * 4;
-          if (w[0] != 0xEEEEEEEEu)
-            std::fprintf(stderr, "[fstamd dbg] wg %u item %u si %d k %u phase %u\n", b, w[0],
-                         (int)w[1], w[2], w[3]);
-        }
-        if (e != hipSuccess) return e;
-      }
+#ifdef FSTAMD_DEBUG_WAIT
+      HIP_TRY(debug_wait(stream, grid2, "tier2"));
 #endif
     }
     if (stats) {

@@ -22,12 +22,21 @@ namespace fstamd {
 
 class FrozenFst;
 
+// RhsView::sspan[s].z when the state's arcs carry more than one ilabel / no arcs.
+constexpr uint32_t kSpanMixed = 0xFFFFFFFEu;
+constexpr uint32_t kSpanNone = 0xFFFFFFFFu;
+// The device arc mirror (RhsView::rec) has kRecPad zeroed records past num_arcs, so a
+// kernel may read rec[lo + j] for any lo <= num_arcs and j < kRecPad unconditionally.
+constexpr uint32_t kRecPad = 16;
+
 // Read-only view of a device-resident rhs (the kernels' only rhs interface).
 struct RhsView {
   const uint2* span;        // [num_states] (arc_offset, num_arcs)
   const double* final_w;    // [num_states]
   const uint32_t* il;       // [num_arcs] sorted ilabels per state span
   const ArcRec* rec;        // [num_arcs] {nextstate, olabel, weight}
+  const uint4* sspan;       // [num_states] {arc_offset, num_arcs, ilabel shared by all
+                            //  arcs of the state | kSpanMixed | kSpanNone, 0}
   uint32_t num_states;
   uint32_t num_arcs;
   uint32_t start;
@@ -42,6 +51,7 @@ struct DeviceFst {
   double* final_w = nullptr;
   uint32_t* il = nullptr;
   ArcRec* rec = nullptr;
+  uint4* sspan = nullptr;
   RhsView view{};
   bool has_eps = false;
   bool nonneg = true;

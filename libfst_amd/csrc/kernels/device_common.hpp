@@ -15,6 +15,12 @@ constexpr unsigned long long kMaxU64 = ~0ull;
 // an out-of-range index is reported with device printf and clamped to 0, so a bug
 // shows up as a message instead of a GPU memory fault.  Release builds: no-op.
 #ifdef FSTAMD_DEBUG_BOUNDS
+#define FSTAMD_DEBUG_FB 1
+#define FSTAMD_DEBUG_FT 1
+#define FSTAMD_DEBUG_WAIT 1
+#endif
+
+#ifdef FSTAMD_DEBUG_FB
 __device__ __forceinline__ uint64_t fst_bound(uint64_t i, uint64_t cap, int site) {
   if (i >= cap) {
     printf("[fstamd OOB] site %d index %llu cap %llu block %u thread %u\n", site,
@@ -24,9 +30,16 @@ __device__ __forceinline__ uint64_t fst_bound(uint64_t i, uint64_t cap, int site
   return i;
 }
 #define FB(i, cap, site) fst_bound((uint64_t)(i), (uint64_t)(cap), (site))
+#else
+#define FB(i, cap, site) (i)
+#endif
+
+#if defined(FSTAMD_DEBUG_FT) || defined(FSTAMD_DEBUG_WAIT)
 // Progress trace into fine-grained host memory (survives a queue abort): thread 0 of
 // each workgroup records (item, string, layer, phase) before every phase.
 __device__ uint32_t* g_fst_trace;
+#endif
+#ifdef FSTAMD_DEBUG_FT
 __device__ __forceinline__ void fst_trace(uint32_t item, uint32_t si, uint32_t k, uint32_t ph) {
   uint32_t* t = g_fst_trace;
   if (t && threadIdx.x == 0) {
@@ -37,7 +50,6 @@ __device__ __forceinline__ void fst_trace(uint32_t item, uint32_t si, uint32_t k
 }
 #define FT(item, si, k, ph) fst_trace((item), (si), (k), (ph))
 #else
-#define FB(i, cap, site) (i)
 #define FT(item, si, k, ph) ((void)0)
 #endif
 

@@ -139,6 +139,7 @@ __device__ __forceinline__ void tbl_clear_slot(const LayerTables& T, uint32_t s)
 struct LayerShared {
   uint32_t scan[16];
   uint32_t item;
+  uint32_t expired;  // watchdog verdict of thread 0 for this item (uniform for all waves)
   uint32_t nnext;
   uint32_t flag;
   uint32_t bestp;
@@ -203,7 +204,10 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
 
   for (;;) {
     __syncthreads();
-    if (tid == 0) SH.item = atomicAdd(next_item, 1u);
+    if (tid == 0) {
+      SH.item = atomicAdd(next_item, 1u);
+      SH.expired = __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks;
+    }
     __syncthreads();
     const uint32_t item = SH.item;
     if (item >= num_items) break;
@@ -219,8 +223,9 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
                      0, 0);
       continue;
     }
-    // Watchdog: no bug may keep a workgroup resident forever (status INTERNAL).
-    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+    // Watchdog: no bug may keep a workgroup resident forever (status INTERNAL).  The
+    // verdict comes from thread 0 through LDS, so every wave takes the same path.
+    if (SH.expired) {
       if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
       continue;
     }
@@ -475,7 +480,10 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
 
   for (;;) {
     __syncthreads();
-    if (tid == 0) SH.item = atomicAdd(next_item, 1u);
+    if (tid == 0) {
+      SH.item = atomicAdd(next_item, 1u);
+      SH.expired = __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks;
+    }
     __syncthreads();
     const uint32_t item = SH.item;
     if (item >= lp.num_items) break;
@@ -489,7 +497,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
                      0, 0);
       continue;
     }
-    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+    if (SH.expired) {  // thread 0's verdict (LDS): every wave takes the same path
       if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
       continue;
     }

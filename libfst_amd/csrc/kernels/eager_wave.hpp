@@ -1,0 +1,419 @@
+// eager_wave.hpp -- eager compose + shortestPath on layered lattices, one wavefront per
+// string (gfx950 / CDNA4).  Tier 1 of the eager engine since round 1 (v3).
+//
+// Same results as eager_layered.hpp (and so as compose.zig:64-195 + shortest-path.zig:
+// 64-136, see the proof there and DESIGN.md §4.1): per layer the next tuples are the
+// distinct rhs targets in first-occurrence order of the candidates (source position,
+// arc index); d = min over candidate sums; the back-pointer is the tight candidate with
+// the smallest index; the best final is lexmin (total, position).
+//
+// Why one wave per string.  A layer of the metric holds <= 257 tuples and ~635
+// candidates: a 64-lane wave covers it with <= 5 tuples and <= 25 candidates per lane,
+// and a single wave needs no s_barrier -- LDS operations of one wave complete in order,
+// so a wavefront-scope fence (compiler ordering only) separates the phases.  The LDS
+// footprint per string is 12.6 KB (vs 39 KB for the 256-thread tier), so ~12 strings
+// are in flight per CU instead of 4, and their phases overlap.
+//
+// Per layer k (label = labels[k]); lane l owns the contiguous tuple chunk
+// [l*E, l*E + E), E = ceil(n/64), in registers (rhs state, distance, arc span), and its
+// candidates' rhs records (target, weight) were loaded at the end of layer k-1:
+//   B  insert targets into the LDS hash; atomicMin first candidate and distance
+//   C  tight candidates -> atomicMin of the packed (index, source, arc); creators counted
+//   D  ranks of created tuples (wave scan) -> rank->slot table
+//   E  each lane takes ranks [l*E', l*E' + E') of the next layer: back record to HBM,
+//      slot cleared, and the next layer's spans and arc records loaded.
+#pragma once
+
+#include "device_common.hpp"
+#include "eager_layered.hpp"  // EagerLaunch, write_status, lhash
+
+namespace fstamd {
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int FCAP, int HCAP>
+struct WaveLds {
+  uint32_t key[HCAP];              // rhs state; kEmptyKey = free
+  uint32_t first[HCAP];            // first (smallest) candidate index reaching the key
+  unsigned long long dmin[HCAP];   // okey of the minimum candidate distance
+  unsigned long long bpack[HCAP];  // (index << 48) | (source position << 32) | rhs arc of
+                                   // the tight candidate with the smallest index
+  uint16_t nslot[FCAP];            // next-layer rank -> slot
+  unsigned long long best;         // best-final reduction word
+};
+
+// Exclusive prefix sum over the wave of a value < 2^BITS, from bit-plane ballots:
+// prefix = sum_b popcount(ballot(bit b) & lanes below) << b.  No LDS, no bpermute
+// address registers; `total` is wave-uniform.
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_excl_scan_small(uint32_t v, uint32_t& total) {
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const unsigned long long m = __ballot((v >> b) & 1u);
+    pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+    tot += (uint32_t)__popcll(m) << b;
+  }
+  total = tot;
+  return pre;
+}
+
+// arcsByIlabel (src/fst.zig:112-136) with the per-state summary: one 16-B load when all
+// arcs of the state share an ilabel (or it has none), binary search otherwise.
+__device__ __forceinline__ void wave_span(const RhsView& r, uint32_t s, uint32_t label,
+                                          uint32_t& lo, uint32_t& cnt) {
+  const uint4 ss = r.sspan[FB(s, r.num_states, 30)];
+  if (ss.z == label) {
+    lo = ss.x;
+    cnt = ss.y;
+  } else if (ss.z != kSpanMixed) {
+    lo = ss.x;
+    cnt = 0;
+  } else {
+    uint32_t a, b;
+    span_by_ilabel(r, s, label, a, b);
+    lo = a;
+    cnt = b - a;
+  }
+}
+
+// Spans of the owned tuples for `label`, then the (target, weight) of their first KMAX
+// arcs.  The loads are unconditional: the arc mirror is padded by kRecPad >= KMAX records,
+// so rec[lo + j] is in bounds for any lo <= num_arcs; lanes mask what they do not own.
+template <int EMAX, int KMAX>
+__device__ __forceinline__ bool wave_load_layer(const RhsView& rhs, uint32_t label,
+                                                uint32_t first_p, uint32_t E, uint32_t n_cur,
+                                                const uint32_t (&s2)[EMAX], uint32_t (&lo)[EMAX],
+                                                uint32_t (&cnt)[EMAX], uint32_t (&ct)[EMAX][KMAX],
+                                                double (&cw)[EMAX][KMAX]) {
+  bool too_long = false;
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) {
+    uint32_t l = 0, c = 0;
+    if ((uint32_t)e < E && first_p + e < n_cur) wave_span(rhs, s2[e], label, l, c);
+    lo[e] = l;
+    cnt[e] = c;
+    too_long |= c > (uint32_t)KMAX;
+  }
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) {
+    const ArcRec* b = rhs.rec + lo[e];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+      ct[e][j] = b[j].next;
+      cw[e][j] = b[j].weight;
+    }
+  }
+  return too_long;
+}
+
+template <int FCAP, int HCAP, int EMAX, int KMAX>
+__global__ void __launch_bounds__(64, 3)
+eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
+                  EagerLaunch lp, BatchOutDev out) {
+  static_assert(FCAP == 64 * EMAX, "FCAP = 64 lanes x EMAX tuples");
+  static_assert(EMAX * KMAX <= 64, "creator mask is 64 bits");
+  static_assert(KMAX <= kRecPad, "arc mirror padding covers KMAX records");
+  static_assert(HCAP >= FCAP && (HCAP & (HCAP - 1)) == 0, "HCAP: power of two >= FCAP");
+  constexpr unsigned long long kFree = ~0ull;
+  // per-lane candidate counts are <= EMAX * KMAX
+  constexpr int kCandBits = 32 - __builtin_clz((unsigned)(EMAX * KMAX));
+  constexpr uint32_t kHbits = __builtin_ctz(HCAP);
+  __shared__ WaveLds<FCAP, HCAP> S;
+  const uint32_t lane = threadIdx.x;
+  uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+#pragma unroll 1
+  for (uint32_t i = lane; i < HCAP; i += 64) {
+    S.key[i] = kEmptyKey;
+    S.first[i] = kEmptyKey;
+    S.dmin[i] = kFree;
+    S.bpack[i] = kFree;
+  }
+  wave_lds_sync();
+
+  for (;;) {
+    // hard stop: even a wave whose control flow went wrong ends (its strings keep the
+    // INTERNAL status the host pre-fills)
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * lp.wd_ticks) return;
+    // work item: fetched by the first active lane, broadcast through an SGPR
+    uint32_t item = 0;
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
+        (uint32_t)(__ffsll((long long)__ballot(1)) - 1))
+      item = atomicAdd(next_item, 1u);
+    item = __builtin_amdgcn_readlane(item, __ffsll((long long)__ballot(1)) - 1);
+    if (item >= lp.num_items) break;
+    FT(item, 0xFFFFFFFFu, 0, 0);
+    const uint32_t si = item;
+    // every value that steers control flow is made provably wave-uniform (SGPR), so the
+    // compiler emits scalar branches and no divergent-loop structure
+    const uint64_t off0 = in.offsets[si];
+    const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
+                         __builtin_amdgcn_readfirstlane((uint32_t)off0);
+    const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)(in.offsets[si + 1] - off));
+
+    if (rhs.start == kNoState || n_best != 1) {  // compose.zig:33-35, shortest-path.zig:21-24
+      if (lane == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+      if (lane == 0) write_status(out, si, kPathInternal, 0, 0);
+      continue;
+    }
+
+    // layer 0: the start tuple, owned by lane 0
+    uint32_t n_cur = 1, E = 1, cur_base = 0;
+    uint32_t tuples = 1, relax = 0;
+    uint32_t s2[EMAX];
+    double dd[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      s2[e] = rhs.start;
+      dd[e] = w_one();
+    }
+    int32_t fail = kPathOk;
+
+    for (uint32_t k = 0; k < L; ++k) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {  // no wave stays forever
+        fail = kPathInternal;
+        tuples = 0x10000u | k;
+        relax = n_cur;
+        break;
+      }
+      FT(item, si, k, 1);
+      const uint32_t lab = __builtin_amdgcn_readfirstlane(in.labels[off + k]);
+      if (lab == kEpsilon) {  // lhs epsilon output: not a layered lattice
+        fail = kPathUnsupported;
+        break;
+      }
+      uint32_t lo[EMAX], cnt[EMAX];
+      uint32_t ct[EMAX][KMAX];
+      double cw[EMAX][KMAX];
+      if (__ballot(wave_load_layer<EMAX, KMAX>(rhs, lab, lane * E, E, n_cur, s2, lo, cnt, ct, cw))) {
+        fail = kPathOverflow;  // a span longer than KMAX: the next tier takes the string
+        break;
+      }
+      FT(item, si, k, 2);
+      // candidate index base of this lane: exclusive scan of per-lane candidate counts
+      uint32_t tsum = 0;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) tsum += cnt[e];
+      uint32_t ctot;
+      const uint32_t cbase = wave_excl_scan_small<kCandBits>(tsum, ctot);
+      relax += ctot;
+
+      // ---- (B) insert targets; first occurrence and minimum distance ----
+      // Linear probing in uniform rounds: in round r every still-pending candidate tries
+      // slot (hash + r), so no per-candidate probe state is needed besides a pending bit.
+      unsigned long long pend = 0;
+      uint32_t c = cbase;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          const double nd = w_times(dd[e], w_times(w_one(), cw[e][j]));  // compose.zig:104
+          cw[e][j] = nd;
+          if ((uint32_t)j < cnt[e]) {
+            const uint32_t t = ct[e][j];
+            const uint32_t i = lhash(t, kHbits);
+            const uint32_t old = atomicCAS(&S.key[i], kEmptyKey, t);
+            if (old == kEmptyKey || old == t) {
+              ct[e][j] = i;
+              atomicMin(&S.first[i], c + j);
+              atomicMin(&S.dmin[i], (unsigned long long)okey(nd));
+            } else {
+              pend |= 1ull << (e * KMAX + j);
+            }
+          }
+        }
+        c += cnt[e];
+      }
+      FT(item, si, k, 3);
+#pragma unroll 1
+      for (uint32_t r = 1; __ballot(pend != 0) && r < (uint32_t)HCAP; ++r) {
+        c = cbase;
+#pragma unroll
+        for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+          for (int j = 0; j < KMAX; ++j) {
+            if (pend & (1ull << (e * KMAX + j))) {
+              const uint32_t t = ct[e][j];
+              const uint32_t i = (lhash(t, kHbits) + r) & (HCAP - 1);
+              const uint32_t old = atomicCAS(&S.key[i], kEmptyKey, t);
+              if (old == kEmptyKey || old == t) {
+                ct[e][j] = i;
+                atomicMin(&S.first[i], c + j);
+                atomicMin(&S.dmin[i], (unsigned long long)okey(cw[e][j]));
+                pend &= ~(1ull << (e * KMAX + j));
+              }
+            }
+          }
+          c += cnt[e];
+        }
+      }
+      if (__ballot(pend != 0)) {  // table full
+        fail = kPathOverflow;
+        break;
+      }
+      wave_lds_sync();
+
+      FT(item, si, k, 4);
+      // ---- (C) tight candidates -> packed back-pointer; creators ----
+      unsigned long long creators = 0;
+      uint32_t nf = 0;
+      c = cbase;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if ((uint32_t)j < cnt[e]) {
+            const uint32_t slot = ct[e][j];
+            const uint32_t ci = c + j;
+            if (okey(cw[e][j]) == S.dmin[slot])
+              atomicMin(&S.bpack[slot], ((unsigned long long)ci << 48) |
+                                            ((unsigned long long)(lane * E + e) << 32) |
+                                            (lo[e] + j));
+            if (S.first[slot] == ci) {
+              creators |= 1ull << (e * KMAX + j);
+              ++nf;
+            }
+          }
+        }
+        c += cnt[e];
+      }
+      uint32_t n_next;
+      const uint32_t fex = wave_excl_scan_small<kCandBits>(nf, n_next);
+      if (n_next > (uint32_t)FCAP || (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
+        fail = kPathOverflow;
+        break;
+      }
+
+      FT(item, si, k, 5);
+      // ---- (D) ranks of the created tuples (candidate order) ----
+      uint32_t rank = fex;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          if (creators & (1ull << (e * KMAX + j))) S.nslot[rank++] = (uint16_t)ct[e][j];
+        }
+      }
+      wave_lds_sync();
+
+      FT(item, si, k, 6);
+      // ---- (E) next layer: back records, slot reset, spans and arc records ----
+      const uint32_t next_base = cur_base + n_cur;
+      const uint32_t En = (n_next + 63) / 64;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        const uint32_t r = lane * En + e;
+        const bool own = (uint32_t)e < En && r < n_next;
+        const uint32_t slot = S.nslot[own ? r : 0];
+        const uint32_t key = S.key[slot];
+        const unsigned long long dm = S.dmin[slot];
+        const unsigned long long bp = S.bpack[slot];
+        s2[e] = key;
+        dd[e] = from_okey(dm);
+        if (own) {
+          back[FB(next_base + r, lp.back_cap, 32)] =
+              make_uint2(cur_base + (uint32_t)((bp >> 32) & 0xFFFFu), (uint32_t)bp);
+          S.key[slot] = kEmptyKey;
+          S.first[slot] = kEmptyKey;
+          S.dmin[slot] = kFree;
+          S.bpack[slot] = kFree;
+        }
+      }
+      cur_base = next_base;
+      n_cur = n_next;
+      E = En;
+      tuples += n_next;
+      wave_lds_sync();
+    }
+
+    if (fail != kPathOk) {
+      // leave the table clean for the next string
+      wave_lds_sync();
+#pragma unroll 1
+      for (uint32_t i = lane; i < HCAP; i += 64) {
+        S.key[i] = kEmptyKey;
+        S.first[i] = kEmptyKey;
+        S.dmin[i] = kFree;
+        S.bpack[i] = kFree;
+      }
+      wave_lds_sync();
+      if (lane == 0) write_status(out, si, fail, tuples, relax);
+      continue;
+    }
+
+    FT(item, si, L, 7);
+    // ---- best final: lexmin (total, position) over the last layer (shortest-path.zig:88-104)
+    unsigned long long mykey = kMaxU64;
+    uint32_t myp = kEmptyKey;
+    double myfw = 0.0;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      const uint32_t p = lane * E + e;
+      if ((uint32_t)e < E && p < n_cur) {
+        const double fw2 = rhs.final_w[FB(s2[e], rhs.num_states, 33)];
+        if (!w_is_zero(dd[e]) && !w_is_zero(fw2)) {
+          const unsigned long long kk = okey(w_times(dd[e], w_times(w_one(), fw2)));
+          if (kk < mykey) {  // e ascending: equal keys keep the lower position
+            mykey = kk;
+            myp = p;
+            myfw = fw2;
+          }
+        }
+      }
+    }
+    if (lane == 0) S.best = kMaxU64;
+    wave_lds_sync();
+    if (mykey != kMaxU64) atomicMin(&S.best, mykey);
+    wave_lds_sync();
+    const unsigned long long best = S.best;
+    const unsigned long long hit = __ballot(best != kMaxU64 && mykey == best);
+    const uint32_t blane = hit ? (uint32_t)(__ffsll((long long)hit) - 1) : 0u;
+    const uint32_t bp = __builtin_amdgcn_readlane(myp, blane);
+    const unsigned long long fwb = __builtin_amdgcn_readlane(
+        (long long)__double_as_longlong(myfw), blane);
+    const double fw2 = __longlong_as_double((long long)fwb);
+
+    if (lane == 0) {
+      if (!hit) {
+        write_status(out, si, kPathEmpty, tuples, relax);
+      } else {
+        const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
+        if (o + L > out.arc_cap) {
+          write_status(out, si, kPathOutputFull, tuples, relax);
+        } else {
+          FT(item, si, L, 8);
+          uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
+          for (uint32_t k = L; k > 0; --k) {
+            const uint2 b = back[FB(id, lp.back_cap, 34)];
+            const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
+            out.out_il[o + k - 1] = in.labels[off + k - 1];
+            out.out_ol[o + k - 1] = r.olabel;
+            out.out_w[o + k - 1] = w_times(w_one(), r.weight);
+            id = b.x;
+          }
+          out.status[si] = kPathOk;
+          out.path_len[si] = L;
+          out.path_off[si] = o;
+          out.final_w[si] = w_times(w_one(), fw2);  // compose.zig:73: fw1 (0) (x) fw2
+          if (out.work) {
+            out.work[2 * si] = tuples;
+            out.work[2 * si + 1] = relax;
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace fstamd

@@ -16,7 +16,8 @@ from dataclasses import dataclass
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libfst_amd.so")
+# LIBFST_AMD_LIB: an alternate build of the same library (A/B runs of kernel variants).
+LIB_PATH = os.environ.get("LIBFST_AMD_LIB") or os.path.join(PKG_DIR, "libfst_amd.so")
 
 FST_NO_STATE = 0xFFFFFFFF
 FST_EPSILON = 0
