@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -201,6 +202,58 @@ MutableFst chain_result(const HostPaths& h, uint32_t i) {
   return r;
 }
 
+// A MutableFst uploaded as CSR (arcs in insertion order): the lhs of the single-call
+// compose entries, or the FST itself for fst_shortest_path.
+struct GraphUpload {
+  DevBuf off, il, ol, w, nx, fin;
+  GraphInput g{};
+  bool ok = false;
+  bool nonneg = true;  // every arc and final weight >= +0.0 (no -0.0, no NaN)
+  explicit GraphUpload(const MutableFst& a)
+      : off((a.num_states() + 1) * 4ull), il(a.total_arcs() * 4), ol(a.total_arcs() * 4),
+        w(a.total_arcs() * 8), nx(a.total_arcs() * 4), fin(a.num_states() * 8ull) {
+    const uint32_t ns = (uint32_t)a.num_states();
+    std::vector<uint32_t> soff(ns + 1, 0), vil, vol, vnx;
+    std::vector<double> vw, vfin(ns);
+    uint32_t maxdeg = 0;
+    auto neg = [](double x) { return x < 0.0 || std::isnan(x) || (x == 0.0 && std::signbit(x)); };
+    for (uint32_t s = 0; s < ns; ++s) {
+      soff[s] = (uint32_t)vil.size();
+      vfin[s] = a.final_weight(s);
+      if (neg(vfin[s])) nonneg = false;
+      maxdeg = std::max<uint32_t>(maxdeg, (uint32_t)a.arcs(s).size());
+      for (const Arc& x : a.arcs(s)) {
+        vil.push_back(x.ilabel);
+        vol.push_back(x.olabel);
+        vw.push_back(x.weight);
+        vnx.push_back(x.nextstate);
+        if (neg(x.weight)) nonneg = false;
+      }
+    }
+    soff[ns] = (uint32_t)vil.size();
+    const size_t na = vil.size();
+    if (!off.p || !il.p || !ol.p || !w.p || !nx.p || !fin.p) return;
+    bool good = hipMemcpy(off.p, soff.data(), (ns + 1) * 4ull, hipMemcpyHostToDevice) == hipSuccess;
+    if (na) {
+      good = good && hipMemcpy(il.p, vil.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(ol.p, vol.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(w.p, vw.data(), na * 8, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(nx.p, vnx.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (ns) good = good && hipMemcpy(fin.p, vfin.data(), ns * 8ull, hipMemcpyHostToDevice) == hipSuccess;
+    g.state_off = (const uint32_t*)off.p;
+    g.arc_il = (const uint32_t*)il.p;
+    g.arc_ol = (const uint32_t*)ol.p;
+    g.arc_w = (const double*)w.p;
+    g.arc_next = (const uint32_t*)nx.p;
+    g.final_w = (const double*)fin.p;
+    g.num_states = ns;
+    g.start = a.start();
+    g.max_outdeg = maxdeg;
+    ok = good;
+  }
+};
+
 // Lazy 1-best of one general lhs on the GPU (single-call C ABI path).
 int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* result,
                     double* kernel_ms) {
@@ -208,45 +261,9 @@ int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* r
   if (dev < 0) return -1;
   DeviceFst* D = b.device(dev);
   if (!D) return -1;
-  // CSR of the lhs, arcs in insertion order.
-  const uint32_t ns = (uint32_t)a.num_states();
-  std::vector<uint32_t> soff(ns + 1, 0), il, ol, nx;
-  std::vector<double> w, fin(ns);
-  uint32_t maxdeg = 0;
-  for (uint32_t s = 0; s < ns; ++s) {
-    soff[s] = (uint32_t)il.size();
-    fin[s] = a.final_weight(s);
-    maxdeg = std::max<uint32_t>(maxdeg, (uint32_t)a.arcs(s).size());
-    for (const Arc& x : a.arcs(s)) {
-      il.push_back(x.ilabel);
-      ol.push_back(x.olabel);
-      w.push_back(x.weight);
-      nx.push_back(x.nextstate);
-    }
-  }
-  soff[ns] = (uint32_t)il.size();
-  const size_t na = il.size();
-  DevBuf d_off((ns + 1) * 4ull), d_il(na * 4), d_ol(na * 4), d_w(na * 8), d_nx(na * 4),
-      d_fin(ns * 8ull);
-  if (!d_off.p || !d_il.p || !d_ol.p || !d_w.p || !d_nx.p || !d_fin.p) return -1;
-  (void)hipMemcpy(d_off.p, soff.data(), (ns + 1) * 4ull, hipMemcpyHostToDevice);
-  if (na) {
-    (void)hipMemcpy(d_il.p, il.data(), na * 4, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_ol.p, ol.data(), na * 4, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_w.p, w.data(), na * 8, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_nx.p, nx.data(), na * 4, hipMemcpyHostToDevice);
-  }
-  if (ns) (void)hipMemcpy(d_fin.p, fin.data(), ns * 8ull, hipMemcpyHostToDevice);
-  GraphInput g{};
-  g.state_off = (const uint32_t*)d_off.p;
-  g.arc_il = (const uint32_t*)d_il.p;
-  g.arc_ol = (const uint32_t*)d_ol.p;
-  g.arc_w = (const double*)d_w.p;
-  g.arc_next = (const uint32_t*)d_nx.p;
-  g.final_w = (const double*)d_fin.p;
-  g.num_states = ns;
-  g.start = a.start();
-  g.max_outdeg = maxdeg;
+  GraphUpload up(a);
+  if (!up.ok) return -1;
+  GraphInput g = up.g;
   DeviceEngine& E = DeviceEngine::get(dev);
   std::lock_guard<std::mutex> lk(E.mutex());
   // Grow the tuple capacity on overflow (the reference has no limit but memory).
@@ -560,23 +577,102 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
 }
 
 FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handle) {
-  // Eager lattice output (src/ops/compose.zig:29-198) needs the general eager
-  // engine, which is not built yet.  Validate arguments like the
-  // reference, then report an error rather than computing on the CPU.
+  // src/c-api.zig:675-742 -> src/ops/compose.zig:29-198 on the GPU (kernels/eager_bfs.hpp):
+  // the whole lattice, states numbered in BFS discovery order, arcs in compose order.
+  const auto t0 = std::chrono::steady_clock::now();
+  auto us = [&] {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  };
+  std::shared_ptr<MutableFst> a;
+  std::shared_ptr<FrozenFst> b;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    auto ha = g_mut.get(a_handle);
+    if (!ha) {
+      trace("invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
+      return kInvalid;
+    }
+    a = std::make_shared<MutableFst>(*ha);  // snapshot (c-api.zig:686)
+    b = g_fst.get(b_handle);                // pin (c-api.zig:691)
+    if (!b) {
+      trace("invalid_b", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(), 0);
+      return kInvalid;
+    }
+  }
+  if (!gpu_available()) return kInvalid;
+  const int dev = current_device();
+  DeviceFst* D = dev >= 0 ? b->device(dev) : nullptr;
+  if (!D) return kInvalid;
+  GraphUpload up(*a);
+  if (!up.ok) return kInvalid;
+  HostLattice lat;
+  LaunchStats st;
+  {
+    DeviceEngine& E = DeviceEngine::get(dev);
+    std::lock_guard<std::mutex> lk(E.mutex());
+    if (E.compose_lattice(*D, up.g, &lat, &st) != hipSuccess || lat.status != kPathOk) {
+      trace("compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(),
+            st.kernel_ms);
+      return kInvalid;
+    }
+  }
+  t_last_stats = st;
+  MutableFst result;
+  if (lat.n_nodes > 0) {
+    result.add_states(lat.n_nodes);
+    result.set_start(0);
+    for (uint32_t s2 = 0; s2 < lat.n_nodes; ++s2) {
+      if (!w_is_zero(lat.nfin[s2])) result.set_final(s2, lat.nfin[s2]);
+      for (uint32_t k = lat.aoff[s2]; k < lat.aoff[s2 + 1]; ++k)
+        result.add_arc(s2, Arc{lat.ail[k], lat.aol[k], lat.aw[k], lat.anext[k]});
+    }
+  }
+  trace("ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
+        result.total_arcs(), us(), st.kernel_ms);
   std::lock_guard<std::mutex> g(g_api_mu);
-  if (!g_mut.get(a_handle) || !g_fst.get(b_handle)) return kInvalid;
-  if (trace_enabled())
-    std::fprintf(stderr, "[libfst_amd] fst_compose_frozen: lattice output not implemented\n");
-  return kInvalid;
+  return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
 FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
+  // src/c-api.zig:897-916 -> src/ops/shortest-path.zig:18-139 on the GPU.
+  std::shared_ptr<MutableFst> m;
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    auto h = g_mut.get(handle);
+    if (!h) return kInvalid;
+    m = std::make_shared<MutableFst>(*h);  // snapshot
+  }
+  MutableFst result;
+  if (m->start() == kNoState || n == 0) {  // :21-23 -> empty
+  } else if (n != 1) {                     // :24 UnsupportedNShortest
+    return kInvalid;
+  } else {
+    if (!gpu_available()) return kInvalid;
+    const int dev = current_device();
+    if (dev < 0) return kInvalid;
+    GraphUpload up(*m);
+    // The GPU 1-best is exact for non-negative weights (eager_bfs.hpp); a negative
+    // weight (Dijkstra replay) is not covered yet: reported as an error.
+    if (!up.ok || !up.nonneg) return kInvalid;
+    const uint64_t cap = std::max<uint64_t>(m->num_states() + 16, 1024);
+    DevOut out(1, cap);
+    if (!out.ok()) return kInvalid;
+    LaunchStats st;
+    HostPaths hp;
+    {
+      DeviceEngine& E = DeviceEngine::get(dev);
+      std::lock_guard<std::mutex> lk(E.mutex());
+      if (E.shortest_path_graph(up.g, n, out.v, &st) != hipSuccess) return kInvalid;
+      if (!out.download(1, &hp)) return kInvalid;
+    }
+    t_last_stats = st;
+    if (hp.status[0] == kPathCycle || hp.status[0] == kPathInternal ||
+        hp.status[0] == kPathOutputFull)
+      return kInvalid;
+    result = chain_result(hp, 0);  // OK or EMPTY
+  }
   std::lock_guard<std::mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
-  if (!m) return kInvalid;
-  if (m->start() == kNoState || n == 0) return g_mut.insert(std::make_shared<MutableFst>());
-  if (n != 1) return kInvalid;
-  return kInvalid;  // general-lattice 1-best: see DESIGN.md §8 (next)
+  return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
 // ---- Strings ------------------------------------------------------------------------

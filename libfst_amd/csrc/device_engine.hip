@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "host_fst.hpp"
+#include "kernels/eager_bfs.hpp"
 #include "kernels/eager_layered.hpp"
 #include "kernels/eager_wave.hpp"
 #include "kernels/lazy_wave.hpp"
@@ -182,6 +183,10 @@ enum Scratch : size_t {
   kDebug,
   kElSlab,
   kElBack2,
+  kBfsSlab,
+  kBfsHdr,
+  kBfsList,
+  kBfsList2,
   kNumScratch
 };
 
@@ -317,12 +322,24 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
 
   // Eager semantics on a layered lattice -> eager-layered engine.
   if (semantics == 1) {
-    if (rhs.has_eps || !rhs.nonneg) {
-      // Not layered (rhs epsilon arcs), or negative weights (Dijkstra on the
-      // lattice is then not the exact SSSP the layered kernel computes).
+    if (!rhs.nonneg) {
+      // Negative weights: shortest-path.zig's Dijkstra is then not the exact SSSP the
+      // eager engines compute (an exact replay is future work): UNSUPPORTED.
       mark_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(in.num_strings, n,
                                                                            rhs.view.start, out);
       return hipGetLastError();
+    }
+    if (rhs.has_eps) {  // not layered: the general BFS engine takes every string
+      if (stats) {
+        stats->engine = 2;
+        HIP_TRY(hipEventRecord(ev0_, stream));
+      }
+      HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, true));
+      if (stats) {
+        HIP_TRY(hipEventRecord(ev1_, stream));
+        HIP_TRY(finish_stats(ev0_, ev1_, stats));
+      }
+      return hipSuccess;
     }
     // Tier 1: the 256-thread LDS kernel (layers of <= kElFcap tuples), or with
     // FSTAMD_EAGER_TIER1=wave the one-wavefront-per-string kernel (<= kEwFcap tuples;
@@ -399,6 +416,9 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       HIP_TRY(debug_wait(stream, grid2, "tier2"));
 #endif
     }
+    // Strings the layered tiers cannot take (label-0 inputs -> UNSUPPORTED, tier-2
+    // OVERFLOW) go to the general BFS engine.
+    HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, false));
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
@@ -459,6 +479,213 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     HIP_TRY(finish_stats(ev0_, ev1_, stats));
   }
   return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------
+// General eager engine (kernels/eager_bfs.hpp)
+// ---------------------------------------------------------------------------------
+
+namespace {
+// Per-string workspace tiers: nodes / arcs grow x16 until one slab would exceed the
+// budget.  Tier 0 covers every metric-like string; eps-dense T=4096 L=96 (781K tuples,
+// 10M arcs) needs tier 1.
+constexpr uint32_t kBfsNcap0 = 1u << 16;
+constexpr uint32_t kBfsAcap0 = 1u << 20;
+constexpr uint64_t kBfsBudget = 40ull << 30;  // bytes of BFS workspace per launch
+constexpr int kBfsWG = 256;
+
+struct BfsCaps {
+  uint32_t ncap, acap, hcap, lcap;
+  size_t stride;
+};
+BfsCaps bfs_caps(int tier) {
+  BfsCaps c;
+  uint64_t n = (uint64_t)kBfsNcap0 << (4 * tier), a = (uint64_t)kBfsAcap0 << (4 * tier);
+  c.ncap = (uint32_t)std::min<uint64_t>(n, 1u << 30);
+  c.acap = (uint32_t)std::min<uint64_t>(a, 0x7FFFFFFFu);
+  c.hcap = next_pow2(2ull * c.ncap);
+  c.lcap = c.ncap;
+  c.stride = bfs_slab_bytes(c.ncap, c.acap, c.hcap, c.lcap);
+  return c;
+}
+}  // namespace
+
+__global__ void collect_status2_kernel(const int32_t* status, uint32_t num, int32_t a, int32_t b,
+                                       uint32_t* list, uint32_t* count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < num && (status[i] == a || status[i] == b)) list[atomicAdd(count, 1u)] = i;
+}
+
+__global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_count,
+                                    const int32_t* status, int32_t code, uint32_t* list,
+                                    uint32_t* count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < *in_count && status[in_list[i]] == code) list[atomicAdd(count, 1u)] = in_list[i];
+}
+
+hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                       const BatchOutDev& out, hipStream_t stream, bool all) {
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, 64);  // [8..15] are ours
+  uint32_t* list = (uint32_t*)scratch(kBfsList, (size_t)in.num_strings * 4);
+  uint32_t* list2 = (uint32_t*)scratch(kBfsList2, (size_t)in.num_strings * 4);
+  if (!ctr || !list || !list2) return hipErrorOutOfMemory;
+  uint32_t* cnt = ctr + 8;
+  HIP_TRY(hipMemsetAsync(cnt, 0, 32, stream));
+  const uint32_t blocks = (in.num_strings + 255) / 256;
+  if (all) {
+    mark_status_kernel<<<blocks, 256, 0, stream>>>(in.num_strings, 1, rhs.view.start, out);
+    collect_status2_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
+                                                       kPathUnsupported, kPathUnsupported, list,
+                                                       cnt);
+  } else {
+    collect_status2_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
+                                                       kPathUnsupported, kPathOverflow, list, cnt);
+  }
+  HIP_TRY(hipGetLastError());
+  uint32_t count = 0;
+  HIP_TRY(hipMemcpyAsync(&count, cnt, 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  for (int tier = 0; count > 0; ++tier) {
+    const BfsCaps c = bfs_caps(tier);
+    const uint64_t fit = std::max<uint64_t>(1, kBfsBudget / c.stride);
+    if (kBfsBudget < c.stride) break;  // beyond the budget: those strings stay OVERFLOW
+    const uint32_t grid = (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_, fit});
+    BfsWs ws{};
+    ws.slab = (uint8_t*)scratch(kBfsSlab, (size_t)grid * c.stride);
+    ws.hdr = (uint32_t*)scratch(kBfsHdr, (size_t)grid * 8 * 4);
+    if (!ws.slab || !ws.hdr) return hipErrorOutOfMemory;
+    ws.stride = c.stride;
+    ws.ncap = c.ncap;
+    ws.acap = c.acap;
+    ws.hcap = c.hcap;
+    ws.lcap = c.lcap;
+    ws.wd_ticks = watchdog_ticks();
+    ws.lattice_only = 0;
+    HIP_TRY(hipMemsetAsync(cnt + 1, 0, 8, stream));  // item counter + next list count
+    GraphInput none{};
+    eager_bfs_kernel<kBfsWG, false><<<grid, kBfsWG, 0, stream>>>(
+        rhs.view, in, none, n, cnt + 1, list, cnt, 0, ws, out);
+    HIP_TRY(hipGetLastError());
+    // strings that overflowed this tier move on to the next one
+    collect_list_kernel<<<(count + 255) / 256, 256, 0, stream>>>(list, cnt, out.status,
+                                                                 kPathOverflow, list2, cnt + 2);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&count, cnt + 2, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(cnt, cnt + 2, 4, hipMemcpyDeviceToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::swap(list, list2);
+  }
+  return hipSuccess;
+}
+
+hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput& lhs,
+                                         HostLattice* lat, LaunchStats* stats) {
+  HIP_TRY(hipSetDevice(dev_));
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, 64);
+  if (!ctr) return hipErrorOutOfMemory;
+  BatchOutDev none_out{};
+  for (int tier = 0;; ++tier) {
+    const BfsCaps c = bfs_caps(tier);
+    if (c.stride > kBfsBudget) {
+      lat->status = kPathOverflow;
+      return hipSuccess;
+    }
+    BfsWs ws{};
+    ws.slab = (uint8_t*)scratch(kBfsSlab, c.stride);
+    ws.hdr = (uint32_t*)scratch(kBfsHdr, 8 * 4);
+    if (!ws.slab || !ws.hdr) return hipErrorOutOfMemory;
+    ws.stride = c.stride;
+    ws.ncap = c.ncap;
+    ws.acap = c.acap;
+    ws.hcap = c.hcap;
+    ws.lcap = c.lcap;
+    ws.wd_ticks = watchdog_ticks();
+    ws.lattice_only = 1;
+    HIP_TRY(hipMemset(ctr, 0, 64));
+    if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
+    ChainInput none{};
+    eager_bfs_kernel<kBfsWG, true><<<1, kBfsWG, 0, nullptr>>>(rhs.view, none, lhs, 1, ctr,
+                                                              nullptr, nullptr, 1, ws, none_out);
+    HIP_TRY(hipGetLastError());
+    if (stats) {
+      HIP_TRY(hipEventRecord(ev1_, nullptr));
+      HIP_TRY(finish_stats(ev0_, ev1_, stats));
+      stats->engine = 2;
+      stats->grid = 1;
+      stats->launches = tier + 1;
+    }
+    uint32_t hdr[8];
+    HIP_TRY(hipMemcpy(hdr, ws.hdr, sizeof(hdr), hipMemcpyDeviceToHost));
+    lat->status = (int32_t)hdr[3];
+    if (lat->status == kPathOverflow) continue;
+    lat->n_nodes = hdr[0];
+    lat->n_arcs = hdr[1];
+    if (lat->status != kPathOk) return hipSuccess;
+    // copy the lattice out of the slab (same carve as the kernel)
+    const size_t N = lat->n_nodes, A = lat->n_arcs;
+    lat->aoff.resize(N + 1);
+    lat->nfin.resize(N);
+    lat->anext.resize(A);
+    lat->ail.resize(A);
+    lat->aol.resize(A);
+    lat->aw.resize(A);
+    if (N == 0) {
+      lat->aoff.assign(1, 0);
+      return hipSuccess;
+    }
+    auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    uint8_t* p = ws.slab;
+    const size_t o_hkey = 0, o_hval = o_hkey + r((size_t)c.hcap * 8),
+                 o_nkey = o_hval + r((size_t)c.hcap * 4), o_aoff = o_nkey + r((size_t)c.ncap * 8),
+                 o_lvl = o_aoff + r(((size_t)c.ncap + 1) * 4),
+                 o_nd = o_lvl + r(((size_t)c.lcap + 2) * 4), o_nback = o_nd + r((size_t)c.ncap * 8),
+                 o_nfin = o_nback + r((size_t)c.ncap * 8), o_anext = o_nfin + r((size_t)c.ncap * 8),
+                 o_ail = o_anext + r((size_t)c.acap * 4), o_aol = o_ail + r((size_t)c.acap * 4),
+                 o_aw = o_aol + r((size_t)c.acap * 4);
+    HIP_TRY(hipMemcpy(lat->aoff.data(), p + o_aoff, (N + 1) * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lat->nfin.data(), p + o_nfin, N * 8, hipMemcpyDeviceToHost));
+    if (A) {
+      HIP_TRY(hipMemcpy(lat->anext.data(), p + o_anext, A * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(lat->ail.data(), p + o_ail, A * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(lat->aol.data(), p + o_aol, A * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(lat->aw.data(), p + o_aw, A * 8, hipMemcpyDeviceToHost));
+    }
+    return hipSuccess;
+  }
+}
+
+hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
+                                             const BatchOutDev& out, LaunchStats* stats) {
+  HIP_TRY(hipSetDevice(dev_));
+  const uint32_t N = g.num_states;
+  // work arrays: distances, back-pointers, the one "level" [0, N)
+  uint8_t* w = (uint8_t*)scratch(kBfsSlab, (size_t)N * 16 + 256);
+  uint32_t* lv = (uint32_t*)scratch(kBfsHdr, 16);
+  if (!w || !lv) return hipErrorOutOfMemory;
+  const uint32_t lvh[2] = {0, N};
+  HIP_TRY(hipMemcpy(lv, lvh, 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(out.cursor, 0, 8));
+  BfsTables T{};
+  T.aoff = const_cast<uint32_t*>(g.state_off);
+  T.anext = const_cast<uint32_t*>(g.arc_next);
+  T.ail = const_cast<uint32_t*>(g.arc_il);
+  T.aol = const_cast<uint32_t*>(g.arc_ol);
+  T.aw = const_cast<double*>(g.arc_w);
+  T.nfin = const_cast<double*>(g.final_w);
+  T.lvl = lv;
+  T.nd = (unsigned long long*)w;
+  T.nback = (unsigned long long*)(w + (size_t)N * 8);
+  if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
+  sp_graph_kernel<kBfsWG><<<1, kBfsWG, 0, nullptr>>>(T, N, g.start, n, out, watchdog_ticks());
+  HIP_TRY(hipGetLastError());
+  if (stats) {
+    HIP_TRY(hipEventRecord(ev1_, nullptr));
+    HIP_TRY(finish_stats(ev0_, ev1_, stats));
+    stats->engine = 2;
+    stats->grid = 1;
+    stats->launches = 1;
+  }
+  return hipDeviceSynchronize();
 }
 
 hipError_t DeviceEngine::run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n,

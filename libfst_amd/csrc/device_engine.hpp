@@ -97,6 +97,14 @@ struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
   uint32_t ncap;           // product-tuple capacity for this run (power of two)
 };
 
+// Lattice of one fst_compose_frozen call, downloaded from the device (CSR by source id).
+struct HostLattice {
+  int32_t status = 0;  // PathStatus of the compose (kPathOk or kPathOverflow/kPathInternal)
+  uint32_t n_nodes = 0, n_arcs = 0;
+  std::vector<uint32_t> aoff, anext, ail, aol;
+  std::vector<double> aw, nfin;
+};
+
 struct LaunchStats {
   double kernel_ms = 0;
   uint32_t launches = 0;
@@ -116,12 +124,24 @@ class DeviceEngine {
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
   hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
+  // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp).
+  hipError_t compose_lattice(const DeviceFst& rhs, const GraphInput& lhs, HostLattice* lat,
+                             LaunchStats* stats);
+  // fst_shortest_path on an explicit graph; `g` holds the FST itself (CSR, arcs in
+  // insertion order).  Non-negative weights only (the caller checks).
+  hipError_t shortest_path_graph(const GraphInput& g, uint32_t n, const BatchOutDev& out,
+                                 LaunchStats* stats);
 
   int dev() const { return dev_; }
   std::mutex& mutex() { return mu_; }
 
  private:
   explicit DeviceEngine(int dev);
+  // General eager engine over the strings of `in` whose status is UNSUPPORTED or
+  // OVERFLOW after the layered tiers (all strings when `all`); grows its per-string
+  // workspace in tiers.  Synchronises on `stream` to size the tiers.
+  hipError_t run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                           const BatchOutDev& out, hipStream_t stream, bool all);
   void* scratch(size_t idx, size_t bytes);
   int dev_;
   int num_cus_ = 0;

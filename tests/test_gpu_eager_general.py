@@ -1,0 +1,157 @@
+"""GPU parity of the general eager engine (kernels/eager_bfs.hpp) with the CPU oracle.
+
+* fst_compose_frozen: the whole lattice (state numbering, arc order, labels, weight bits,
+  finals) must equal src/ops/compose.zig's (oracle or_compose);
+* fst_shortest_path: src/ops/shortest-path.zig (oracle or_shortest_path), non-negative
+  weights; a back-pointer cycle (the reference would not terminate) -> invalid handle;
+* batch eager semantics on lattices the layered kernels do not take (rhs epsilons,
+  label-0 inputs), bit-exact against oracle compose + shortestPath.
+"""
+import numpy as np
+import pytest
+
+import libfst_amd as F
+import oracle_ffi as O
+from test_gpu_parity import EAGER, LAZY, bits, check, csr, load_blob, random_rhs, to_product
+
+pytestmark = pytest.mark.gpu
+
+
+def lattice_lists(f):
+    start, finals, arcs = f.to_lists()
+    return (start, [int(bits([x])[0]) for x in finals],
+            [[(a, b, int(bits([w])[0]), d) for (a, b, w, d) in al] for al in arcs])
+
+
+def oracle_lists(f: O.Fst):
+    return (f.start, [int(bits([x])[0]) for x in f.finals],
+            [[(a, b, int(bits([w])[0]), d) for (a, b, w, d) in al] for al in f.arcs])
+
+
+def compare_compose(lhs: O.Fst, blob: bytes):
+    rc, ref = O.compose(lhs, blob)
+    assert rc == O.OR_OK
+    got = F.compose_frozen(to_product(lhs), load_blob(blob))
+    assert got is not None
+    g, r = lattice_lists(got), oracle_lists(ref)
+    assert g[0] == r[0]
+    assert len(g[1]) == len(r[1])
+    assert g[1] == r[1]
+    assert g[2] == r[2]
+
+
+# ---------------------------------------------------------------------------------------
+# fst_compose_frozen
+# ---------------------------------------------------------------------------------------
+
+def test_compose_known_answers():
+    # compose.zig:223 (a -> b -> c), :282 (no final), :311 (frozen rhs)
+    ab = O.compile_string_transducer(b"a", b"b")
+    bc = O.freeze(O.compile_string_transducer(b"b", b"c"))
+    compare_compose(ab, bc)
+    nofinal = O.Fst()
+    nofinal.add_state(float("inf"))
+    nofinal.add_state(float("inf"))
+    nofinal.start = 0
+    nofinal.add_arc(0, 98, 98, 0.5, 1)
+    compare_compose(O.compile_string(b"a"), O.freeze(nofinal))
+    compare_compose(O.compile_string(b"123"), O.freeze(O.compile_string_transducer(b"123", b"abc")))
+
+
+def test_compose_empty_sides():
+    empty = O.Fst()
+    compare_compose(O.compile_string(b"ab"), O.freeze(empty))
+    got = F.compose_frozen(F.MutableFst(), load_blob(O.freeze(O.compile_string(b"ab"))))
+    assert got is not None and got.num_states() == 0
+
+
+@pytest.mark.parametrize("L", [0, 1, 5, 17])
+def test_compose_chain_vs_epsilon_dense(L):
+    # config 1's shape (eager compose of a repeat string against eps-dense), small T
+    compare_compose(chain_of([1] * L), O.freeze(O.gen("eps_dense", 48, 12)))
+
+
+def chain_of(labels):
+    f = O.Fst()
+    for _ in range(len(labels) + 1):
+        f.add_state(float("inf"))
+    f.start = 0
+    f.finals[len(labels)] = 0.0
+    for i, x in enumerate(labels):
+        f.add_arc(i, x, x, 0.0, i + 1)
+    return f
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_compose_random_with_epsilons(seed):
+    rng = np.random.default_rng(5000 + seed)
+    lhs = random_rhs(rng, int(rng.integers(1, 12)), int(rng.integers(1, 40)), 3, eps=True)
+    rhs = random_rhs(rng, int(rng.integers(1, 25)), int(rng.integers(1, 90)), 3, eps=True,
+                     frac=seed % 2 == 1)
+    compare_compose(lhs, O.freeze(rhs))
+
+
+# ---------------------------------------------------------------------------------------
+# fst_shortest_path on explicit FSTs
+# ---------------------------------------------------------------------------------------
+
+def compare_sp(f: O.Fst, n=1):
+    rc, ref = O.shortest_path(f, n)
+    got = F.shortest_path(to_product(f), n)
+    if rc in (O.OR_ERR_UNSUPPORTED_N, O.OR_ERR_CYCLE):
+        assert got is None
+        return
+    assert rc == O.OR_OK and got is not None
+    assert lattice_lists(got) == oracle_lists(ref)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_shortest_path_random_graphs(seed):
+    rng = np.random.default_rng(6000 + seed)
+    f = random_rhs(rng, int(rng.integers(1, 30)), int(rng.integers(0, 120)), 4, eps=True,
+                   frac=seed % 3 == 0)
+    for n in (0, 1, 2):
+        compare_sp(f, n)
+
+
+def test_shortest_path_on_compose_result():
+    # the eager pipeline through the two single-call entries
+    lhs = O.compile_string(b"123")
+    rhs = O.freeze(O.compile_string_transducer(b"123", b"abc"))
+    lat = F.compose_frozen(to_product(lhs), load_blob(rhs))
+    sp = F.shortest_path(lat, 1)
+    assert sp.print_string(output_tape=True) == b"abc"
+
+
+def test_shortest_path_negative_weight_is_reported():
+    f = chain_of([1, 2])
+    f.arcs[0][0] = (1, 1, -1.0, 1)
+    assert F.shortest_path(to_product(f), 1) is None
+
+
+# ---------------------------------------------------------------------------------------
+# batch eager semantics beyond layered lattices
+# ---------------------------------------------------------------------------------------
+
+def test_batch_eager_epsilon_dense():
+    blob = O.freeze(O.gen("eps_dense", 64, 12))
+    seqs = [[1] * L for L in (0, 1, 3, 8, 17, 30)]
+    check(blob, *csr(seqs), EAGER)
+
+
+def test_batch_eager_label_zero_inputs():
+    amb = O.freeze(O.gen("ambiguous", 256, 12))
+    seqs = [[1, 0, 1], [0], [0, 0, 1, 1], [1, 1, 0], [1] * 9]  # layered tier takes the last
+    check(amb, *csr(seqs), EAGER)
+    eps = O.freeze(O.gen("eps_dense", 32, 6))
+    check(eps, *csr(seqs), EAGER)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_batch_eager_random_with_epsilons(seed):
+    rng = np.random.default_rng(7000 + seed)
+    f = random_rhs(rng, int(rng.integers(2, 40)), int(rng.integers(4, 160)), 4, eps=True,
+                   frac=seed % 2 == 0)
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(0, 5, int(rng.integers(0, 12)))] for _ in range(48)]
+    check(blob, *csr(seqs), EAGER)
