@@ -62,7 +62,7 @@ def test_compose_empty_sides():
     empty = O.Fst()
     compare_compose(O.compile_string(b"ab"), O.freeze(empty))
     got = F.compose_frozen(F.MutableFst(), load_blob(O.freeze(O.compile_string(b"ab"))))
-    assert got is not None and got.num_states() == 0
+    assert got is not None and got.num_states == 0
 
 
 @pytest.mark.parametrize("L", [0, 1, 5, 17])
