@@ -262,7 +262,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel_ms": avg_k, "b_alg_per_string": balg / args.batch,
-                         "kernel": "eager_layered_lds_kernel" if sem else "lazy_wave_kernel"},
+                         "kernel": "eager_wave_kernel" if sem else "lazy_wave_kernel"},
             "cpu_baseline": cpu,
         }
         line.update(extra)

@@ -183,6 +183,8 @@ enum Scratch : size_t {
   kDebug,
   kElSlab,
   kElBack2,
+  kElBackB,
+  kItems2,
   kBfsSlab,
   kBfsHdr,
   kBfsList,
@@ -341,79 +343,101 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       }
       return hipSuccess;
     }
-    // Tier 1: the 256-thread LDS kernel (layers of <= kElFcap tuples), or with
-    // FSTAMD_EAGER_TIER1=wave the one-wavefront-per-string kernel (<= kEwFcap tuples;
-    // opt-in until it is validated on hardware).
+    // Tier chain for layered lattices (each tier takes the strings the previous one
+    // reports as OVERFLOW, through a device-side list):
+    //   A  one wavefront per string, LDS tables, <= kEwFcap tuples/layer, spans <= kEwKmax
+    //   B  256 threads per string, LDS tables, <= kElFcap tuples/layer, spans <= kElKmax
+    //   C  256 threads per string, HBM tables sized by the rhs (any layer)
+    // FSTAMD_EAGER_TIER1=wg starts at B (A/B comparisons).  A tier is skipped when the
+    // previous one provably cannot overflow on this rhs.
     const char* t1 = std::getenv("FSTAMD_EAGER_TIER1");
-    const bool wg_tier = !(t1 && std::strcmp(t1, "wave") == 0);
-    const uint32_t fcap1 = wg_tier ? kElFcap : kEwFcap;
-    const uint32_t kmax1 = wg_tier ? kElKmax : kEwKmax;
-    const uint64_t back_cap64 = (uint64_t)(in.max_len + 1) * fcap1;
-    const uint32_t back_cap = (uint32_t)std::min<uint64_t>(back_cap64, 1u << 22);
-    auto k_wg = eager_layered_lds_kernel<kElWG, kElFcap, kElHcap, kElKmax>;
+    const bool use_a = !(t1 && std::strcmp(t1, "wg") == 0);
+    const uint32_t ns = rhs.view.num_states, ms = rhs.view.max_span;
+    auto back_cap_for = [&](uint32_t fcap, uint64_t limit, bool* capped) {
+      const uint64_t want = (uint64_t)(in.max_len + 1) * fcap;
+      *capped = want > limit;
+      return (uint32_t)std::min<uint64_t>(want, limit);
+    };
+    bool cap_a = false, cap_b = false;
+    const uint32_t back_cap_a = back_cap_for(kEwFcap, 1u << 22, &cap_a);
+    const uint32_t back_cap_b = back_cap_for(kElFcap, 1u << 22, &cap_b);
+    const bool need_b = !use_a || ns > (uint32_t)kEwFcap || ms > (uint32_t)kEwKmax || cap_a;
+    const bool need_c = need_b && (ns > (uint32_t)kElFcap || ms > (uint32_t)kElKmax || cap_b);
     auto k_wave = eager_wave_kernel<kEwFcap, kEwHcap, kEwEmax, kEwKmax>;
-    const int block1 = wg_tier ? kElWG : 64;
-    int occ = 0;
-    if (wg_tier) HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_wg, block1, 0));
-    else HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_wave, block1, 0));
-    occ = std::max(occ, 1);
-    uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)occ * num_cus_, in.num_strings);
-    while (grid > 1 && (uint64_t)grid * back_cap * sizeof(uint2) > (4ull << 30)) grid /= 2;
-    uint2* back = (uint2*)scratch(kElBack, (size_t)grid * back_cap * sizeof(uint2));
-    if (!back) return hipErrorOutOfMemory;
-
-    // Tier 2 (HBM tables) takes the strings tier 1 reports as OVERFLOW.  A layer of a
-    // layered lattice holds at most one tuple per rhs state, so fcap = num_states can
-    // only overflow the back-pointer slab.  Skipped when tier 1 cannot overflow.
-    const bool may_overflow = (uint64_t)rhs.view.num_states > (uint64_t)fcap1 ||
-                              back_cap64 > back_cap || rhs.view.max_span > kmax1;
-    uint32_t* list = nullptr;
-    uint32_t* count = counter + 2;
-    uint32_t grid2 = 0, fcap2 = 0, hcap2 = 0, back_cap2 = 0;
-    uint8_t* slab = nullptr;
-    uint2* back2 = nullptr;
-    if (may_overflow) {
-      list = (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4);
-      fcap2 = std::max<uint32_t>(rhs.view.num_states, 1);
-      hcap2 = next_pow2(2ull * fcap2);
-      back_cap2 = (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * fcap2, 1u << 28);
-      const uint64_t per_wg = layer_slab_bytes(fcap2, hcap2) + (uint64_t)back_cap2 * 8;
-      grid2 = (uint32_t)std::min<uint64_t>(num_cus_, std::max<uint64_t>(1, (8ull << 30) / per_wg));
-      slab = (uint8_t*)scratch(kElSlab, (size_t)grid2 * layer_slab_bytes(fcap2, hcap2));
-      back2 = (uint2*)scratch(kElBack2, (size_t)grid2 * back_cap2 * sizeof(uint2));
-      if (!list || !slab || !back2) return hipErrorOutOfMemory;
+    auto k_wg = eager_layered_lds_kernel<kElWG, kElFcap, kElHcap, kElKmax>;
+    auto grid_for = [&](const void* k, int block, uint32_t back_cap) -> uint32_t {
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, block, 0) != hipSuccess) occ = 1;
+      uint32_t g = (uint32_t)std::min<uint64_t>((uint64_t)std::max(occ, 1) * num_cus_,
+                                                in.num_strings);
+      while (g > 1 && (uint64_t)g * back_cap * sizeof(uint2) > (4ull << 30)) g /= 2;
+      return std::max<uint32_t>(g, 1);
+    };
+    const uint32_t grid_a = use_a ? grid_for((const void*)k_wave, 64, back_cap_a) : 0;
+    const uint32_t grid_b = need_b ? grid_for((const void*)k_wg, kElWG, back_cap_b) : 0;
+    uint2* back_a = use_a ? (uint2*)scratch(kElBack, (size_t)grid_a * back_cap_a * 8) : nullptr;
+    uint2* back_b = need_b ? (uint2*)scratch(kElBackB, (size_t)grid_b * back_cap_b * 8) : nullptr;
+    if ((use_a && !back_a) || (need_b && !back_b)) return hipErrorOutOfMemory;
+    uint32_t* list_ab = (use_a && need_b) ? (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4)
+                                          : nullptr;
+    uint32_t* list_bc = need_c ? (uint32_t*)scratch(kItems2, (size_t)in.num_strings * 4) : nullptr;
+    if ((use_a && need_b && !list_ab) || (need_c && !list_bc)) return hipErrorOutOfMemory;
+    uint32_t grid_c = 0, fcap_c = 0, hcap_c = 0, back_cap_c = 0;
+    uint8_t* slab_c = nullptr;
+    uint2* back_c = nullptr;
+    if (need_c) {
+      fcap_c = std::max<uint32_t>(ns, 1);
+      hcap_c = next_pow2(2ull * fcap_c);
+      back_cap_c = (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * fcap_c, 1u << 28);
+      const uint64_t per_wg = layer_slab_bytes(fcap_c, hcap_c) + (uint64_t)back_cap_c * 8;
+      grid_c = (uint32_t)std::min<uint64_t>(num_cus_, std::max<uint64_t>(1, (8ull << 30) / per_wg));
+      slab_c = (uint8_t*)scratch(kElSlab, (size_t)grid_c * layer_slab_bytes(fcap_c, hcap_c));
+      back_c = (uint2*)scratch(kElBack2, (size_t)grid_c * back_cap_c * sizeof(uint2));
+      if (!slab_c || !back_c) return hipErrorOutOfMemory;
     }
     if (stats) {
       stats->engine = 0;
-      stats->grid = grid;
-      stats->launches = may_overflow ? 3 : 1;
+      stats->grid = use_a ? grid_a : grid_b;
+      stats->launches = (use_a ? 1 : 0) + (need_b ? (use_a ? 2 : 1) : 0) + (need_c ? 2 : 0);
       HIP_TRY(hipEventRecord(ev0_, stream));
     }
-    EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back, back_cap,
-                   watchdog_ticks()};
-#ifdef FSTAMD_DEBUG_WAIT
-    HIP_TRY(debug_trace_arm());
-#endif
-    if (wg_tier) k_wg<<<grid, block1, 0, stream>>>(rhs.view, in, n, counter, lp, out);
-    else k_wave<<<grid, block1, 0, stream>>>(rhs.view, in, n, counter, lp, out);
-    HIP_TRY(hipGetLastError());
-#ifdef FSTAMD_DEBUG_WAIT
-    HIP_TRY(debug_wait(stream, grid, "tier1"));
-#endif
-    if (may_overflow) {
-      collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
-          out.status, in.num_strings, kPathOverflow, list, count);
-      EagerLaunch lp2{list, count, 0, slab, fcap2, hcap2, back2, back_cap2, watchdog_ticks()};
+    const unsigned long long wd = watchdog_ticks();
+    const uint32_t blocks = (in.num_strings + 255) / 256;
+    // counters: [0..2] item counters of tiers A, B, C; [3] |list_ab|; [4] |list_bc|
+    if (use_a) {
+      EagerLaunch la{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_a, back_cap_a, wd};
 #ifdef FSTAMD_DEBUG_WAIT
       HIP_TRY(debug_trace_arm());
-      std::fprintf(stderr, "[fstamd dbg] tier2 grid=%u fcap=%u hcap=%u back_cap=%u\n", grid2,
-                   fcap2, hcap2, back_cap2);
 #endif
-      eager_layered_kernel<kElWG, kElFcap, kElHcap, false>
-          <<<grid2, kElWG, 0, stream>>>(rhs.view, in, n, counter + 1, lp2, out);
+      k_wave<<<grid_a, 64, 0, stream>>>(rhs.view, in, n, counter, la, out);
       HIP_TRY(hipGetLastError());
 #ifdef FSTAMD_DEBUG_WAIT
-      HIP_TRY(debug_wait(stream, grid2, "tier2"));
+      HIP_TRY(debug_wait(stream, grid_a, "tierA"));
+#endif
+    }
+    if (need_b) {
+      EagerLaunch lb{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_b, back_cap_b, wd};
+      if (use_a) {
+        collect_status_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
+                                                          kPathOverflow, list_ab, counter + 3);
+        lb.items = list_ab;
+        lb.num_items_dev = counter + 3;
+      }
+      k_wg<<<grid_b, kElWG, 0, stream>>>(rhs.view, in, n, counter + 1, lb, out);
+      HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_DEBUG_WAIT
+      HIP_TRY(debug_wait(stream, grid_b, "tierB"));
+#endif
+    }
+    if (need_c) {
+      collect_status_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
+                                                        kPathOverflow, list_bc, counter + 4);
+      EagerLaunch lc{list_bc, counter + 4, 0, slab_c, fcap_c, hcap_c, back_c, back_cap_c, wd};
+      eager_layered_kernel<kElWG, kElFcap, kElHcap, false>
+          <<<grid_c, kElWG, 0, stream>>>(rhs.view, in, n, counter + 2, lc, out);
+      HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_DEBUG_WAIT
+      HIP_TRY(debug_wait(stream, grid_c, "tierC"));
 #endif
     }
     // Strings the layered tiers cannot take (label-0 inputs -> UNSUPPORTED, tier-2

@@ -475,6 +475,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
   const uint32_t tid = threadIdx.x;
   uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t num_items = lp.num_items_dev ? *lp.num_items_dev : lp.num_items;
 
   for (uint32_t i = tid; i < HCAP; i += WG) tbl_clear_slot(T, i);
 
@@ -486,8 +487,8 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
     }
     __syncthreads();
     const uint32_t item = SH.item;
-    if (item >= lp.num_items) break;
-    const uint32_t si = item;
+    if (item >= num_items) break;
+    const uint32_t si = lp.items ? lp.items[item] : item;
     const uint64_t off = in.offsets[si];
     const uint32_t Lk = (uint32_t)(in.offsets[si + 1] - off);
 

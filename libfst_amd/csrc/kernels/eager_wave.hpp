@@ -380,9 +380,11 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     const unsigned long long hit = __ballot(best != kMaxU64 && mykey == best);
     const uint32_t blane = hit ? (uint32_t)(__ffsll((long long)hit) - 1) : 0u;
     const uint32_t bp = __builtin_amdgcn_readlane(myp, blane);
-    const unsigned long long fwb = __builtin_amdgcn_readlane(
-        (long long)__double_as_longlong(myfw), blane);
-    const double fw2 = __longlong_as_double((long long)fwb);
+    // readlane moves 32 bits: broadcast the f64 final weight as two words
+    const unsigned long long fwbits = (unsigned long long)__double_as_longlong(myfw);
+    const uint32_t fw_lo = __builtin_amdgcn_readlane((uint32_t)fwbits, blane);
+    const uint32_t fw_hi = __builtin_amdgcn_readlane((uint32_t)(fwbits >> 32), blane);
+    const double fw2 = __longlong_as_double((long long)(((unsigned long long)fw_hi << 32) | fw_lo));
 
     if (lane == 0) {
       if (!hit) {
