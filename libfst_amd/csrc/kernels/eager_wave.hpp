@@ -42,7 +42,8 @@ struct WaveLds {
   unsigned long long bpack[HCAP];  // (index << 48) | (source position << 32) | rhs arc of
                                    // the tight candidate with the smallest index
   uint16_t nslot[FCAP];            // next-layer rank -> slot
-  unsigned long long best;         // best-final reduction word
+  unsigned long long best;         // best-final reduction words
+  uint32_t bestp;
 };
 
 // Exclusive prefix sum over the wave of a value < 2^BITS, from bit-plane ballots:
@@ -81,12 +82,13 @@ __device__ __forceinline__ void wave_span(const RhsView& r, uint32_t s, uint32_t
   }
 }
 
-// Spans of the owned tuples for `label`, then the (target, weight) of their first KMAX
-// arcs.  The loads are unconditional: the arc mirror is padded by kRecPad >= KMAX records,
-// so rec[lo + j] is in bounds for any lo <= num_arcs; lanes mask what they do not own.
+// Spans of the owned tuples for `label` (row e holds position e*64 + lane), then the
+// (target, weight) of their first KMAX arcs.  The loads are unconditional: the arc
+// mirror is padded by kRecPad >= KMAX records, so rec[lo + j] is in bounds for any
+// lo <= num_arcs; lanes mask what they do not own.
 template <int EMAX, int KMAX>
 __device__ __forceinline__ bool wave_load_layer(const RhsView& rhs, uint32_t label,
-                                                uint32_t first_p, uint32_t E, uint32_t n_cur,
+                                                uint32_t lane, uint32_t n_cur,
                                                 const uint32_t (&s2)[EMAX], uint32_t (&lo)[EMAX],
                                                 uint32_t (&cnt)[EMAX], uint32_t (&ct)[EMAX][KMAX],
                                                 double (&cw)[EMAX][KMAX]) {
@@ -94,7 +96,7 @@ __device__ __forceinline__ bool wave_load_layer(const RhsView& rhs, uint32_t lab
 #pragma unroll
   for (int e = 0; e < EMAX; ++e) {
     uint32_t l = 0, c = 0;
-    if ((uint32_t)e < E && first_p + e < n_cur) wave_span(rhs, s2[e], label, l, c);
+    if ((uint32_t)e * 64 + lane < n_cur) wave_span(rhs, s2[e], label, l, c);
     lo[e] = l;
     cnt[e] = c;
     too_long |= c > (uint32_t)KMAX;
@@ -111,18 +113,26 @@ __device__ __forceinline__ bool wave_load_layer(const RhsView& rhs, uint32_t lab
   return too_long;
 }
 
+// Slot hash: the identity on state ids below HCAP (banded transducers -- the metric's --
+// then fill the table without a single collision, and lanes holding neighbouring
+// positions hit neighbouring banks), higher bits folded in above.
+template <int HCAP>
+__device__ __forceinline__ uint32_t wave_slot(uint32_t t) {
+  constexpr uint32_t kBits = __builtin_ctz(HCAP);
+  return (t ^ (t >> kBits) ^ (t >> (2 * kBits))) & (HCAP - 1);
+}
+
 template <int FCAP, int HCAP, int EMAX, int KMAX>
 __global__ void __launch_bounds__(64, 3)
 eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
                   EagerLaunch lp, BatchOutDev out) {
-  static_assert(FCAP == 64 * EMAX, "FCAP = 64 lanes x EMAX tuples");
+  static_assert(FCAP == 64 * EMAX, "FCAP = 64 lanes x EMAX rows");
   static_assert(EMAX * KMAX <= 64, "creator mask is 64 bits");
   static_assert(KMAX <= kRecPad, "arc mirror padding covers KMAX records");
   static_assert(HCAP >= FCAP && (HCAP & (HCAP - 1)) == 0, "HCAP: power of two >= FCAP");
   constexpr unsigned long long kFree = ~0ull;
-  // per-lane candidate counts are <= EMAX * KMAX
-  constexpr int kCandBits = 32 - __builtin_clz((unsigned)(EMAX * KMAX));
-  constexpr uint32_t kHbits = __builtin_ctz(HCAP);
+  // per-lane, per-row candidate counts are <= KMAX
+  constexpr int kRowBits = 32 - __builtin_clz((unsigned)KMAX);
   __shared__ WaveLds<FCAP, HCAP> S;
   const uint32_t lane = threadIdx.x;
   uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
@@ -168,8 +178,8 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       continue;
     }
 
-    // layer 0: the start tuple, owned by lane 0
-    uint32_t n_cur = 1, E = 1, cur_base = 0;
+    // layer 0: the start tuple, position 0 (lane 0, row 0)
+    uint32_t n_cur = 1, cur_base = 0;
     uint32_t tuples = 1, relax = 0;
     uint32_t s2[EMAX];
     double dd[EMAX];
@@ -196,66 +206,72 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       uint32_t lo[EMAX], cnt[EMAX];
       uint32_t ct[EMAX][KMAX];
       double cw[EMAX][KMAX];
-      if (__ballot(wave_load_layer<EMAX, KMAX>(rhs, lab, lane * E, E, n_cur, s2, lo, cnt, ct, cw))) {
+      if (__ballot(wave_load_layer<EMAX, KMAX>(rhs, lab, lane, n_cur, s2, lo, cnt, ct, cw))) {
         fail = kPathOverflow;  // a span longer than KMAX: the next tier takes the string
         break;
       }
       FT(item, si, k, 2);
-      // candidate index base of this lane: exclusive scan of per-lane candidate counts
-      uint32_t tsum = 0;
+      // Candidate index of (row e, lane, j) = rows before e + lanes before in row e + j:
+      // candidates enumerate (source position, arc index) and position = e * 64 + lane.
+      const uint32_t rows = (n_cur + 63) / 64;
+      uint32_t cbase[EMAX];
+      uint32_t rbase = 0;
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e) tsum += cnt[e];
-      uint32_t ctot;
-      const uint32_t cbase = wave_excl_scan_small<kCandBits>(tsum, ctot);
-      relax += ctot;
+      for (int e = 0; e < EMAX; ++e) {
+        uint32_t tot = 0;
+        cbase[e] = rbase;
+        if ((uint32_t)e < rows) {
+          cbase[e] += wave_excl_scan_small<kRowBits>(cnt[e], tot);
+          rbase += tot;
+        }
+      }
+      relax += rbase;
 
       // ---- (B) insert targets; first occurrence and minimum distance ----
       // Linear probing in uniform rounds: in round r every still-pending candidate tries
       // slot (hash + r), so no per-candidate probe state is needed besides a pending bit.
+      // Tier A only sees rhs weights >= +0 (no -0, NaN, -inf): there
+      // times(d, times(One, w)) (compose.zig:104, shortest-path.zig:72) is exactly d + w.
       unsigned long long pend = 0;
-      uint32_t c = cbase;
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
-          const double nd = w_times(dd[e], w_times(w_one(), cw[e][j]));  // compose.zig:104
+          const double nd = dd[e] + cw[e][j];
           cw[e][j] = nd;
           if ((uint32_t)j < cnt[e]) {
             const uint32_t t = ct[e][j];
-            const uint32_t i = lhash(t, kHbits);
+            const uint32_t i = wave_slot<HCAP>(t);
             const uint32_t old = atomicCAS(&S.key[i], kEmptyKey, t);
             if (old == kEmptyKey || old == t) {
               ct[e][j] = i;
-              atomicMin(&S.first[i], c + j);
+              atomicMin(&S.first[i], cbase[e] + j);
               atomicMin(&S.dmin[i], (unsigned long long)okey(nd));
             } else {
               pend |= 1ull << (e * KMAX + j);
             }
           }
         }
-        c += cnt[e];
       }
       FT(item, si, k, 3);
 #pragma unroll 1
       for (uint32_t r = 1; __ballot(pend != 0) && r < (uint32_t)HCAP; ++r) {
-        c = cbase;
 #pragma unroll
         for (int e = 0; e < EMAX; ++e) {
 #pragma unroll
           for (int j = 0; j < KMAX; ++j) {
             if (pend & (1ull << (e * KMAX + j))) {
               const uint32_t t = ct[e][j];
-              const uint32_t i = (lhash(t, kHbits) + r) & (HCAP - 1);
+              const uint32_t i = (wave_slot<HCAP>(t) + r) & (HCAP - 1);
               const uint32_t old = atomicCAS(&S.key[i], kEmptyKey, t);
               if (old == kEmptyKey || old == t) {
                 ct[e][j] = i;
-                atomicMin(&S.first[i], c + j);
+                atomicMin(&S.first[i], cbase[e] + j);
                 atomicMin(&S.dmin[i], (unsigned long long)okey(cw[e][j]));
                 pend &= ~(1ull << (e * KMAX + j));
               }
             }
           }
-          c += cnt[e];
         }
       }
       if (__ballot(pend != 0)) {  // table full
@@ -263,58 +279,58 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
         break;
       }
       wave_lds_sync();
-
       FT(item, si, k, 4);
+
       // ---- (C) tight candidates -> packed back-pointer; creators ----
       unsigned long long creators = 0;
-      uint32_t nf = 0;
-      c = cbase;
+      uint32_t nf[EMAX];
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
+        nf[e] = 0;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           if ((uint32_t)j < cnt[e]) {
             const uint32_t slot = ct[e][j];
-            const uint32_t ci = c + j;
+            const uint32_t ci = cbase[e] + j;
             if (okey(cw[e][j]) == S.dmin[slot])
               atomicMin(&S.bpack[slot], ((unsigned long long)ci << 48) |
-                                            ((unsigned long long)(lane * E + e) << 32) |
+                                            ((unsigned long long)(e * 64 + lane) << 32) |
                                             (lo[e] + j));
             if (S.first[slot] == ci) {
               creators |= 1ull << (e * KMAX + j);
-              ++nf;
+              ++nf[e];
             }
           }
         }
-        c += cnt[e];
       }
-      uint32_t n_next;
-      const uint32_t fex = wave_excl_scan_small<kCandBits>(nf, n_next);
+      // ---- (D) ranks of the created tuples (candidate order = row, lane, j) ----
+      uint32_t n_next = 0;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if ((uint32_t)e < rows) {
+          uint32_t tot;
+          uint32_t rank = n_next + wave_excl_scan_small<kRowBits>(nf[e], tot);
+          n_next += tot;
+          if (n_next <= (uint32_t)FCAP) {
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j)
+              if (creators & (1ull << (e * KMAX + j))) S.nslot[rank++] = (uint16_t)ct[e][j];
+          }
+        }
+      }
       if (n_next > (uint32_t)FCAP || (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
         fail = kPathOverflow;
         break;
       }
-
-      FT(item, si, k, 5);
-      // ---- (D) ranks of the created tuples (candidate order) ----
-      uint32_t rank = fex;
-#pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-          if (creators & (1ull << (e * KMAX + j))) S.nslot[rank++] = (uint16_t)ct[e][j];
-        }
-      }
       wave_lds_sync();
-
       FT(item, si, k, 6);
-      // ---- (E) next layer: back records, slot reset, spans and arc records ----
+
+      // ---- (E) next layer: back records, slot reset (rank e * 64 + lane) ----
       const uint32_t next_base = cur_base + n_cur;
-      const uint32_t En = (n_next + 63) / 64;
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
-        const uint32_t r = lane * En + e;
-        const bool own = (uint32_t)e < En && r < n_next;
+        const uint32_t r = e * 64 + lane;
+        const bool own = r < n_next;
         const uint32_t slot = S.nslot[own ? r : 0];
         const uint32_t key = S.key[slot];
         const unsigned long long dm = S.dmin[slot];
@@ -332,7 +348,6 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       }
       cur_base = next_base;
       n_cur = n_next;
-      E = En;
       tuples += n_next;
       wave_lds_sync();
     }
@@ -359,12 +374,12 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     double myfw = 0.0;
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) {
-      const uint32_t p = lane * E + e;
-      if ((uint32_t)e < E && p < n_cur) {
+      const uint32_t p = e * 64 + lane;
+      if (p < n_cur) {
         const double fw2 = rhs.final_w[FB(s2[e], rhs.num_states, 33)];
         if (!w_is_zero(dd[e]) && !w_is_zero(fw2)) {
-          const unsigned long long kk = okey(w_times(dd[e], w_times(w_one(), fw2)));
-          if (kk < mykey) {  // e ascending: equal keys keep the lower position
+          const unsigned long long kk = okey(dd[e] + fw2);  // times(d, times(One, fw2))
+          if (kk < mykey) {  // e ascending = p ascending within the lane
             mykey = kk;
             myp = p;
             myfw = fw2;
@@ -372,18 +387,24 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
         }
       }
     }
-    if (lane == 0) S.best = kMaxU64;
+    if (lane == 0) {
+      S.best = kMaxU64;
+      S.bestp = kEmptyKey;
+    }
     wave_lds_sync();
     if (mykey != kMaxU64) atomicMin(&S.best, mykey);
     wave_lds_sync();
     const unsigned long long best = S.best;
-    const unsigned long long hit = __ballot(best != kMaxU64 && mykey == best);
-    const uint32_t blane = hit ? (uint32_t)(__ffsll((long long)hit) - 1) : 0u;
-    const uint32_t bp = __builtin_amdgcn_readlane(myp, blane);
-    // readlane moves 32 bits: broadcast the f64 final weight as two words
+    if (best != kMaxU64 && mykey == best) atomicMin(&S.bestp, myp);
+    wave_lds_sync();
+    const uint32_t bp = S.bestp;
+    const bool hit = best != kMaxU64;
+    // final weight of the best tuple: its owner lane (bp % 64) has myp == bp; readlane
+    // moves 32 bits, so the f64 goes as two words
+    const uint32_t bl = bp & 63u;
     const unsigned long long fwbits = (unsigned long long)__double_as_longlong(myfw);
-    const uint32_t fw_lo = __builtin_amdgcn_readlane((uint32_t)fwbits, blane);
-    const uint32_t fw_hi = __builtin_amdgcn_readlane((uint32_t)(fwbits >> 32), blane);
+    const uint32_t fw_lo = __builtin_amdgcn_readlane((uint32_t)fwbits, bl);
+    const uint32_t fw_hi = __builtin_amdgcn_readlane((uint32_t)(fwbits >> 32), bl);
     const double fw2 = __longlong_as_double((long long)(((unsigned long long)fw_hi << 32) | fw_lo));
 
     if (lane == 0) {
@@ -401,13 +422,13 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
             const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
             out.out_il[o + k - 1] = in.labels[off + k - 1];
             out.out_ol[o + k - 1] = r.olabel;
-            out.out_w[o + k - 1] = w_times(w_one(), r.weight);
+            out.out_w[o + k - 1] = r.weight;  // times(One, w) == w for w >= +0
             id = b.x;
           }
           out.status[si] = kPathOk;
           out.path_len[si] = L;
           out.path_off[si] = o;
-          out.final_w[si] = w_times(w_one(), fw2);  // compose.zig:73: fw1 (0) (x) fw2
+          out.final_w[si] = fw2;  // compose.zig:73: times(One, fw2) == fw2
           if (out.work) {
             out.work[2 * si] = tuples;
             out.work[2 * si + 1] = relax;
