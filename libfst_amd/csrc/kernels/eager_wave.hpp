@@ -93,10 +93,27 @@ __device__ __forceinline__ bool wave_load_layer(const RhsView& rhs, uint32_t lab
                                                 uint32_t (&cnt)[EMAX], uint32_t (&ct)[EMAX][KMAX],
                                                 double (&cw)[EMAX][KMAX]) {
   bool too_long = false;
+  // all span summaries in flight at once (one round trip), then the rare mixed-label
+  // states fall back to the binary search
+  uint4 ss[EMAX];
 #pragma unroll
   for (int e = 0; e < EMAX; ++e) {
-    uint32_t l = 0, c = 0;
-    if ((uint32_t)e * 64 + lane < n_cur) wave_span(rhs, s2[e], label, l, c);
+    const bool own = (uint32_t)e * 64 + lane < n_cur;
+    ss[e] = rhs.sspan[own ? s2[e] : 0u];
+    if (!own) ss[e] = make_uint4(0u, 0u, kSpanNone, 0u);
+  }
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) {
+    uint32_t l = ss[e].x, c = ss[e].y;
+    if (ss[e].z != label) {
+      c = 0;
+      if (ss[e].z == kSpanMixed) {
+        uint32_t a0, b0;
+        span_by_ilabel(rhs, s2[e], label, a0, b0);
+        l = a0;
+        c = b0 - a0;
+      }
+    }
     lo[e] = l;
     cnt[e] = c;
     too_long |= c > (uint32_t)KMAX;
@@ -232,21 +249,27 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       // slot (hash + r), so no per-candidate probe state is needed besides a pending bit.
       // Tier A only sees rhs weights >= +0 (no -0, NaN, -inf): there
       // times(d, times(One, w)) (compose.zig:104, shortest-path.zig:72) is exactly d + w.
+      // Per row: all compare-and-swaps in flight, then one wait, then the atomics.
       unsigned long long pend = 0;
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
+        if ((uint32_t)e >= rows) continue;  // uniform
+        uint32_t old[KMAX];
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
-          const double nd = dd[e] + cw[e][j];
-          cw[e][j] = nd;
+          cw[e][j] = dd[e] + cw[e][j];
+          old[j] = kEmptyKey - 1u;  // "not inserted" for idle slots
+          if ((uint32_t)j < cnt[e]) old[j] = atomicCAS(&S.key[wave_slot<HCAP>(ct[e][j])], kEmptyKey, ct[e][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
           if ((uint32_t)j < cnt[e]) {
             const uint32_t t = ct[e][j];
-            const uint32_t i = wave_slot<HCAP>(t);
-            const uint32_t old = atomicCAS(&S.key[i], kEmptyKey, t);
-            if (old == kEmptyKey || old == t) {
+            if (old[j] == kEmptyKey || old[j] == t) {
+              const uint32_t i = wave_slot<HCAP>(t);
               ct[e][j] = i;
               atomicMin(&S.first[i], cbase[e] + j);
-              atomicMin(&S.dmin[i], (unsigned long long)okey(nd));
+              atomicMin(&S.dmin[i], (unsigned long long)okey(cw[e][j]));
             } else {
               pend |= 1ull << (e * KMAX + j);
             }
@@ -287,16 +310,24 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
         nf[e] = 0;
+        if ((uint32_t)e >= rows) continue;  // uniform
+        unsigned long long dm[KMAX];
+        uint32_t fi[KMAX];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {  // reads in flight together
+          const uint32_t slot = (uint32_t)j < cnt[e] ? ct[e][j] : 0u;
+          dm[j] = S.dmin[slot];
+          fi[j] = S.first[slot];
+        }
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           if ((uint32_t)j < cnt[e]) {
-            const uint32_t slot = ct[e][j];
             const uint32_t ci = cbase[e] + j;
-            if (okey(cw[e][j]) == S.dmin[slot])
-              atomicMin(&S.bpack[slot], ((unsigned long long)ci << 48) |
-                                            ((unsigned long long)(e * 64 + lane) << 32) |
-                                            (lo[e] + j));
-            if (S.first[slot] == ci) {
+            if (okey(cw[e][j]) == dm[j])
+              atomicMin(&S.bpack[ct[e][j]], ((unsigned long long)ci << 48) |
+                                                ((unsigned long long)(e * 64 + lane) << 32) |
+                                                (lo[e] + j));
+            if (fi[j] == ci) {
               creators |= 1ull << (e * KMAX + j);
               ++nf[e];
             }
@@ -327,23 +358,32 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
 
       // ---- (E) next layer: back records, slot reset (rank e * 64 + lane) ----
       const uint32_t next_base = cur_base + n_cur;
+      const uint32_t rows_n = (n_next + 63) / 64;
+      uint32_t es[EMAX];
+      unsigned long long ebp[EMAX];
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {  // rank -> slot, all rows in flight
+        const uint32_t r = e * 64 + lane;
+        es[e] = (uint32_t)e < rows_n ? S.nslot[r < n_next ? r : 0] : 0u;
+      }
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if ((uint32_t)e < rows_n) {
+          s2[e] = S.key[es[e]];
+          dd[e] = from_okey(S.dmin[es[e]]);
+          ebp[e] = S.bpack[es[e]];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
         const uint32_t r = e * 64 + lane;
-        const bool own = r < n_next;
-        const uint32_t slot = S.nslot[own ? r : 0];
-        const uint32_t key = S.key[slot];
-        const unsigned long long dm = S.dmin[slot];
-        const unsigned long long bp = S.bpack[slot];
-        s2[e] = key;
-        dd[e] = from_okey(dm);
-        if (own) {
+        if ((uint32_t)e < rows_n && r < n_next) {
           back[FB(next_base + r, lp.back_cap, 32)] =
-              make_uint2(cur_base + (uint32_t)((bp >> 32) & 0xFFFFu), (uint32_t)bp);
-          S.key[slot] = kEmptyKey;
-          S.first[slot] = kEmptyKey;
-          S.dmin[slot] = kFree;
-          S.bpack[slot] = kFree;
+              make_uint2(cur_base + (uint32_t)((ebp[e] >> 32) & 0xFFFFu), (uint32_t)ebp[e]);
+          S.key[es[e]] = kEmptyKey;
+          S.first[es[e]] = kEmptyKey;
+          S.dmin[es[e]] = kFree;
+          S.bpack[es[e]] = kFree;
         }
       }
       cur_base = next_base;
