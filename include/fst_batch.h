@@ -93,6 +93,30 @@ FstError fst_device_compose_shortest_path(FstHandle b, const uint32_t* d_labels,
                                           const FstBatchOptions* opts, const FstDeviceBatch* out,
                                           void* stream);
 
+/* Multi-stage pipelines (tagger -> verbalizer, README.md:177-214) without host round
+ * trips.  The reference app does, per utterance and stage:
+ *   print_output_string(best) -> compile_string(bytes) -> compose_frozen_shortest_path.
+ * On a 1-best chain that is: next input labels = the path's non-epsilon olabels
+ * (src/string.zig:60-97 then :24-50; label = byte + 1 on both sides).
+ * fst_device_project_output does that for a whole batch on the device.  A string whose
+ * stage status is not OK, or whose output holds a label > 256 (not a byte: the
+ * reference's @intCast would trap), gets one input label no rhs carries (the next stage
+ * reports EMPTY) and its reason in d_proj_status (the stage's status, or
+ * FST_PATH_UNSUPPORTED for a non-byte label).  d_next_labels needs room for the sum of
+ * path_len plus num_strings; d_next_offsets for num_strings + 1.  Synchronises `stream`
+ * and returns the longest projected input in *max_len. */
+FstError fst_device_project_output(const FstDeviceBatch* stage, uint32_t num_strings,
+                                   uint32_t* d_next_labels, uint64_t* d_next_offsets,
+                                   int32_t* d_proj_status, uint32_t* max_len, void* stream);
+
+/* Host convenience: runs num_stages frozen FSTs in sequence on one device, each stage's
+ * 1-best output tape feeding the next (fst_device_project_output in between).  The
+ * result holds the last stage's paths; a string that failed at an earlier stage reports
+ * that stage's status.  Semantics / device from opts (NULL: lazy, current device). */
+FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const uint32_t* labels,
+                            const uint64_t* offsets, uint32_t num_strings, uint32_t n,
+                            const FstBatchOptions* opts, FstBatchResult* out);
+
 /* Bring a frozen FST's device copy up on `device` (blob H2D + on-device SoA mirror). */
 FstError fst_device_prepare(FstHandle b, int32_t device);
 /* Adopt a blob that already sits in device memory on `device` (e.g. received by an
@@ -114,6 +138,21 @@ FstError fst_last_launch_stats(FstLaunchStats* out);
 /* Generators of the reference bench's synthetic rhs (bench/optimize-bench.zig:219-306),
  * built host-side and frozen: 0 = ambiguous chain, 1 = epsilon dense, 2 = branching. */
 FstHandle fst_bench_transducer(uint32_t kind, uint32_t transducer_len, uint32_t branches);
+/* Same, frozen with the given weight type (0 = tropical, 1 = log; src/fst.zig:43-47). */
+FstHandle fst_bench_transducer_wt(uint32_t kind, uint32_t transducer_len, uint32_t branches,
+                                  uint32_t weight_type);
+
+/* Frozen blobs of either weight type for the batch entries ("weight_type
+ * taken from the blob header").  fst_load stays Tropical-only like the reference c-api
+ * (src/c-api.zig:601, W = TropicalWeight); these accept header weight_type 0 (tropical)
+ * or 1 (log) and otherwise validate exactly like Fst.fromBytes (src/fst.zig:227-273).
+ * On this path LogWeight's times / compare / isZero equal TropicalWeight's
+ * (src/weight.zig:15-37 vs :88-104; log-add `plus` is never used), so both run through
+ * the same engines. */
+FstHandle fst_batch_load(const char* path);
+FstHandle fst_batch_load_bytes(const void* bytes, uint64_t len);
+/* Header weight type of a frozen FST: 0 tropical, 1 log, -1 invalid handle. */
+int32_t fst_weight_type(FstHandle b);
 
 #ifdef __cplusplus
 }

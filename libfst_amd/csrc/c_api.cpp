@@ -289,6 +289,10 @@ int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* r
   return -1;
 }
 
+FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_labels,
+                             uint32_t n, int semantics, int dev, HostPaths* h,
+                             std::unique_ptr<DevOut>* keep);
+
 // Chain batch on the GPU from host arrays; fills `h` in input order.
 FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
                               uint32_t num, uint32_t n, int semantics, int dev, HostPaths* h) {
@@ -310,27 +314,75 @@ FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64
   if (hipMemcpy(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice) != hipSuccess)
     return FST_OOM;
   ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
+  return run_chain_batch_dev(*D, in, total, n, semantics, dev, h, nullptr);
+}
+
+// One batch on device inputs; the path arena grows on OUTPUT_FULL.  With `keep` the
+// device outputs stay alive (pipelines) and `h` receives only the statuses.
+FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_labels,
+                             uint32_t n, int semantics, int dev, HostPaths* h,
+                             std::unique_ptr<DevOut>* keep) {
+  const uint32_t num = in.num_strings;
   // Arena: chains without rhs epsilons produce exactly L arcs per path.
-  uint64_t arc_cap = std::max<uint64_t>(total + 16, 1024);
+  uint64_t arc_cap = std::max<uint64_t>(total_labels + 16, 1024);
   DeviceEngine& E = DeviceEngine::get(dev);
   std::lock_guard<std::mutex> lk(E.mutex());
   for (int attempt = 0; attempt < 6; ++attempt, arc_cap *= 4) {
-    DevOut out(num, arc_cap);
-    if (!out.ok()) return FST_OOM;
+    auto out = std::make_unique<DevOut>(num, arc_cap);
+    if (!out->ok()) return FST_OOM;
     LaunchStats st;
-    hipError_t err = E.run_chain(*D, in, n, semantics, out.v, nullptr, &st);
+    hipError_t err = E.run_chain(D, in, n, semantics, out->v, nullptr, &st);
     if (err == hipSuccess) err = hipDeviceSynchronize();
     if (err != hipSuccess) {
       std::fprintf(stderr, "[libfst_amd] batch engine failed: %s\n", hipGetErrorString(err));
       return FST_OOM;
     }
-    if (!out.download(num, h)) return FST_OOM;
     t_last_stats = st;
     bool full = false;
+    if (keep) {
+      h->status.resize(num);
+      if (num && hipMemcpy(h->status.data(), out->v.status, num * 4ull, hipMemcpyDeviceToHost) !=
+                     hipSuccess)
+        return FST_OOM;
+    } else if (!out->download(num, h)) {
+      return FST_OOM;
+    }
     for (uint32_t i = 0; i < num; ++i) full |= h->status[i] == kPathOutputFull;
-    if (!full) return FST_OK;
+    if (!full) {
+      if (keep) *keep = std::move(out);
+      return FST_OK;
+    }
   }
   return FST_OK;
+}
+
+// HostPaths (engine order) -> FstBatchResult (malloc'ed CSR, fst_batch_result_free).
+void fill_batch_result(const HostPaths& h, uint32_t num_strings, FstBatchResult* out) {
+  out->num_strings = num_strings;
+  out->status = (int32_t*)std::malloc(std::max<size_t>(num_strings, 1) * 4);
+  out->path_offsets = (uint64_t*)std::malloc((num_strings + 1ull) * 8);
+  out->final_weights = (double*)std::malloc(std::max<size_t>(num_strings, 1) * 8);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < num_strings; ++i) {
+    out->path_offsets[i] = tot;
+    if (h.status[i] == kPathOk) tot += h.len[i];
+  }
+  out->path_offsets[num_strings] = tot;
+  out->total_arcs = tot;
+  out->ilabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
+  out->olabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
+  out->weights = (double*)std::malloc(std::max<uint64_t>(tot, 1) * 8);
+  for (uint32_t i = 0; i < num_strings; ++i) {
+    out->status[i] = h.status[i];
+    out->final_weights[i] = h.status[i] == kPathOk ? h.fin[i] : w_zero();
+    if (h.status[i] != kPathOk) continue;
+    const uint64_t o = out->path_offsets[i];
+    for (uint32_t k = 0; k < h.len[i]; ++k) {
+      out->ilabels[o + k] = h.il[h.off[i] + k];
+      out->olabels[o + k] = h.ol[h.off[i] + k];
+      out->weights[o + k] = h.w[h.off[i] + k];
+    }
+  }
 }
 
 }  // namespace
@@ -732,32 +784,7 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   HostPaths h;
   FstError e = run_chain_batch_host(*b, labels, offsets, num_strings, n, semantics, dev, &h);
   if (e != FST_OK) return e;
-  // CSR in input order
-  out->num_strings = num_strings;
-  out->status = (int32_t*)std::malloc(std::max<size_t>(num_strings, 1) * 4);
-  out->path_offsets = (uint64_t*)std::malloc((num_strings + 1ull) * 8);
-  out->final_weights = (double*)std::malloc(std::max<size_t>(num_strings, 1) * 8);
-  uint64_t tot = 0;
-  for (uint32_t i = 0; i < num_strings; ++i) {
-    out->path_offsets[i] = tot;
-    if (h.status[i] == kPathOk) tot += h.len[i];
-  }
-  out->path_offsets[num_strings] = tot;
-  out->total_arcs = tot;
-  out->ilabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
-  out->olabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
-  out->weights = (double*)std::malloc(std::max<uint64_t>(tot, 1) * 8);
-  for (uint32_t i = 0; i < num_strings; ++i) {
-    out->status[i] = h.status[i];
-    out->final_weights[i] = h.status[i] == kPathOk ? h.fin[i] : w_zero();
-    if (h.status[i] != kPathOk) continue;
-    const uint64_t o = out->path_offsets[i];
-    for (uint32_t k = 0; k < h.len[i]; ++k) {
-      out->ilabels[o + k] = h.il[h.off[i] + k];
-      out->olabels[o + k] = h.ol[h.off[i] + k];
-      out->weights[o + k] = h.w[h.off[i] + k];
-    }
-  }
+  fill_batch_result(h, num_strings, out);
   return FST_OK;
 }
 
@@ -770,6 +797,104 @@ void fst_batch_result_free(FstBatchResult* r) {
   std::free(r->weights);
   std::free(r->final_weights);
   std::memset(r, 0, sizeof(*r));
+}
+
+FstError fst_device_project_output(const FstDeviceBatch* o, uint32_t num_strings,
+                                   uint32_t* d_next_labels, uint64_t* d_next_offsets,
+                                   int32_t* d_proj_status, uint32_t* max_len, void* stream) {
+  if (!o || !d_next_offsets || !d_proj_status || (num_strings && !d_next_labels))
+    return FST_INVALID_ARG;
+  if (!gpu_available()) return FST_INVALID_ARG;
+  const int dev = current_device();
+  if (dev < 0) return FST_INVALID_ARG;
+  BatchOutDev v{o->status, o->path_len, o->path_offset, o->final_weight, o->ilabels,
+                o->olabels, o->weights, o->arc_capacity,
+                (unsigned long long*)o->arc_cursor, o->work};
+  uint32_t ml = 0;
+  DeviceEngine& E = DeviceEngine::get(dev);
+  std::lock_guard<std::mutex> lk(E.mutex());
+  if (E.project_output(v, num_strings, d_next_labels, d_next_offsets, d_proj_status, &ml,
+                       (hipStream_t)stream) != hipSuccess)
+    return FST_OOM;
+  if (max_len) *max_len = ml;
+  return FST_OK;
+}
+
+FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const uint32_t* labels,
+                            const uint64_t* offsets, uint32_t num_strings, uint32_t n,
+                            const FstBatchOptions* opts, FstBatchResult* out) {
+  if (!out || !stages || num_stages == 0 || !offsets ||
+      (!labels && num_strings && offsets[num_strings] != offsets[0]))
+    return FST_INVALID_ARG;
+  std::memset(out, 0, sizeof(*out));
+  for (uint32_t i = 0; i < num_strings; ++i)
+    if (offsets[i + 1] < offsets[i]) return FST_INVALID_ARG;
+  std::vector<std::shared_ptr<FrozenFst>> fs(num_stages);
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    for (uint32_t k = 0; k < num_stages; ++k)
+      if (!(fs[k] = g_fst.get(stages[k]))) return FST_INVALID_ARG;
+  }
+  if (!gpu_available()) return FST_INVALID_ARG;
+  const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
+  int dev = opts && opts->device >= 0 ? opts->device : current_device();
+  if (dev < 0 || hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  // stage-1 inputs
+  const uint64_t total = num_strings ? offsets[num_strings] - offsets[0] : 0;
+  uint32_t max_len = 0;
+  std::vector<uint64_t> rebased(num_strings + 1);
+  for (uint32_t i = 0; i <= num_strings; ++i) rebased[i] = offsets[i] - offsets[0];
+  for (uint32_t i = 0; i < num_strings; ++i)
+    max_len = std::max<uint32_t>(max_len, (uint32_t)(rebased[i + 1] - rebased[i]));
+  auto lab = std::make_unique<DevBuf>(total * 4), off = std::make_unique<DevBuf>((num_strings + 1ull) * 8);
+  if (!lab->p || !off->p) return FST_OOM;
+  if (total && hipMemcpy(lab->p, labels + offsets[0], total * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return FST_OOM;
+  if (hipMemcpy(off->p, rebased.data(), (num_strings + 1ull) * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return FST_OOM;
+  std::vector<int32_t> fail(num_strings, kPathOk);  // first failing stage's status
+  uint64_t in_total = total;
+  HostPaths h;
+  for (uint32_t k = 0; k < num_stages; ++k) {
+    DeviceFst* D = fs[k]->device(dev);
+    if (!D) return FST_OOM;
+    ChainInput in{(const uint32_t*)lab->p, (const uint64_t*)off->p, num_strings, max_len};
+    const bool last = k + 1 == num_stages;
+    std::unique_ptr<DevOut> keep;
+    FstError e = run_chain_batch_dev(*D, in, in_total, n, semantics, dev, &h, last ? nullptr : &keep);
+    if (e != FST_OK) return e;
+    if (last) break;
+    // project this stage's outputs into the next stage's inputs, on the device
+    unsigned long long used = 0;
+    if (hipMemcpy(&used, keep->v.cursor, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
+    auto nlab = std::make_unique<DevBuf>((used + num_strings) * 4);
+    auto noff = std::make_unique<DevBuf>((num_strings + 1ull) * 8);
+    DevBuf pst(num_strings * 4ull);
+    if (!nlab->p || !noff->p || !pst.p) return FST_OOM;
+    {
+      DeviceEngine& E = DeviceEngine::get(dev);
+      std::lock_guard<std::mutex> lk(E.mutex());
+      if (E.project_output(keep->v, num_strings, (uint32_t*)nlab->p, (uint64_t*)noff->p,
+                           (int32_t*)pst.p, &max_len, nullptr) != hipSuccess)
+        return FST_OOM;
+    }
+    std::vector<int32_t> ps(num_strings);
+    if (num_strings &&
+        hipMemcpy(ps.data(), pst.p, num_strings * 4ull, hipMemcpyDeviceToHost) != hipSuccess)
+      return FST_OOM;
+    for (uint32_t i = 0; i < num_strings; ++i)
+      if (fail[i] == kPathOk && ps[i] != kPathOk) fail[i] = ps[i];
+    uint64_t nt = 0;
+    if (hipMemcpy(&nt, (uint64_t*)noff->p + num_strings, 8, hipMemcpyDeviceToHost) != hipSuccess)
+      return FST_OOM;
+    in_total = nt;
+    lab = std::move(nlab);
+    off = std::move(noff);
+  }
+  for (uint32_t i = 0; i < num_strings; ++i)
+    if (fail[i] != kPathOk) h.status[i] = fail[i];
+  fill_batch_result(h, num_strings, out);
+  return FST_OK;
 }
 
 FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_labels,
@@ -844,8 +969,47 @@ FstError fst_last_launch_stats(FstLaunchStats* out) {
   return FST_OK;
 }
 
+FstHandle fst_batch_load_bytes(const void* bytes, uint64_t len) {
+  if (!bytes || len < sizeof(Header)) return kInvalid;
+  Header h;
+  std::memcpy(&h, bytes, sizeof(h));
+  if (h.weight_type != kWeightTropical && h.weight_type != kWeightLog) return kInvalid;
+  auto f = FrozenFst::from_bytes((const uint8_t*)bytes, len, h.weight_type, nullptr);
+  if (!f) return kInvalid;
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
+}
+
+FstHandle fst_batch_load(const char* path) {
+  if (!path) return kInvalid;
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return kInvalid;
+  std::vector<uint8_t> bytes;
+  if (std::fseek(fp, 0, SEEK_END) == 0) {
+    const long sz = std::ftell(fp);
+    if (sz >= 0) {
+      bytes.resize((size_t)sz);
+      std::rewind(fp);
+      if (sz > 0 && std::fread(bytes.data(), 1, (size_t)sz, fp) != (size_t)sz) bytes.clear();
+    }
+  }
+  std::fclose(fp);
+  return fst_batch_load_bytes(bytes.data(), bytes.size());
+}
+
+int32_t fst_weight_type(FstHandle b) {
+  std::lock_guard<std::mutex> g(g_api_mu);
+  auto f = g_fst.get(b);
+  return f ? (int32_t)f->weight_type() : -1;
+}
+
 // Reference bench rhs generators (bench/optimize-bench.zig:219-306).
 FstHandle fst_bench_transducer(uint32_t kind, uint32_t T, uint32_t B) {
+  return fst_bench_transducer_wt(kind, T, B, kWeightTropical);
+}
+
+FstHandle fst_bench_transducer_wt(uint32_t kind, uint32_t T, uint32_t B, uint32_t weight_type) {
+  if (weight_type != kWeightTropical && weight_type != kWeightLog) return kInvalid;
   MutableFst m;
   if (kind == 0) {  // buildAmbiguousChainTransducer, :250-277
     m.add_states(T + 1);
@@ -879,7 +1043,7 @@ FstHandle fst_bench_transducer(uint32_t kind, uint32_t T, uint32_t B) {
   } else {
     return kInvalid;
   }
-  auto f = FrozenFst::from_mutable(m, kWeightTropical);
+  auto f = FrozenFst::from_mutable(m, (uint8_t)weight_type);
   std::lock_guard<std::mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }

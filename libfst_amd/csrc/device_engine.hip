@@ -9,6 +9,8 @@
 #include <memory>
 #include <thread>
 
+#include <hipcub/hipcub.hpp>
+
 #include "host_fst.hpp"
 #include "kernels/eager_bfs.hpp"
 #include "kernels/eager_layered.hpp"
@@ -189,6 +191,8 @@ enum Scratch : size_t {
   kBfsHdr,
   kBfsList,
   kBfsList2,
+  kProjCount,
+  kProjTemp,
   kNumScratch
 };
 
@@ -450,54 +454,84 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     return hipSuccess;
   }
 
-  // Lazy semantics -> exact replay, one wavefront per string.
-  LazyWs ws{};
-  const uint64_t want_nodes = std::max<uint64_t>(4096, (uint64_t)256 * (in.max_len + 1));
-  ws.ncap = next_pow2(want_nodes);
-  ws.hcap = ws.ncap * 2;
-  ws.qcap = ws.ncap * 4;
-  ws.gcap = 64;
-  const uint64_t per_wave = (uint64_t)ws.hcap * sizeof(uint4) +
-                            (uint64_t)ws.ncap * (8 + 8 + 16 + 8) +
-                            (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
-  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 16, in.num_strings);
-  while (grid > 1 && (uint64_t)grid * per_wave > (6ull << 30)) grid /= 2;
-  ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
-  ws.nkey = (unsigned long long*)scratch(kLzNkey, (size_t)grid * ws.ncap * 8);
-  ws.ndist = (double*)scratch(kLzNdist, (size_t)grid * ws.ncap * 8);
-  ws.nback = (uint4*)scratch(kLzNback, (size_t)grid * ws.ncap * 16);
-  ws.nbw = (double*)scratch(kLzNbw, (size_t)grid * ws.ncap * 8);
-  ws.qd = (double*)scratch(kLzQd, (size_t)grid * ws.qcap * 8);
-  ws.qid = (uint32_t*)scratch(kLzQid, (size_t)grid * ws.qcap * 4);
-  ws.gscratch = (uint4*)scratch(kLzG, (size_t)grid * ws.gcap * sizeof(uint4));
-  if (!ws.hslot || !ws.nkey || !ws.ndist || !ws.nback || !ws.nbw || !ws.qd || !ws.qid ||
-      !ws.gscratch)
-    return hipErrorOutOfMemory;
-  // Stamps: zero the table whenever it was (re)allocated or the stamp would wrap.
-  if (lazy_hash_bytes_ != (size_t)grid * ws.hcap * sizeof(uint4) ||
-      (uint64_t)lazy_stamp_ + in.num_strings + 2 > 0xFFFFFFF0ull) {
-    HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
-    lazy_hash_bytes_ = (size_t)grid * ws.hcap * sizeof(uint4);
-    lazy_stamp_ = 0;
-  }
-  ws.stamp_base = lazy_stamp_;
-  ws.max_pops = ws.qcap + 1;
-  lazy_stamp_ += in.num_strings + 1;
+  // Lazy semantics -> exact replay, one wavefront per string.  The per-wave workspace
+  // is sized from max_len; strings that outgrow it (OVERFLOW) are re-run from a list
+  // with 8x the capacity and fewer waves, until they fit or the budget is exhausted.
+  GraphInput none{};
+  const bool debug = std::getenv("FSTAMD_LAZY_DEBUG") != nullptr;
+  auto launch_lazy = [&](uint64_t want_nodes, const uint32_t* items, uint32_t num_items,
+                         unsigned int* ctr, uint32_t* grid_out) -> hipError_t {
+    LazyWs ws{};
+    ws.ncap = next_pow2(want_nodes);
+    ws.hcap = ws.ncap * 2;
+    ws.qcap = ws.ncap * 4;
+    ws.gcap = 64;
+    const uint64_t per_wave = (uint64_t)ws.hcap * sizeof(uint4) +
+                              (uint64_t)ws.ncap * (8 + 8 + 16 + 8) +
+                              (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
+    if (per_wave > (24ull << 30)) return hipErrorOutOfMemory;
+    uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 16, num_items);
+    const uint64_t budget = want_nodes <= (1u << 20) ? (6ull << 30) : (24ull << 30);
+    while (grid > 1 && (uint64_t)grid * per_wave > budget) grid /= 2;
+    grid = std::max<uint32_t>(grid, 1);
+    ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
+    ws.nkey = (unsigned long long*)scratch(kLzNkey, (size_t)grid * ws.ncap * 8);
+    ws.ndist = (double*)scratch(kLzNdist, (size_t)grid * ws.ncap * 8);
+    ws.nback = (uint4*)scratch(kLzNback, (size_t)grid * ws.ncap * 16);
+    ws.nbw = (double*)scratch(kLzNbw, (size_t)grid * ws.ncap * 8);
+    ws.qd = (double*)scratch(kLzQd, (size_t)grid * ws.qcap * 8);
+    ws.qid = (uint32_t*)scratch(kLzQid, (size_t)grid * ws.qcap * 4);
+    ws.gscratch = (uint4*)scratch(kLzG, (size_t)grid * ws.gcap * sizeof(uint4));
+    if (!ws.hslot || !ws.nkey || !ws.ndist || !ws.nback || !ws.nbw || !ws.qd || !ws.qid ||
+        !ws.gscratch)
+      return hipErrorOutOfMemory;
+    // Stamps: zero the table whenever it was (re)allocated or the stamp would wrap.
+    if (lazy_hash_bytes_ != (size_t)grid * ws.hcap * sizeof(uint4) ||
+        (uint64_t)lazy_stamp_ + num_items + 2 > 0xFFFFFFF0ull) {
+      HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
+      lazy_hash_bytes_ = (size_t)grid * ws.hcap * sizeof(uint4);
+      lazy_stamp_ = 0;
+    }
+    ws.stamp_base = lazy_stamp_;
+    ws.max_pops = ws.qcap + 1;
+    lazy_stamp_ += num_items + 1;
+    ws.wd_ticks = watchdog_ticks();
+    ws.dbg = debug ? (uint32_t*)scratch(kDebug, (size_t)grid * 8 * 4) : nullptr;
+    if (ws.dbg) HIP_TRY(hipMemsetAsync(ws.dbg, 0, (size_t)grid * 8 * 4, stream));
+    lazy_wave_kernel<false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
+                                                     num_items, ws, out);
+    HIP_TRY(hipGetLastError());
+    if (debug) dump_debug(ws.dbg, grid, stream);
+    *grid_out = grid;
+    return hipSuccess;
+  };
+  uint64_t want = std::max<uint64_t>(4096, (uint64_t)256 * (in.max_len + 1));
   if (stats) {
     stats->engine = 1;
-    stats->grid = grid;
     stats->launches = 1;
     HIP_TRY(hipEventRecord(ev0_, stream));
   }
-  GraphInput none{};
-  ws.wd_ticks = watchdog_ticks();
-  const bool debug = std::getenv("FSTAMD_LAZY_DEBUG") != nullptr;
-  ws.dbg = debug ? (uint32_t*)scratch(kDebug, (size_t)grid * 8 * 4) : nullptr;
-  if (ws.dbg) HIP_TRY(hipMemsetAsync(ws.dbg, 0, (size_t)grid * 8 * 4, stream));
-  lazy_wave_kernel<false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, counter, nullptr,
-                                                   in.num_strings, ws, out);
-  HIP_TRY(hipGetLastError());
-  if (debug) dump_debug(ws.dbg, grid, stream);
+  uint32_t grid0 = 0;
+  HIP_TRY(launch_lazy(want, nullptr, in.num_strings, counter, &grid0));
+  if (stats) stats->grid = grid0;
+  // retry tiers for OVERFLOW strings (host reads the count: this path is for outliers)
+  uint32_t* list = (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4);
+  if (!list) return hipErrorOutOfMemory;
+  for (int tier = 1; tier <= 4; ++tier) {
+    unsigned int* ctr = counter + 4 + 2 * tier;  // [item counter, list count] per tier
+    HIP_TRY(hipMemsetAsync(ctr, 0, 8, stream));
+    collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
+        out.status, in.num_strings, kPathOverflow, list, ctr + 1);
+    HIP_TRY(hipGetLastError());
+    uint32_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, ctr + 1, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (cnt == 0) break;
+    want *= 8;
+    uint32_t g = 0;
+    if (launch_lazy(want, list, cnt, ctr, &g) != hipSuccess) break;  // stays OVERFLOW
+    if (stats) stats->launches += 2;
+  }
   if (stats) {
     HIP_TRY(hipEventRecord(ev1_, stream));
     HIP_TRY(finish_stats(ev0_, ev1_, stats));
@@ -710,6 +744,82 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
     stats->launches = 1;
   }
   return hipDeviceSynchronize();
+}
+
+// ---------------------------------------------------------------------------------
+// Stage -> stage projection (src/string.zig:60-97 printOutputString, then :24-50
+// compileString: label = byte + 1 on both sides, so the next input labels are the
+// path's non-epsilon olabels; a label > 256 is not a byte -- the reference's @intCast
+// would trap -- and is reported instead).
+// ---------------------------------------------------------------------------------
+__global__ void project_count_kernel(BatchOutDev s, uint32_t num, uint64_t* counts,
+                                     int32_t* proj_status, uint32_t* max_len) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > num) return;
+  if (i == num) {  // the scan's last element: offsets[num] = total
+    counts[i] = 0;
+    return;
+  }
+  int32_t ps = s.status[i];
+  uint64_t c = 0;
+  if (ps == kPathOk) {
+    const uint64_t o = s.path_off[i];
+    const uint32_t L = s.path_len[i];
+    for (uint32_t k = 0; k < L; ++k) {
+      const uint32_t ol = s.out_ol[o + k];
+      if (ol > 256u) {
+        ps = kPathUnsupported;
+        break;
+      }
+      c += ol != kEpsilon;
+    }
+  }
+  if (ps != kPathOk) c = 1;  // kDeadLabel
+  counts[i] = c;
+  proj_status[i] = ps;
+  atomicMax(max_len, (uint32_t)c);
+}
+
+__global__ void project_write_kernel(BatchOutDev s, uint32_t num, const uint64_t* offsets,
+                                     const int32_t* proj_status, uint32_t* labels) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= num) return;
+  uint64_t w = offsets[i];
+  if (proj_status[i] != kPathOk) {
+    labels[w] = kDeadLabel;
+    return;
+  }
+  const uint64_t o = s.path_off[i];
+  const uint32_t L = s.path_len[i];
+  for (uint32_t k = 0; k < L; ++k) {
+    const uint32_t ol = s.out_ol[o + k];
+    if (ol != kEpsilon) labels[w++] = ol;
+  }
+}
+
+hipError_t DeviceEngine::project_output(const BatchOutDev& stage, uint32_t num,
+                                        uint32_t* next_labels, uint64_t* next_offsets,
+                                        int32_t* proj_status, uint32_t* max_len,
+                                        hipStream_t stream) {
+  HIP_TRY(hipSetDevice(dev_));
+  uint64_t* counts = (uint64_t*)scratch(kProjCount, ((size_t)num + 1) * 8 + 16);
+  uint32_t* ml = (uint32_t*)scratch(kCounter, 64) + 15;
+  if (!counts || !ml) return hipErrorOutOfMemory;
+  HIP_TRY(hipMemsetAsync(ml, 0, 4, stream));
+  project_count_kernel<<<(num + 256) / 256, 256, 0, stream>>>(stage, num, counts, proj_status,
+                                                             ml);
+  HIP_TRY(hipGetLastError());
+  size_t tbytes = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, counts, next_offsets, num + 1,
+                                           stream));
+  void* temp = scratch(kProjTemp, tbytes + 16);
+  if (!temp) return hipErrorOutOfMemory;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(temp, tbytes, counts, next_offsets, num + 1, stream));
+  project_write_kernel<<<(num + 255) / 256, 256, 0, stream>>>(stage, num, next_offsets,
+                                                             proj_status, next_labels);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(max_len, ml, 4, hipMemcpyDeviceToHost, stream));
+  return hipStreamSynchronize(stream);
 }
 
 hipError_t DeviceEngine::run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n,

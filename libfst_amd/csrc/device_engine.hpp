@@ -28,6 +28,8 @@ constexpr uint32_t kSpanNone = 0xFFFFFFFFu;
 // The device arc mirror (RhsView::rec) has kRecPad zeroed records past num_arcs, so a
 // kernel may read rec[lo + j] for any lo <= num_arcs and j < kRecPad unconditionally.
 constexpr uint32_t kRecPad = 16;
+// Input label no rhs arc carries: a pipeline string that failed an earlier stage.
+constexpr uint32_t kDeadLabel = 0xFFFFFFFFu;
 
 // Read-only view of a device-resident rhs (the kernels' only rhs interface).
 struct RhsView {
@@ -127,6 +129,14 @@ class DeviceEngine {
   // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp).
   hipError_t compose_lattice(const DeviceFst& rhs, const GraphInput& lhs, HostLattice* lat,
                              LaunchStats* stats);
+  // Output tape of each path of a finished stage as the next stage's chain inputs
+  // (printOutputString + compileString on device): next_labels = the path's non-epsilon
+  // olabels.  A string whose status is not OK, or whose output has a label > 256, gets
+  // the single input label kDeadLabel (no rhs arc matches it: the next stage reports
+  // EMPTY) and its reason in proj_status.  Synchronises on `stream` (returns max_len).
+  hipError_t project_output(const BatchOutDev& stage, uint32_t num, uint32_t* next_labels,
+                            uint64_t* next_offsets, int32_t* proj_status, uint32_t* max_len,
+                            hipStream_t stream);
   // fst_shortest_path on an explicit graph; `g` holds the FST itself (CSR, arcs in
   // insertion order).  Non-negative weights only (the caller checks).
   hipError_t shortest_path_graph(const GraphInput& g, uint32_t n, const BatchOutDev& out,

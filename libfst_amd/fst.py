@@ -100,6 +100,14 @@ SIGNATURES = {
     "fst_device_adopt_blob": (_u64, [_P, _u64, _i32, _P]),
     "fst_last_launch_stats": (C.c_int, [C.POINTER(FstLaunchStats)]),
     "fst_bench_transducer": (_u64, [_u32, _u32, _u32]),
+    "fst_bench_transducer_wt": (_u64, [_u32, _u32, _u32, _u32]),
+    "fst_batch_load": (_u64, [C.c_char_p]),
+    "fst_batch_load_bytes": (_u64, [C.c_void_p, C.c_uint64]),
+    "fst_weight_type": (C.c_int32, [_u64]),
+    "fst_device_project_output": (C.c_int, [C.c_void_p, _u32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.POINTER(_u32), C.c_void_p]),
+    "fst_pipeline_batch": (C.c_int, [C.c_void_p, _u32, C.c_void_p, C.c_void_p, _u32, _u32,
+                                     C.c_void_p, C.c_void_p]),
 }
 
 _lib = None
@@ -222,8 +230,23 @@ class Fst:
         return Fst(lib().fst_load(path.encode()))
 
     @staticmethod
-    def bench_transducer(kind, transducer_len, branches) -> "Fst":
-        return Fst(lib().fst_bench_transducer(kind, transducer_len, branches))
+    def load_any(path) -> "Fst":
+        """Tropical or Log blob (fst_batch_load: weight type from the header)."""
+        return Fst(lib().fst_batch_load(path.encode()))
+
+    @staticmethod
+    def from_bytes(blob: bytes) -> "Fst":
+        """Tropical or Log blob from memory (fst_batch_load_bytes)."""
+        buf = C.create_string_buffer(blob, len(blob))
+        return Fst(lib().fst_batch_load_bytes(C.cast(buf, C.c_void_p), len(blob)))
+
+    @property
+    def weight_type(self):
+        return lib().fst_weight_type(self.h)
+
+    @staticmethod
+    def bench_transducer(kind, transducer_len, branches, weight_type=0) -> "Fst":
+        return Fst(lib().fst_bench_transducer_wt(kind, transducer_len, branches, weight_type))
 
     def prepare(self, device=-1):
         rc = lib().fst_device_prepare(self.h, device)
@@ -271,6 +294,29 @@ def compose_frozen_shortest_path_batch(b: Fst, labels, offsets, n: int = 1,
                                                   num, n, C.byref(opts), C.byref(res))
     if rc != FST_OK:
         raise RuntimeError(f"fst_compose_frozen_shortest_path_batch failed: {rc}")
+    return _take_result(res, num)
+
+
+def pipeline_batch(stages, labels, offsets, n: int = 1, semantics: int = FST_SEM_LAZY,
+                   device: int = -1) -> BatchResult:
+    """Multi-stage batch (tagger -> verbalizer ...): each stage's 1-best output tape is the
+    next stage's input, projected on the device (fst_pipeline_batch)."""
+    L = lib()
+    labels = np.ascontiguousarray(labels, dtype=np.uint32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    num = len(offsets) - 1
+    hs = (C.c_uint64 * len(stages))(*[s.h for s in stages])
+    opts = FstBatchOptions(device, semantics, 0)
+    res = FstBatchResult()
+    rc = L.fst_pipeline_batch(hs, len(stages), labels.ctypes.data, offsets.ctypes.data, num, n,
+                              C.byref(opts), C.byref(res))
+    if rc != FST_OK:
+        raise RuntimeError(f"fst_pipeline_batch failed: {rc}")
+    return _take_result(res, num)
+
+
+def _take_result(res, num) -> BatchResult:
+    L = lib()
     tot = int(res.total_arcs)
 
     def arr(p, cnt, dt):

@@ -177,3 +177,27 @@ def test_compose_entries_validate_handles_without_gpu_work():
     r = F.compose_frozen_shortest_path(m, fz, 0)
     assert r is not None and r.num_states == 0 and r.start == F.FST_NO_STATE
     assert F.compose_frozen_shortest_path(m, fz, 2) is None
+
+
+def test_log_weight_blobs_load_through_batch_loaders(tmp_path):
+    """fst_load stays tropical-only (src/c-api.zig:601); fst_batch_load* take the header's
+    weight type (0 or 1) with the same fromBytes validation otherwise."""
+    f = O.gen("ambiguous", 16, 12)
+    blob_log = O.freeze(f, 1)
+    p = str(tmp_path / "log.fst")
+    open(p, "wb").write(blob_log)
+    L = F.lib()
+    assert L.fst_load(p.encode()) == F.FST_INVALID_HANDLE
+    g = F.Fst.load_any(p)
+    assert g.h != F.FST_INVALID_HANDLE and g.weight_type == 1
+    g2 = F.Fst.from_bytes(blob_log)
+    assert g2.weight_type == 1 and g2.num_states == g.num_states
+    assert F.Fst.from_bytes(O.freeze(f, 0)).weight_type == 0
+    bad = bytearray(blob_log)
+    bad[6] = 2
+    assert L.fst_batch_load_bytes(bytes(bad), len(bad)) == F.FST_INVALID_HANDLE
+    # the bench generator frozen as Log: same arcs, header weight type 1
+    fz = F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, 16, 12, weight_type=1)
+    assert fz.weight_type == 1
+    for s in range(fz.num_states):
+        assert fz.arcs(s) == g.arcs(s)
