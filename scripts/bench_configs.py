@@ -1,0 +1,198 @@
+"""Measures BASELINE.json's configs 1-5 on one GPU (the headline metric, config 2 at 1M
+strings, is bench.py's).  One JSON line per config; CPU time of the oracle restatement
+(oracle/fst_oracle.c, single thread, -O3) on a bounded sample beside each.
+
+  1  compose_frozen_epsilon_dense: one 1^96 string vs eps-dense T=4096 B=12, eager
+     compose only (fst_compose_frozen, the whole lattice)
+  2  compose_frozen_shortest_path_ambiguous: 64K 1^64 strings, eager and lazy
+  3  compose_frozen_lazy_shortest_path_epsilon_dense: lazy, mixed lengths; the full
+     config (T=65,536, L 11..251, ~17M tuples per string) is far beyond the lazy
+     engine's per-string budget (one wavefront replays ~17M pops), so T=256 is measured
+     and said so
+  4  two-stage tagger -> verbalizer (synthetic stand-ins, libfst_amd/synthetic.py)
+  5  LogWeight ambiguous chain, 256K strings, lengths 1..64, 10 % dead strings
+
+usage: python scripts/bench_configs.py [--configs 1,2,3,4,5] [--out FILE]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import bench  # noqa: E402
+import libfst_amd as F  # noqa: E402
+from libfst_amd import dist as D  # noqa: E402
+from libfst_amd import synthetic as SY  # noqa: E402
+import oracle_ffi as O  # noqa: E402  (CPU baseline only)
+
+
+def dev_rhs(fz):
+    blob = D.blob_bytes(fz)
+    return D.adopt_on_device(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to("cuda:0"), 0), blob
+
+
+def timed_device(batch, rhs, sem, steps=3):
+    stream = torch.cuda.current_stream().cuda_stream
+    batch.run(rhs, sem, 0, stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(steps):
+        kms.append(batch.run(rhs, sem, 0, stream).kernel_ms)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, float(np.mean(kms))
+
+
+def cpu_rate(blob, labels, offsets, sem, budget_s=4.0):
+    """single-thread oracle strings/s on a prefix of the batch sized to ~budget_s"""
+    n = len(offsets) - 1
+    take = 1
+    while True:
+        secs, _ = O.batch_time(blob, labels, offsets[: take + 1], sem, 1)
+        if secs > budget_s / 8 or take >= n:
+            break
+        take = min(n, take * 4)
+    return take / secs, take
+
+
+def config1():
+    T, B, L = 4096, 12, 96
+    fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, B)
+    lhs = F.MutableFst.compile_string(b"\x00" * L)  # labels 1 = compileString of byte 0
+    F.compose_frozen(lhs, fz)  # warm (device copy, workspace)
+    t0 = time.perf_counter()
+    lat = F.compose_frozen(lhs, fz)
+    wall = time.perf_counter() - t0
+    st = F.last_launch_stats()
+    blob = O.freeze(O.gen("eps_dense", T, B))
+    chain = O.Fst()
+    for _ in range(L + 1):
+        chain.add_state()
+    chain.start = 0
+    chain.finals[L] = 0.0
+    for i in range(L):
+        chain.add_arc(i, 1, 1, 0.0, i + 1)
+    import ctypes as C
+    L_ = O.lib()
+    ma = chain.to_oracle()
+    res = C.c_void_p()
+    st2 = (C.c_uint64 * 2)()
+    t0 = time.perf_counter()
+    rc = L_.or_compose(ma, None, blob, C.byref(res), st2)
+    cpu = time.perf_counter() - t0
+    L_.or_mfst_free(ma)
+    L_.or_mfst_free(res)
+    ns, na = int(st2[0]), int(st2[1])
+    assert rc == O.OR_OK and ns == lat.num_states
+    return {"config": 1, "workload": "compose_frozen_epsilon_dense len=96 T=4096 B=12, eager compose (lattice)",
+            "states": int(ns), "arcs": int(na), "gpu_kernel_ms": st.kernel_ms,
+            "gpu_call_ms": wall * 1e3, "note": "call time includes lattice download and host MutableFst build",
+            "cpu_oracle_ms": cpu * 1e3, "cpu_kind": "port, 1 thread (or_compose)"}
+
+
+def config2(n=65536, L=64):
+    fz = F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, 4096, 12)
+    rhs, blob = dev_rhs(fz)
+    out = []
+    for sem, name in ((F.FST_SEM_EAGER, "eager"), (F.FST_SEM_LAZY, "lazy")):
+        m = n if sem == F.FST_SEM_EAGER else 8192
+        b = bench.DeviceBatch(np.full(m, L, np.int64), lambda t: torch.ones(t, dtype=torch.int32), "cuda:0")
+        wall, kms = timed_device(b, rhs, sem, steps=3 if sem == F.FST_SEM_EAGER else 1)
+        assert np.all(b.status.cpu().numpy() == 0)
+        labels = np.ones(64 * L, np.uint32)
+        offs = np.arange(65, dtype=np.uint64) * L
+        cr, take = cpu_rate(blob, labels, offs, 1 if sem == F.FST_SEM_EAGER else 0)
+        out.append({"config": 2, "workload": f"compose_frozen_shortest_path_ambiguous {name}, {m} x 1^64",
+                    "strings_per_s": m / wall, "kernel_ms": kms, "cpu_oracle_strings_per_s": cr,
+                    "cpu_sample": take, "cpu_kind": "port, 1 thread"})
+    return out
+
+
+def config3(T=256, n=256):
+    fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, 12)
+    rhs, blob = dev_rhs(fz)
+    rng = np.random.default_rng(0x5EED)
+    lens = rng.integers(11, 252, n)
+    b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0")
+    wall, kms = timed_device(b, rhs, F.FST_SEM_LAZY, steps=1)
+    st = b.status.cpu().numpy()
+    labels = np.ones(int(lens[:8].sum()), np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:8])]).astype(np.uint64)
+    cr, take = cpu_rate(blob, labels, offs, 0, budget_s=8.0)
+    return {"config": 3, "workload": f"compose_frozen_lazy_shortest_path_epsilon_dense T={T} (full config: T=65536), {n} strings, L uniform 11..251",
+            "strings_per_s": n / wall, "kernel_ms": kms, "ok": int((st == 0).sum()),
+            "overflow": int((st == 4).sum()), "cpu_oracle_strings_per_s": cr, "cpu_sample": take,
+            "cpu_kind": "port, 1 thread"}
+
+
+def config4(n=65536):
+    stages = [SY.to_mutable(SY.tagger()).freeze(), SY.to_mutable(SY.verbalizer()).freeze()]
+    rng = np.random.default_rng(44)
+    texts = SY.utterances(rng, n)
+    labels, offsets = SY.to_labels(texts)
+    F.pipeline_batch(stages, labels[: int(offsets[64])], offsets[:65], 1, F.FST_SEM_LAZY)
+    out = []
+    for sem, name in ((F.FST_SEM_LAZY, "lazy (fst_compose_frozen_shortest_path)"),
+                      (F.FST_SEM_EAGER, "eager")):
+        t0 = time.perf_counter()
+        r = F.pipeline_batch(stages, labels, offsets, 1, sem)
+        wall = time.perf_counter() - t0
+        ok = int((r.status == 0).sum())
+        out.append({"config": 4, "workload": f"tagger -> verbalizer (synthetic stand-ins), {n} utterances, {name}",
+                    "strings_per_s": n / wall, "ok": ok,
+                    "note": "host API end to end: H2D inputs, 2 stages + device projection, D2H results"})
+    return out
+
+
+def config5(n=262144):
+    fz = F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, 4096, 12, weight_type=1)
+    assert fz.weight_type == 1
+    rhs, blob = dev_rhs(fz)
+    rng = np.random.default_rng(5)
+    lens = rng.integers(1, 65, n)
+
+    def labels_fn(t):
+        x = np.ones(t, np.int32)
+        kill = rng.random(t) < (0.1 / 32)
+        x[kill] = 2
+        return torch.from_numpy(x)
+    b = bench.DeviceBatch(lens, labels_fn, "cuda:0")
+    wall, kms = timed_device(b, rhs, F.FST_SEM_EAGER)
+    st = b.status.cpu().numpy()
+    labels = np.ones(int(lens[:256].sum()), np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:256])]).astype(np.uint64)
+    cr, take = cpu_rate(blob, labels, offs, 1)
+    return {"config": 5, "workload": f"LogWeight ambiguous T=4096 B=12, {n} strings, L 1..64, ~10% dead, eager",
+            "strings_per_s": n / wall, "kernel_ms": kms, "ok": int((st == 0).sum()),
+            "empty": int((st == 1).sum()), "cpu_oracle_strings_per_s": cr, "cpu_sample": take,
+            "cpu_kind": "port, 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,2,3,4,5")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    fns = {"1": config1, "2": config2, "3": config3, "4": config4, "5": config5}
+    lines = []
+    for c in args.configs.split(","):
+        r = fns[c]()
+        for x in (r if isinstance(r, list) else [r]):
+            s = json.dumps(x)
+            print(s, flush=True)
+            lines.append(s)
+    if args.out:
+        open(args.out, "w").write("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()
