@@ -471,7 +471,9 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                               (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
     if (per_wave > (24ull << 30)) return hipErrorOutOfMemory;
     uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 16, num_items);
-    const uint64_t budget = want_nodes <= (1u << 20) ? (6ull << 30) : (24ull << 30);
+    // latency-bound: as many waves in flight as the SIMDs hold (4/SIMD), within 20 GB of
+    // the 288 GB HBM
+    const uint64_t budget = 20ull << 30;
     while (grid > 1 && (uint64_t)grid * per_wave > budget) grid /= 2;
     grid = std::max<uint32_t>(grid, 1);
     ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
