@@ -58,7 +58,7 @@ def parse():
     p.add_argument("--semantics", choices=["eager", "lazy"], default="eager")
     p.add_argument("--varied", action="store_true",
                    help="also time a varied batch (lengths 1..len, 10%% dead strings)")
-    p.add_argument("--lazy-batch", type=int, default=8192,
+    p.add_argument("--lazy-batch", type=int, default=65536,
                    help="also time the lazy engine on this many metric strings (0 = off)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
