@@ -1,0 +1,55 @@
+"""The parallel lazy-engine plan (tests/lazy_model.py) against the oracle's
+sequential composeShortestPath replay (src/ops/compose-shortest-path.zig:26-401).
+
+CPU only: the model is the specification the device engine is built to; it must give the
+reference's exact result (ids, back-pointers, best, backtrace) on every input."""
+import numpy as np
+import pytest
+
+import lazy_model as M
+import oracle_ffi as O
+from test_gpu_parity import random_rhs
+
+
+def oracle_lazy(lhs, blob):
+    rc, res = O.compose_shortest_path(lhs, blob, 1)
+    if rc == O.OR_ERR_CYCLE:
+        return "cycle"
+    assert rc == O.OR_OK
+    return O.chain(res)
+
+
+def chain_of(labels):
+    f = O.Fst()
+    for _ in range(len(labels) + 1):
+        f.add_state()
+    f.start = 0
+    f.finals[len(labels)] = 0.0
+    for i, x in enumerate(labels):
+        f.add_arc(i, x, x, 0.0, i + 1)
+    return f
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_model_random_with_epsilons(block):
+    for seed in range(block * 100, block * 100 + 100):
+        rng = np.random.default_rng(9000 + seed)
+        lhs = random_rhs(rng, int(rng.integers(1, 8)), int(rng.integers(1, 25)), 3, eps=True,
+                         wmax=2, frac=seed % 3 == 0)
+        rhs = random_rhs(rng, int(rng.integers(1, 15)), int(rng.integers(1, 60)), 3, eps=True,
+                         wmax=2, frac=seed % 3 == 0)
+        blob = O.freeze(rhs)
+        got, _ = M.lazy_via_rounds(lhs, blob)
+        assert got == oracle_lazy(lhs, blob), seed
+
+
+@pytest.mark.parametrize("name,T,L,max_rounds", [("ambiguous", 4096, 64, 257),
+                                                 ("eps_dense", 64, 12, None)])
+def test_model_bench_shapes(name, T, L, max_rounds):
+    lhs = chain_of([1] * L)
+    blob = O.freeze(O.gen(name, T, 12))
+    got, rounds = M.lazy_via_rounds(lhs, blob)
+    assert got == oracle_lazy(lhs, blob)
+    if max_rounds is not None:
+        # 4 pops' worth of depth per input symbol: the metric's 8385 pops in 257 rounds
+        assert rounds <= max_rounds
