@@ -130,7 +130,8 @@ FstHandle fst_device_adopt_blob(const void* d_blob, uint64_t len, int32_t device
 typedef struct {
     double kernel_ms;           /* sum of kernel durations, HIP events on the launch stream */
     uint32_t launches;          /* kernel launches in the call */
-    uint32_t engine;            /* 0 = eager-layered, 1 = lazy-wave, 2 = eager-general */
+    uint32_t engine;            /* 0 = eager-layered, 1 = lazy replay, 2 = eager-general,
+                                   3 = lazy rounds */
     uint32_t grid;              /* workgroups of the dominant kernel */
 } FstLaunchStats;
 FstError fst_last_launch_stats(FstLaunchStats* out);

@@ -108,6 +108,7 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   d->view = RhsView{d->span, d->final_w, d->il, d->rec, d->sspan, ns, na, h.start_state, max_span};
   d->has_eps = f.has_epsilon_input();
   d->nonneg = f.weights_nonnegative();
+  d->finite = f.arc_weights_finite();
   d->weight_type = f.weight_type();
   return d;
 }
@@ -454,9 +455,26 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     return hipSuccess;
   }
 
-  // Lazy semantics -> exact replay, one wavefront per string.  The per-wave workspace
-  // is sized from max_len; strings that outgrow it (OVERFLOW) are re-run from a list
-  // with 8x the capacity and fewer waves, until they fit or the budget is exhausted.
+  // Lazy semantics.  Finite weights >= 0 -> the parallel rounds engine (eager_bfs.hpp,
+  // bfs_lazy_path), one workgroup per string.  Otherwise (+inf arcs, negative weights),
+  // or with FSTAMD_LAZY_ENGINE=replay, the exact replay, one wavefront per string.
+  const char* le = std::getenv("FSTAMD_LAZY_ENGINE");
+  const bool use_rounds = rhs.nonneg && rhs.finite && !(le && std::strcmp(le, "replay") == 0);
+  if (use_rounds) {
+    if (stats) {
+      stats->engine = 3;
+      HIP_TRY(hipEventRecord(ev0_, stream));
+    }
+    HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, true, true));
+    if (stats) {
+      HIP_TRY(hipEventRecord(ev1_, stream));
+      HIP_TRY(finish_stats(ev0_, ev1_, stats));
+    }
+    return hipSuccess;
+  }
+  // Replay: the per-wave workspace is sized from max_len; strings that outgrow it
+  // (OVERFLOW) are re-run from a list with 8x the capacity and fewer waves, until they
+  // fit or the budget is exhausted.
   GraphInput none{};
   const bool debug = std::getenv("FSTAMD_LAZY_DEBUG") != nullptr;
   auto launch_lazy = [&](uint64_t want_nodes, const uint32_t* items, uint32_t num_items,
@@ -546,11 +564,13 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
 // ---------------------------------------------------------------------------------
 
 namespace {
-// Per-string workspace tiers: nodes / arcs grow x16 until one slab would exceed the
-// budget.  Tier 0 covers every metric-like string; eps-dense T=4096 L=96 (781K tuples,
-// 10M arcs) needs tier 1.
-constexpr uint32_t kBfsNcap0 = 1u << 16;
-constexpr uint32_t kBfsAcap0 = 1u << 20;
+// Per-string workspace tiers: nodes / arcs grow x8 until one slab would exceed the
+// budget.  Tier 0 (16K tuples, 256K arcs, ~4 MB) covers metric-like strings with
+// 4 workgroups per CU in flight; eps-dense T=4096 L=96 (781K tuples, 10M arcs) needs
+// tier 2.
+constexpr uint32_t kBfsNcap0 = 1u << 14;
+constexpr uint32_t kBfsAcap0 = 1u << 18;
+constexpr uint32_t kBfsWgPerCu0 = 4;
 constexpr uint64_t kBfsBudget = 40ull << 30;  // bytes of BFS workspace per launch
 constexpr int kBfsWG = 256;
 
@@ -560,7 +580,7 @@ struct BfsCaps {
 };
 BfsCaps bfs_caps(int tier) {
   BfsCaps c;
-  uint64_t n = (uint64_t)kBfsNcap0 << (4 * tier), a = (uint64_t)kBfsAcap0 << (4 * tier);
+  uint64_t n = (uint64_t)kBfsNcap0 << (3 * tier), a = (uint64_t)kBfsAcap0 << (3 * tier);
   c.ncap = (uint32_t)std::min<uint64_t>(n, 1u << 30);
   c.acap = (uint32_t)std::min<uint64_t>(a, 0x7FFFFFFFu);
   c.hcap = next_pow2(2ull * c.ncap);
@@ -584,7 +604,8 @@ __global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_
 }
 
 hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
-                                       const BatchOutDev& out, hipStream_t stream, bool all) {
+                                       const BatchOutDev& out, hipStream_t stream, bool all,
+                                       bool lazy) {
   unsigned int* ctr = (unsigned int*)scratch(kCounter, 64);  // [8..15] are ours
   uint32_t* list = (uint32_t*)scratch(kBfsList, (size_t)in.num_strings * 4);
   uint32_t* list2 = (uint32_t*)scratch(kBfsList2, (size_t)in.num_strings * 4);
@@ -609,7 +630,9 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     const BfsCaps c = bfs_caps(tier);
     const uint64_t fit = std::max<uint64_t>(1, kBfsBudget / c.stride);
     if (kBfsBudget < c.stride) break;  // beyond the budget: those strings stay OVERFLOW
-    const uint32_t grid = (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_, fit});
+    const uint64_t per_cu = tier == 0 ? kBfsWgPerCu0 : 1;
+    const uint32_t grid =
+        (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_ * per_cu, fit});
     BfsWs ws{};
     ws.slab = (uint8_t*)scratch(kBfsSlab, (size_t)grid * c.stride);
     ws.hdr = (uint32_t*)scratch(kBfsHdr, (size_t)grid * 8 * 4);
@@ -621,6 +644,7 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     ws.lcap = c.lcap;
     ws.wd_ticks = watchdog_ticks();
     ws.lattice_only = 0;
+    ws.lazy = lazy ? 1u : 0u;
     HIP_TRY(hipMemsetAsync(cnt + 1, 0, 8, stream));  // item counter + next list count
     GraphInput none{};
     eager_bfs_kernel<kBfsWG, false><<<grid, kBfsWG, 0, stream>>>(
@@ -644,7 +668,7 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
   unsigned int* ctr = (unsigned int*)scratch(kCounter, 64);
   if (!ctr) return hipErrorOutOfMemory;
   BatchOutDev none_out{};
-  for (int tier = 0;; ++tier) {
+  for (int tier = 1;; ++tier) {  // one lattice: start at 128K tuples
     const BfsCaps c = bfs_caps(tier);
     if (c.stride > kBfsBudget) {
       lat->status = kPathOverflow;
@@ -672,7 +696,7 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
       stats->engine = 2;
       stats->grid = 1;
-      stats->launches = tier + 1;
+      stats->launches = tier;
     }
     uint32_t hdr[8];
     HIP_TRY(hipMemcpy(hdr, ws.hdr, sizeof(hdr), hipMemcpyDeviceToHost));

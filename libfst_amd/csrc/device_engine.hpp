@@ -56,7 +56,8 @@ struct DeviceFst {
   uint4* sspan = nullptr;
   RhsView view{};
   bool has_eps = false;
-  bool nonneg = true;
+  bool nonneg = true;        // every arc and final weight >= +0
+  bool finite = true;        // every arc weight finite
   uint8_t weight_type = 0;
 
   static DeviceFst* create(const FrozenFst& f, int dev);
@@ -147,11 +148,13 @@ class DeviceEngine {
 
  private:
   explicit DeviceEngine(int dev);
-  // General eager engine over the strings of `in` whose status is UNSUPPORTED or
-  // OVERFLOW after the layered tiers (all strings when `all`); grows its per-string
-  // workspace in tiers.  Synchronises on `stream` to size the tiers.
+  // General engine (kernels/eager_bfs.hpp) over the strings of `in` whose status is
+  // UNSUPPORTED or OVERFLOW after the layered tiers (all strings when `all`); eager
+  // shortestPath or, with `lazy`, composeShortestPath semantics (finite weights >= 0).
+  // Grows its per-string workspace in tiers.  Synchronises on `stream` to size the tiers.
   hipError_t run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
-                           const BatchOutDev& out, hipStream_t stream, bool all);
+                           const BatchOutDev& out, hipStream_t stream, bool all,
+                           bool lazy = false);
   void* scratch(size_t idx, size_t bytes);
   int dev_;
   int num_cus_ = 0;

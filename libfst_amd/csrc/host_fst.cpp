@@ -138,12 +138,14 @@ std::shared_ptr<FrozenFst> FrozenFst::from_bytes(const uint8_t* bytes, size_t le
 void FrozenFst::analyze() {
   has_eps_ = false;
   nonneg_ = true;
+  finite_ = true;
   const Header& h = header();
   const PackedArc* a = arcs();
   for (uint32_t i = 0; i < h.num_arcs; ++i) {
     if (a[i].ilabel == kEpsilon) has_eps_ = true;
     const double w = a[i].weight;
     if (!(w >= 0.0) || std::signbit(w)) nonneg_ = false;  // negative, -0.0 or NaN
+    if (!std::isfinite(w)) finite_ = false;
   }
   const StateEntry* s = states();
   for (uint32_t i = 0; i < h.num_states; ++i) {

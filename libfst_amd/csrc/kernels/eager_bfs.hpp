@@ -38,6 +38,7 @@ struct BfsWs {
   uint32_t* hdr;            // [grid * 8]: n_nodes, n_arcs, n_levels, status, item
   unsigned long long wd_ticks;
   uint32_t lattice_only;    // 1: stop after compose (fst_compose_frozen)
+  uint32_t lazy;            // 1: composeShortestPath semantics (bfs_lazy_path)
 };
 
 struct BfsTables {
@@ -191,23 +192,23 @@ __device__ __forceinline__ void bfs_expand(const RhsView& rhs, const BfsLhs<kGra
 
 struct BfsShared {
   uint32_t scan[16];
+  unsigned long long red[16];  // per-wave partials of block reductions
   uint32_t item;
   uint32_t expired;
   uint32_t flag;
   uint32_t changed;
   unsigned long long best;
   uint32_t bestid;
+  uint32_t count;              // lazy rounds: next active list length
 };
 
-// shortestPath on a lattice held in BfsTables (aoff / anext / aw / ail / aol / nfin, BFS
-// levels in lvl[0..n_levels]); the whole workgroup calls it; thread 0 writes the result.
+// Least fixpoint of d(X) = min fl(d(s) + w) from d(start) = One, by Gauss-Seidel sweeps
+// over the BFS levels (lvl[0..n_levels]); also clears nback.  The whole workgroup calls
+// it; false = the deadline passed (uniform).
 template <int WG>
-__device__ void bfs_shortest_path(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
-                                  uint32_t n_levels, uint32_t start, const BatchOutDev& out,
-                                  uint32_t si, BfsShared& SH, unsigned long long deadline) {
+__device__ bool bfs_fixpoint(const BfsTables& T, uint32_t n_nodes, uint32_t n_levels,
+                             uint32_t start, BfsShared& SH, unsigned long long deadline) {
   const uint32_t tid = threadIdx.x;
-  int32_t fail = kPathOk;
-  // ---- shortestPath: Gauss-Seidel sweeps to the least fixpoint ----
   for (uint32_t i = tid; i < n_nodes; i += WG) {
     T.nd[i] = i == start ? okey(w_one()) : okey(w_zero());
     T.nback[i] = ~0ull;
@@ -235,14 +236,20 @@ __device__ void bfs_shortest_path(const BfsTables& T, uint32_t n_nodes, uint32_t
     __syncthreads();
     const bool changed = SH.changed != 0, expired = SH.flag != 0;
     __syncthreads();
-    if (!changed) break;
-    if (expired || sweep > n_nodes) {  // sweep > n_nodes cannot happen for weights >= 0
-      fail = kPathInternal;
-      break;
-    }
+    if (!changed) return true;
+    if (expired || sweep > n_nodes) return false;  // sweep > n_nodes: impossible for w >= 0
   }
-  if (fail != kPathOk) {
-    if (tid == 0) write_status(out, si, fail, n_nodes, n_arcs);
+}
+
+// shortestPath on a lattice held in BfsTables (aoff / anext / aw / ail / aol / nfin, BFS
+// levels in lvl[0..n_levels]); the whole workgroup calls it; thread 0 writes the result.
+template <int WG>
+__device__ void bfs_shortest_path(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
+                                  uint32_t n_levels, uint32_t start, const BatchOutDev& out,
+                                  uint32_t si, BfsShared& SH, unsigned long long deadline) {
+  const uint32_t tid = threadIdx.x;
+  if (!bfs_fixpoint<WG>(T, n_nodes, n_levels, start, SH, deadline)) {
+    if (tid == 0) write_status(out, si, kPathInternal, n_nodes, n_arcs);
     return;
   }
   // back-pointers: tight in-arc with the smallest (source, arc index)
@@ -326,6 +333,384 @@ __device__ void bfs_shortest_path(const BfsTables& T, uint32_t n_nodes, uint32_t
           }
         }
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// composeShortestPath (src/ops/compose-shortest-path.zig:26-401) for finite weights >= 0,
+// on the lattice compose built (same tuples, same arcs in the same candidate order: the
+// lazy expansion at :182-365 follows compose.zig's 4 phases).  Its answer depends on the
+// heap order only through the ids, which are assigned at first touch in pop order; so:
+//   dist  = the least fixpoint (bfs_fixpoint), as for shortestPath;
+//   lid   = first-touch ids in pop order, computed in parallel rounds (below);
+//   back  = lexmin (lid(source), il, ol, candidate order) over tight in-arcs (relax at
+//           :107-141: a lexicographic min on (dist, source id, il, ol); a full tie keeps
+//           the earlier relaxation);
+//   best  = lexmin (total, lid) over nodes with both finals non-Zero (:165-179);
+//   path  = back-pointers from best until the start id (:368-380).
+// Rounds.  A node is poppable ("active") once a popped in-neighbour reaches it tightly
+// (its tentative dist is then final), the start from the outset; with weights >= 0 the
+// heap minimum is always an active node at the minimum active dist dmin.  A round takes
+// the active nodes at dmin in lid order and pops the longest prefix that no member's
+// "joiner" undercuts: popping u activates an older, inactive node x at dmin (0-weight
+// arc) that must pop before every member with a larger lid.  Targets first touched in
+// the round get fresh lids in (popper order, candidate order) -- larger than every
+// existing lid, so they never undercut.  tests/lazy_model.py is the executable model,
+// checked against the sequential replay on random tie-heavy inputs.
+// ---------------------------------------------------------------------------------------
+
+// Wavefront-then-workgroup reductions / scans through SH (all threads call).
+template <int WG>
+__device__ __forceinline__ unsigned long long block_min_u64(unsigned long long v, BfsShared& SH) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(v, o, 64);
+    v = y < v ? y : v;
+  }
+  if constexpr (WG == 64) {
+    return v;
+  } else {
+    if ((threadIdx.x & 63) == 0) SH.red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    unsigned long long m = SH.red[0];
+#pragma unroll
+    for (int i = 1; i < WG / 64; ++i) m = SH.red[i] < m ? SH.red[i] : m;
+    __syncthreads();
+    return m;
+  }
+}
+
+// Exclusive prefix minimum in thread order (identity ~0u); `total` = the block minimum.
+template <int WG>
+__device__ __forceinline__ uint32_t block_excl_min(uint32_t v, BfsShared& SH, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = y < inc ? y : inc;
+  }
+  uint32_t ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = ~0u;
+  if constexpr (WG == 64) {
+    total = __shfl(inc, 63, 64);
+    return ex;
+  } else {
+    if (lane == 63) SH.scan[w] = inc;
+    __syncthreads();
+    uint32_t base = ~0u, tot = ~0u;
+#pragma unroll
+    for (int i = 0; i < WG / 64; ++i) {
+      const uint32_t t = SH.scan[i];
+      if (i < w) base = t < base ? t : base;
+      tot = t < tot ? t : tot;
+    }
+    __syncthreads();
+    total = tot;
+    return base < ex ? base : ex;
+  }
+}
+
+// Round tables, carved from the BFS tables compose no longer needs (hkey / hval / nkey /
+// lvl / cslot; the fixpoint has finished with lvl).
+struct LazyTables {
+  uint32_t* lid;    // [n] first-touch id, ~0 = untouched
+  uint32_t* inv;    // [n] lid -> node
+  uint32_t* flg;    // [n] kLzActive | kLzPopped
+  uint32_t* touch;  // [n] smallest candidate rank touching an untouched node this round
+  uint32_t* act;    // [n] active nodes (unordered)
+  uint32_t* act2;   // [n] next round's active nodes
+  uint32_t* slist;  // [n] this round's dmin members in lid order
+  uint32_t* bmap;   // [n / 32 + 1] lid bitmap of the members (clear between rounds)
+  uint32_t* rk;     // [arcs] arc index of each candidate rank of the round
+};
+constexpr uint32_t kLzActive = 1u, kLzPopped = 2u;
+
+__device__ inline LazyTables lazy_carve(const BfsTables& T, uint32_t ncap) {
+  LazyTables L;
+  uint32_t* h = (uint32_t*)T.hkey;  // 8 * hcap >= 16 * ncap bytes
+  L.lid = h;
+  L.inv = h + ncap;
+  L.flg = h + 2 * (size_t)ncap;
+  L.touch = h + 3 * (size_t)ncap;
+  L.act = T.hval;                   // 4 * hcap >= 8 * ncap bytes
+  L.act2 = T.hval + ncap;
+  L.slist = (uint32_t*)T.nkey;      // 8 * ncap bytes
+  L.bmap = T.lvl;                   // 4 * (ncap + 2) bytes
+  L.rk = T.cslot;
+  return L;
+}
+
+template <int WG>
+__device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_nodes,
+                              uint32_t n_arcs, uint32_t n_levels, uint32_t start,
+                              const BatchOutDev& out, uint32_t si, BfsShared& SH,
+                              unsigned long long deadline) {
+  const uint32_t tid = threadIdx.x;
+  if (!bfs_fixpoint<WG>(T, n_nodes, n_levels, start, SH, deadline)) {
+    if (tid == 0) write_status(out, si, kPathInternal, n_nodes, n_arcs);
+    return;
+  }
+  const LazyTables L = lazy_carve(T, ncap);
+  for (uint32_t i = tid; i < n_nodes; i += WG) {
+    L.lid[i] = i == start ? 0u : ~0u;
+    L.flg[i] = i == start ? kLzActive : 0u;
+    L.touch[i] = ~0u;
+  }
+  for (uint32_t i = tid; i <= n_nodes / 32; i += WG) L.bmap[i] = 0;
+  if (tid == 0) {
+    L.inv[0] = start;
+    L.act[0] = start;
+  }
+  __syncthreads();
+
+  uint32_t* A = L.act;
+  uint32_t* A2 = L.act2;
+  uint32_t na = 1, nxt = 1, popped = 0;
+  int32_t fail = kPathOk;
+  while (na > 0) {
+    // (1) dmin over the active nodes
+    unsigned long long m = kMaxU64;
+    for (uint32_t i = tid; i < na; i += WG) {
+      const unsigned long long d = ld_agent(&T.nd[A[i]]);
+      m = d < m ? d : m;
+    }
+    const unsigned long long dmin = block_min_u64<WG>(m, SH);
+    // (2) members (active at dmin) into the lid bitmap; lid range
+    uint32_t lo = ~0u, hi = 0;
+    for (uint32_t i = tid; i < na; i += WG) {
+      const uint32_t u = A[i];
+      if (ld_agent(&T.nd[u]) != dmin) continue;
+      const uint32_t l = L.lid[u];
+      atomicOr(&L.bmap[l >> 5], 1u << (l & 31));
+      lo = l < lo ? l : lo;
+      hi = l > hi ? l : hi;
+    }
+    lo = (uint32_t)(block_min_u64<WG>(lo, SH));
+    hi = ~(uint32_t)(block_min_u64<WG>((unsigned long long)(~hi), SH));
+    // (3) members in lid order: compact the bitmap words [lo/32, hi/32], clearing them
+    uint32_t ns = 0;
+    const uint32_t w0 = lo >> 5, w1 = hi >> 5;
+    for (uint32_t b = w0; b <= w1; b += WG) {
+      const uint32_t w = b + tid;
+      uint32_t bits = w <= w1 ? ld_agent(&L.bmap[w]) : 0u;
+      uint32_t tot;
+      uint32_t pos = ns + block_excl_scan<WG>((uint32_t)__builtin_popcount(bits), SH.scan, tot);
+      if (w <= w1) L.bmap[w] = 0;
+      while (bits) {
+        const uint32_t bit = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        L.slist[pos++] = L.inv[(w << 5) | bit];
+      }
+      ns += tot;
+    }
+    __syncthreads();
+    // (4) batch = longest lid-ordered prefix no earlier member's joiner undercuts
+    const double dminw = from_okey(dmin);
+    uint32_t k = ns, carry = ~0u;
+    for (uint32_t b = 0; b < ns; b += WG) {
+      const uint32_t p = b + tid;
+      uint32_t j = ~0u, my = 0;
+      if (p < ns) {
+        const uint32_t u = L.slist[p];
+        my = L.lid[u];
+        for (uint32_t a = T.aoff[u]; a < T.aoff[u + 1]; ++a) {
+          const uint32_t x = T.anext[a];
+          if (okey(w_times(dminw, T.aw[a])) != dmin || ld_agent(&T.nd[x]) != dmin) continue;
+          const uint32_t lx = L.lid[x];
+          if (lx != ~0u && (ld_agent(&L.flg[x]) & (kLzActive | kLzPopped)) == 0)
+            j = lx < j ? lx : j;
+        }
+      }
+      uint32_t tot;
+      uint32_t ex = block_excl_min<WG>(j, SH, tot);
+      ex = carry < ex ? carry : ex;
+      const uint32_t viol = (p < ns && my > ex) ? p : ~0u;
+      const uint32_t cut = (uint32_t)block_min_u64<WG>(viol, SH);
+      if (cut != ~0u) {
+        k = cut;
+        break;
+      }
+      carry = tot < carry ? tot : carry;
+    }
+    // (5) pop the batch: candidate ranks in (batch order, arc order)
+    uint32_t R = 0;
+    for (uint32_t b = 0; b < k; b += WG) {
+      const uint32_t p = b + tid;
+      uint32_t u = 0, a0 = 0, deg = 0;
+      if (p < k) {
+        u = L.slist[p];
+        a0 = T.aoff[u];
+        deg = T.aoff[u + 1] - a0;
+      }
+      uint32_t tot;
+      const uint32_t base = R + block_excl_scan<WG>(deg, SH.scan, tot);
+      if (p < k) {
+        L.flg[u] = kLzPopped;
+        for (uint32_t i = 0; i < deg; ++i) L.rk[base + i] = a0 + i;
+      }
+      R += tot;
+    }
+    if (tid == 0) SH.count = 0;
+    __syncthreads();
+    // (6) first touches; tight targets become active; survivors of the old list stay
+    for (uint32_t r = tid; r < R; r += WG) {
+      const uint32_t a = L.rk[r], x = T.anext[a];
+      if (L.lid[x] == ~0u) atomicMin(&L.touch[x], r);
+      if (okey(w_times(dminw, T.aw[a])) == ld_agent(&T.nd[x]) &&
+          (ld_agent(&L.flg[x]) & kLzPopped) == 0) {
+        const uint32_t old = atomicOr(&L.flg[x], kLzActive);
+        if ((old & kLzActive) == 0) A2[atomicAdd(&SH.count, 1u)] = x;
+      }
+    }
+    for (uint32_t i = tid; i < na; i += WG) {
+      const uint32_t u = A[i];
+      if ((ld_agent(&L.flg[u]) & kLzPopped) == 0) A2[atomicAdd(&SH.count, 1u)] = u;
+    }
+    __syncthreads();
+    // (7) fresh lids for the first touches, in rank order (K contiguous ranks per thread)
+    constexpr uint32_t K = 4;
+    uint32_t newc = 0;
+    for (uint32_t b = 0; b < R; b += WG * K) {
+      const uint32_t r0 = b + tid * K;
+      uint32_t mask = 0, nf = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < K; ++q) {
+        const uint32_t r = r0 + q;
+        if (r < R) {
+          const uint32_t x = T.anext[L.rk[r]];
+          if (ld_agent(&L.touch[x]) == r && L.lid[x] == ~0u) {
+            mask |= 1u << q;
+            ++nf;
+          }
+        }
+      }
+      uint32_t tot;
+      uint32_t rank = nxt + newc + block_excl_scan<WG>(nf, SH.scan, tot);
+#pragma unroll
+      for (uint32_t q = 0; q < K; ++q) {
+        if (mask & (1u << q)) {
+          const uint32_t x = T.anext[L.rk[r0 + q]];
+          L.lid[x] = rank;
+          L.inv[rank] = x;
+          ++rank;
+        }
+      }
+      newc += tot;
+    }
+    nxt += newc;
+    popped += k;
+    if (tid == 0) SH.flag = __builtin_amdgcn_s_memrealtime() > deadline;
+    __syncthreads();
+    na = SH.count;
+    const bool expired = SH.flag != 0;
+    __syncthreads();
+    uint32_t* t = A;
+    A = A2;
+    A2 = t;
+    if (expired || popped > n_nodes || nxt > n_nodes) {
+      fail = kPathInternal;
+      break;
+    }
+  }
+  if (fail == kPathOk && (popped != n_nodes || nxt != n_nodes)) fail = kPathInternal;
+  if (fail != kPathOk) {
+    if (tid == 0) write_status(out, si, fail, n_nodes, n_arcs);
+    return;
+  }
+
+  // back-pointers: lexmin (lid(source), il, ol, candidate order) over tight in-arcs; a
+  // source contributes only its own best tight arc into each target
+  for (uint32_t s = tid; s < n_nodes; s += WG) {
+    const double ds = from_okey(ld_agent(&T.nd[s]));
+    const uint32_t a0 = T.aoff[s], a1 = T.aoff[s + 1];
+    const unsigned long long ls = (unsigned long long)L.lid[s] << 32;
+    for (uint32_t a = a0; a < a1; ++a) {
+      const uint32_t x = T.anext[a];
+      const unsigned long long dx = ld_agent(&T.nd[x]);
+      if (okey(w_times(ds, T.aw[a])) != dx) continue;
+      const uint32_t il = T.ail[a], ol = T.aol[a];
+      bool win = true;
+      for (uint32_t c = a0; c < a1 && win; ++c) {
+        if (c == a || T.anext[c] != x) continue;
+        const uint32_t cil = T.ail[c], col = T.aol[c];
+        const bool before = cil < il || (cil == il && (col < ol || (col == ol && c < a)));
+        if (before && okey(w_times(ds, T.aw[c])) == dx) win = false;
+      }
+      if (win) atomicMin(&T.nback[x], ls | (a - a0));
+    }
+  }
+  // best final: lexmin (total, lid)
+  if (tid == 0) {
+    SH.best = kMaxU64;
+    SH.bestid = kEmptyKey;
+  }
+  __syncthreads();
+  unsigned long long mk = kMaxU64;
+  uint32_t ml = kEmptyKey;
+  for (uint32_t s = tid; s < n_nodes; s += WG) {
+    const double fw = T.nfin[s];
+    if (w_is_zero(fw)) continue;
+    const unsigned long long kk = okey(w_times(from_okey(ld_agent(&T.nd[s])), fw));
+    const uint32_t l = L.lid[s];
+    if (kk < mk || (kk == mk && l < ml)) {
+      mk = kk;
+      ml = l;
+    }
+  }
+  if (mk != kMaxU64) atomicMin(&SH.best, mk);
+  __syncthreads();
+  if (mk != kMaxU64 && mk == SH.best) atomicMin(&SH.bestid, ml);
+  __syncthreads();
+
+  if (tid == 0) {
+    if (SH.bestid == kEmptyKey) {
+      write_status(out, si, kPathEmpty, n_nodes, n_arcs);
+      return;
+    }
+    const uint32_t best = L.inv[SH.bestid];
+    // walk 1 (compose-shortest-path.zig:372-380): until the start id; bounded
+    uint32_t cur = best, hops = 0;
+    int32_t st = kPathOk;
+    while (cur != start) {
+      const unsigned long long b = ld_agent(&T.nback[cur]);
+      if (b == ~0ull) {
+        st = kPathEmpty;
+        break;
+      }
+      if (++hops > n_nodes) {
+        st = kPathCycle;
+        break;
+      }
+      cur = L.inv[(uint32_t)(b >> 32)];
+    }
+    if (st != kPathOk) {
+      write_status(out, si, st, n_nodes, n_arcs);
+      return;
+    }
+    const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)hops);
+    if (o + hops > out.arc_cap) {
+      write_status(out, si, kPathOutputFull, n_nodes, n_arcs);
+      return;
+    }
+    cur = best;
+    for (uint32_t k = hops; k > 0; --k) {  // walk 2: emit arcs back to front
+      const unsigned long long b = ld_agent(&T.nback[cur]);
+      const uint32_t s = L.inv[(uint32_t)(b >> 32)];
+      const uint32_t a = T.aoff[s] + (uint32_t)b;
+      out.out_il[o + k - 1] = T.ail[a];
+      out.out_ol[o + k - 1] = T.aol[a];
+      out.out_w[o + k - 1] = T.aw[a];
+      cur = s;
+    }
+    out.status[si] = kPathOk;
+    out.path_len[si] = hops;
+    out.path_off[si] = o;
+    out.final_w[si] = T.nfin[best];
+    if (out.work) {
+      out.work[2 * si] = n_nodes;
+      out.work[2 * si + 1] = n_arcs;
     }
   }
 }
@@ -545,7 +930,12 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       continue;
     }
 
-    bfs_shortest_path<WG>(T, n_nodes, n_arcs, n_levels, 0u, out, si, SH, t0 + 2 * ws.wd_ticks);
+    if (ws.lazy)
+      bfs_lazy_path<WG>(T, ws.ncap, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
+                        t0 + 2 * ws.wd_ticks);
+    else
+      bfs_shortest_path<WG>(T, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
+                            t0 + 2 * ws.wd_ticks);
   }
 }
 

@@ -1,0 +1,104 @@
+"""GPU parity of the parallel lazy engine (kernels/eager_bfs.hpp, bfs_lazy_path) and of the
+replay engine it replaces for finite weights >= 0 (kernels/lazy_wave.hpp), both against
+the oracle's sequential composeShortestPath (src/ops/compose-shortest-path.zig:26-401).
+
+FSTAMD_LAZY_ENGINE=replay forces the replay; unset, the rounds engine takes every rhs
+with finite arc weights >= 0 (engine 3 in fst_last_launch_stats)."""
+import math
+
+import numpy as np
+import pytest
+
+import libfst_amd as F
+import oracle_ffi as O
+from test_gpu_parity import LAZY, check, csr, load_blob, random_rhs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["rounds", "replay"])
+def engine(request, monkeypatch):
+    if request.param == "replay":
+        monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
+    else:
+        monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
+    return request.param
+
+
+def expect_engine(engine):
+    st = F.last_launch_stats()
+    assert st.engine == (3 if engine == "rounds" else 1)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_tie_heavy(engine, seed):
+    rng = np.random.default_rng(31000 + seed)
+    f = random_rhs(rng, int(rng.integers(2, 30)), int(rng.integers(4, 120)), 3,
+                   eps=seed % 4 != 3, wmax=2, frac=seed % 3 == 0)
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(0, 4, int(rng.integers(0, 10)))] for _ in range(48)]
+    check(blob, *csr(seqs), LAZY)
+    expect_engine(engine)
+
+
+def test_metric_shape(engine):
+    blob = O.freeze(O.gen("ambiguous", 4096, 12))
+    rhs = load_blob(blob)
+    seqs = [[1] * 64] * 6 + [[1] * L for L in (0, 1, 2, 17, 63, 128)] + [[1, 2, 1]]
+    check(blob, *csr(seqs), LAZY, rhs=rhs)
+    expect_engine(engine)
+
+
+@pytest.mark.parametrize("T,lens", [(64, (0, 1, 5, 12, 40)), (256, (11, 24, 40))])
+def test_epsilon_dense(engine, T, lens):
+    blob = O.freeze(O.gen("eps_dense", T, 12))
+    check(blob, *csr([[1] * L for L in lens]), LAZY)
+    expect_engine(engine)
+
+
+def test_zero_weight_cycles_through_start(engine):
+    # start carries 0-weight self loops and a 0-weight 2-cycle: the lazy backtrace stops
+    # at the start id (compose-shortest-path.zig:372), so these are not CYCLE
+    f = O.Fst()
+    for _ in range(3):
+        f.add_state(math.inf)
+    f.start = 0
+    f.finals[2] = 0.0
+    f.add_arc(0, 0, 5, 0.0, 0)
+    f.add_arc(0, 1, 6, 0.0, 1)
+    f.add_arc(1, 0, 7, 0.0, 0)
+    f.add_arc(1, 1, 8, 0.0, 2)
+    f.add_arc(2, 0, 9, 0.0, 1)
+    check(O.freeze(f), *csr([[1], [1, 1], [1, 1, 1], []]), LAZY)
+    expect_engine(engine)
+
+
+def test_infinite_arc_weights_use_the_replay(monkeypatch):
+    monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
+    f = O.Fst()
+    for _ in range(3):
+        f.add_state(math.inf)
+    f.start = 0
+    f.finals[2] = 0.0
+    f.add_arc(0, 1, 1, math.inf, 1)
+    f.add_arc(0, 1, 2, 1.0, 1)
+    f.add_arc(1, 1, 3, 0.0, 2)
+    check(O.freeze(f), *csr([[1, 1], [1], [1, 1, 1]]), LAZY)
+    assert F.last_launch_stats().engine == 1
+
+
+def test_engines_agree_on_a_large_varied_batch(monkeypatch):
+    blob = O.freeze(O.gen("ambiguous", 4096, 12))
+    rhs = load_blob(blob)
+    rng = np.random.default_rng(77)
+    seqs = [[int(x) for x in (rng.random(int(L)) < 0.02) + 1] for L in rng.integers(0, 65, 2048)]
+    labels, offsets = csr(seqs)
+    monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
+    a = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, LAZY)
+    monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
+    b = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, LAZY)
+    assert np.array_equal(a.status, b.status)
+    assert np.array_equal(a.offsets, b.offsets)
+    assert np.array_equal(a.ilabels, b.ilabels) and np.array_equal(a.olabels, b.olabels)
+    assert np.array_equal(a.weights.view(np.uint64), b.weights.view(np.uint64))
+    assert np.array_equal(a.finals.view(np.uint64), b.finals.view(np.uint64))
