@@ -630,7 +630,11 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     const BfsCaps c = bfs_caps(tier);
     const uint64_t fit = std::max<uint64_t>(1, kBfsBudget / c.stride);
     if (kBfsBudget < c.stride) break;  // beyond the budget: those strings stay OVERFLOW
-    const uint64_t per_cu = tier == 0 ? kBfsWgPerCu0 : 1;
+    // tier 0: small lattices -> one wavefront per string by default (wave-level
+    // barriers, 4x the strings in flight); FSTAMD_BFS_WG0=256 for A/B runs
+    const char* wge = std::getenv("FSTAMD_BFS_WG0");
+    const bool wave = tier == 0 && !(wge && std::strcmp(wge, "256") == 0);
+    const uint64_t per_cu = tier == 0 ? (wave ? 4 * kBfsWgPerCu0 : kBfsWgPerCu0) : 1;
     const uint32_t grid =
         (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_ * per_cu, fit});
     BfsWs ws{};
@@ -645,11 +649,33 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     ws.wd_ticks = watchdog_ticks();
     ws.lattice_only = 0;
     ws.lazy = lazy ? 1u : 0u;
+    const bool prof = std::getenv("FSTAMD_BFS_PROF") != nullptr;
+    ws.prof = prof ? (unsigned long long*)scratch(kDebug, (size_t)grid * 64) : nullptr;
+    if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)grid * 64, stream));
     HIP_TRY(hipMemsetAsync(cnt + 1, 0, 8, stream));  // item counter + next list count
     GraphInput none{};
-    eager_bfs_kernel<kBfsWG, false><<<grid, kBfsWG, 0, stream>>>(
-        rhs.view, in, none, n, cnt + 1, list, cnt, 0, ws, out);
+    if (wave)
+      eager_bfs_kernel<64, false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1, list,
+                                                           cnt, 0, ws, out);
+    else
+      eager_bfs_kernel<kBfsWG, false><<<grid, kBfsWG, 0, stream>>>(rhs.view, in, none, n, cnt + 1,
+                                                                   list, cnt, 0, ws, out);
     HIP_TRY(hipGetLastError());
+    if (ws.prof) {  // phase profile: sums over workgroups, ticks at 100 MHz
+      std::vector<unsigned long long> h((size_t)grid * 8);
+      HIP_TRY(hipMemcpyAsync(h.data(), ws.prof, h.size() * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      unsigned long long sum[8] = {};
+      for (size_t i = 0; i < h.size(); ++i) sum[i % 8] += h[i];
+      std::fprintf(stderr,
+                   "[bfs prof] tier %d grid %u wg %d items %llu | us/item: compose %.1f "
+                   "fixpoint %.1f rounds %.1f tail %.1f | rounds/item %.1f active/round %.1f "
+                   "members/round %.1f\n",
+                   tier, grid, wave ? 64 : kBfsWG, sum[4], sum[0] / 100.0 / sum[4],
+                   sum[1] / 100.0 / sum[4], sum[2] / 100.0 / sum[4], sum[3] / 100.0 / sum[4],
+                   (double)sum[5] / sum[4], (double)sum[6] / std::max(1ull, sum[5]),
+                   (double)sum[7] / std::max(1ull, sum[5]));
+    }
     // strings that overflowed this tier move on to the next one
     collect_list_kernel<<<(count + 255) / 256, 256, 0, stream>>>(list, cnt, out.status,
                                                                  kPathOverflow, list2, cnt + 2);

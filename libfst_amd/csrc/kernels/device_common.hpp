@@ -93,6 +93,25 @@ __device__ __forceinline__ void span_by_ilabel(const RhsView& r, uint32_t s, uin
   hi = off + a;
 }
 
+// arcsByIlabel (src/fst.zig:112-136) with the per-state summary: one 16-B load when all
+// arcs of the state share an ilabel (or it has none), binary search otherwise.
+__device__ __forceinline__ void span_summary(const RhsView& r, uint32_t s, uint32_t label,
+                                             uint32_t& lo, uint32_t& cnt) {
+  const uint4 ss = r.sspan[FB(s, r.num_states, 30)];
+  if (ss.z == label) {
+    lo = ss.x;
+    cnt = ss.y;
+  } else if (ss.z != kSpanMixed) {
+    lo = ss.x;
+    cnt = 0;
+  } else {
+    uint32_t a, b;
+    span_by_ilabel(r, s, label, a, b);
+    lo = a;
+    cnt = b - a;
+  }
+}
+
 // Wavefront inclusive prefix sum (64 lanes).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   const int lane = threadIdx.x & 63;

@@ -39,7 +39,24 @@ struct BfsWs {
   unsigned long long wd_ticks;
   uint32_t lattice_only;    // 1: stop after compose (fst_compose_frozen)
   uint32_t lazy;            // 1: composeShortestPath semantics (bfs_lazy_path)
+  unsigned long long* prof; // [grid * 8] phase ticks (FSTAMD_BFS_PROF) or null
 };
+
+// Phase profile (thread 0): prof[slot] += ticks since *tp; *tp = now.  Slots: 0 compose,
+// 1 fixpoint, 2 lazy rounds, 3 back/best/backtrace, 4 items, 5 rounds, 6 sum of active
+// list lengths, 7 sum of members.
+__device__ __forceinline__ void prof_mark(unsigned long long* prof, int slot,
+                                          unsigned long long* tp) {
+  if (prof && threadIdx.x == 0) {
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    prof[slot] += now - *tp;
+    *tp = now;
+  }
+}
+__device__ __forceinline__ void prof_add(unsigned long long* prof, int slot,
+                                         unsigned long long v) {
+  if (prof && threadIdx.x == 0) prof[slot] += v;
+}
 
 struct BfsTables {
   unsigned long long* hkey;  // [hcap] tuple key, ~0 = free
@@ -54,7 +71,7 @@ struct BfsTables {
   uint32_t* ail;
   uint32_t* aol;
   double* aw;
-  uint32_t* cslot;           // [acap] hash slot of the arc's target (level scratch)
+  uint32_t* cslot;           // [acap + ncap] hash slot of the arc's target (level scratch)
 };
 
 __host__ __device__ inline size_t bfs_slab_bytes(uint32_t ncap, uint32_t acap, uint32_t hcap,
@@ -63,7 +80,7 @@ __host__ __device__ inline size_t bfs_slab_bytes(uint32_t ncap, uint32_t acap, u
   return r((size_t)hcap * 8) + r((size_t)hcap * 4) + r((size_t)ncap * 8) +
          r(((size_t)ncap + 1) * 4) + r(((size_t)lcap + 2) * 4) + r((size_t)ncap * 8) +
          r((size_t)ncap * 8) + r((size_t)ncap * 8) + r((size_t)acap * 4) * 3 +
-         r((size_t)acap * 8) + r((size_t)acap * 4);
+         r((size_t)acap * 8) + r(((size_t)acap + ncap) * 4);
 }
 
 __device__ inline BfsTables bfs_carve(uint8_t* p, uint32_t ncap, uint32_t acap, uint32_t hcap,
@@ -86,7 +103,7 @@ __device__ inline BfsTables bfs_carve(uint8_t* p, uint32_t ncap, uint32_t acap, 
   t.ail = (uint32_t*)take((size_t)acap * 4);
   t.aol = (uint32_t*)take((size_t)acap * 4);
   t.aw = (double*)take((size_t)acap * 8);
-  t.cslot = (uint32_t*)take((size_t)acap * 4);
+  t.cslot = (uint32_t*)take(((size_t)acap + ncap) * 4);
   return t;
 }
 
@@ -150,9 +167,9 @@ __device__ __forceinline__ void bfs_expand(const RhsView& rhs, const BfsLhs<kGra
     double w;
     lhs.arc(s1, i, il, ol, w, nx);
     if (ol == kEpsilon) continue;
-    uint32_t lo, hi;
-    span_by_ilabel(rhs, s2, ol, lo, hi);
-    for (uint32_t a = lo; a < hi; ++a) {
+    uint32_t lo, cnt;
+    span_summary(rhs, s2, ol, lo, cnt);
+    for (uint32_t a = lo; a < lo + cnt; ++a) {
       const ArcRec r = rhs.rec[a];
       emit(il, r.olabel, w_times(w, r.weight), bfs_key(nx, r.next, 0));
     }
@@ -167,8 +184,9 @@ __device__ __forceinline__ void bfs_expand(const RhsView& rhs, const BfsLhs<kGra
       emit(il, kEpsilon, w, bfs_key(nx, s2, nf));
     }
   }
-  uint32_t elo, ehi;
-  span_by_ilabel(rhs, s2, kEpsilon, elo, ehi);
+  uint32_t elo, ecnt;
+  span_summary(rhs, s2, kEpsilon, elo, ecnt);
+  const uint32_t ehi = elo + ecnt;
   if (f != 2) {  // phase 3: rhs epsilon input alone
     const uint32_t nf = f == 0 ? 1u : f;
     for (uint32_t a = elo; a < ehi; ++a) {
@@ -204,16 +222,20 @@ struct BfsShared {
 
 // Least fixpoint of d(X) = min fl(d(s) + w) from d(start) = One, by Gauss-Seidel sweeps
 // over the BFS levels (lvl[0..n_levels]); also clears nback.  The whole workgroup calls
-// it; false = the deadline passed (uniform).
+// it; false = the deadline passed (uniform).  `init`: start from d = (One at the start,
+// Zero elsewhere); otherwise nd already holds path sums (compose relaxed every level in
+// order), and `dag` (every arc goes to the next level) means they are already final.
 template <int WG>
 __device__ bool bfs_fixpoint(const BfsTables& T, uint32_t n_nodes, uint32_t n_levels,
-                             uint32_t start, BfsShared& SH, unsigned long long deadline) {
+                             uint32_t start, BfsShared& SH, unsigned long long deadline,
+                             bool init = true, bool dag = false) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < n_nodes; i += WG) {
-    T.nd[i] = i == start ? okey(w_one()) : okey(w_zero());
+    if (init) T.nd[i] = i == start ? okey(w_one()) : okey(w_zero());
     T.nback[i] = ~0ull;
   }
   __syncthreads();
+  if (dag) return true;
   for (uint32_t sweep = 0;; ++sweep) {
     if (tid == 0) SH.changed = 0;
     __syncthreads();
@@ -246,9 +268,10 @@ __device__ bool bfs_fixpoint(const BfsTables& T, uint32_t n_nodes, uint32_t n_le
 template <int WG>
 __device__ void bfs_shortest_path(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
                                   uint32_t n_levels, uint32_t start, const BatchOutDev& out,
-                                  uint32_t si, BfsShared& SH, unsigned long long deadline) {
+                                  uint32_t si, BfsShared& SH, unsigned long long deadline,
+                                  bool init = true, bool dag = false) {
   const uint32_t tid = threadIdx.x;
-  if (!bfs_fixpoint<WG>(T, n_nodes, n_levels, start, SH, deadline)) {
+  if (!bfs_fixpoint<WG>(T, n_nodes, n_levels, start, SH, deadline, init, dag)) {
     if (tid == 0) write_status(out, si, kPathInternal, n_nodes, n_arcs);
     return;
   }
@@ -422,9 +445,11 @@ struct LazyTables {
   uint32_t* act;    // [n] active nodes (unordered)
   uint32_t* act2;   // [n] next round's active nodes
   uint32_t* slist;  // [n] this round's dmin members in lid order
+  uint32_t* mbase;  // [n] rank of each member's header entry in rk
   uint32_t* bmap;   // [n / 32 + 1] lid bitmap of the members (clear between rounds)
-  uint32_t* rk;     // [arcs] arc index of each candidate rank of the round
+  uint32_t* rk;     // [arcs + n] per member: header (kLzHdr | member), then its arcs
 };
+constexpr uint32_t kLzHdr = 0x80000000u;
 constexpr uint32_t kLzActive = 1u, kLzPopped = 2u;
 
 __device__ inline LazyTables lazy_carve(const BfsTables& T, uint32_t ncap) {
@@ -437,6 +462,7 @@ __device__ inline LazyTables lazy_carve(const BfsTables& T, uint32_t ncap) {
   L.act = T.hval;                   // 4 * hcap >= 8 * ncap bytes
   L.act2 = T.hval + ncap;
   L.slist = (uint32_t*)T.nkey;      // 8 * ncap bytes
+  L.mbase = (uint32_t*)T.nkey + ncap;
   L.bmap = T.lvl;                   // 4 * (ncap + 2) bytes
   L.rk = T.cslot;
   return L;
@@ -446,9 +472,12 @@ template <int WG>
 __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_nodes,
                               uint32_t n_arcs, uint32_t n_levels, uint32_t start,
                               const BatchOutDev& out, uint32_t si, BfsShared& SH,
-                              unsigned long long deadline) {
+                              unsigned long long deadline, unsigned long long* prof,
+                              unsigned long long* tp, bool dag) {
   const uint32_t tid = threadIdx.x;
-  if (!bfs_fixpoint<WG>(T, n_nodes, n_levels, start, SH, deadline)) {
+  const bool fix_ok = bfs_fixpoint<WG>(T, n_nodes, n_levels, start, SH, deadline, false, dag);
+  prof_mark(prof, 1, tp);
+  if (!fix_ok) {
     if (tid == 0) write_status(out, si, kPathInternal, n_nodes, n_arcs);
     return;
   }
@@ -470,6 +499,8 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
   uint32_t na = 1, nxt = 1, popped = 0;
   int32_t fail = kPathOk;
   while (na > 0) {
+    prof_add(prof, 5, 1);
+    prof_add(prof, 6, na);
     // (1) dmin over the active nodes
     unsigned long long m = kMaxU64;
     for (uint32_t i = tid; i < na; i += WG) {
@@ -505,28 +536,54 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
       }
       ns += tot;
     }
+    prof_add(prof, 7, ns);
     __syncthreads();
-    // (4) batch = longest lid-ordered prefix no earlier member's joiner undercuts
-    const double dminw = from_okey(dmin);
-    uint32_t k = ns, carry = ~0u;
+    // (4) rank list: per member (lid order) a header entry, then its arcs (candidate
+    // order); the batch's candidates are the ranks before the first unpopped header
+    uint32_t RA = 0;
     for (uint32_t b = 0; b < ns; b += WG) {
       const uint32_t p = b + tid;
-      uint32_t j = ~0u, my = 0;
+      uint32_t a0 = 0, deg = 0;
       if (p < ns) {
         const uint32_t u = L.slist[p];
-        my = L.lid[u];
-        for (uint32_t a = T.aoff[u]; a < T.aoff[u + 1]; ++a) {
-          const uint32_t x = T.anext[a];
-          if (okey(w_times(dminw, T.aw[a])) != dmin || ld_agent(&T.nd[x]) != dmin) continue;
-          const uint32_t lx = L.lid[x];
-          if (lx != ~0u && (ld_agent(&L.flg[x]) & (kLzActive | kLzPopped)) == 0)
-            j = lx < j ? lx : j;
+        a0 = T.aoff[u];
+        deg = T.aoff[u + 1] - a0;
+      }
+      uint32_t tot;
+      const uint32_t base = RA + block_excl_scan<WG>(p < ns ? deg + 1 : 0u, SH.scan, tot);
+      if (p < ns) {
+        L.mbase[p] = base;
+        L.rk[base] = kLzHdr | p;
+        for (uint32_t i = 0; i < deg; ++i) L.rk[base + 1 + i] = a0 + i;
+      }
+      RA += tot;
+    }
+    __syncthreads();
+    // (5) batch = longest lid-ordered prefix no earlier member's joiner undercuts: per
+    // arc the joiner lid (an older, inactive node it reaches tightly at dmin), an
+    // exclusive prefix minimum in rank order, checked at every member's header
+    const double dminw = from_okey(dmin);
+    uint32_t k = ns, carry = ~0u;
+    for (uint32_t b = 0; b < RA; b += WG) {
+      const uint32_t r = b + tid;
+      uint32_t j = ~0u, my = 0, hp = ~0u;
+      if (r < RA) {
+        const uint32_t e = L.rk[r];
+        if (e & kLzHdr) {
+          hp = e & ~kLzHdr;
+          my = L.lid[L.slist[hp]];
+        } else {
+          const uint32_t x = T.anext[e];
+          if (okey(w_times(dminw, T.aw[e])) == dmin && ld_agent(&T.nd[x]) == dmin) {
+            const uint32_t lx = L.lid[x];
+            if (lx != ~0u && (ld_agent(&L.flg[x]) & (kLzActive | kLzPopped)) == 0) j = lx;
+          }
         }
       }
       uint32_t tot;
       uint32_t ex = block_excl_min<WG>(j, SH, tot);
       ex = carry < ex ? carry : ex;
-      const uint32_t viol = (p < ns && my > ex) ? p : ~0u;
+      const uint32_t viol = (hp != ~0u && my > ex) ? hp : ~0u;
       const uint32_t cut = (uint32_t)block_min_u64<WG>(viol, SH);
       if (cut != ~0u) {
         k = cut;
@@ -534,29 +591,15 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
       }
       carry = tot < carry ? tot : carry;
     }
-    // (5) pop the batch: candidate ranks in (batch order, arc order)
-    uint32_t R = 0;
-    for (uint32_t b = 0; b < k; b += WG) {
-      const uint32_t p = b + tid;
-      uint32_t u = 0, a0 = 0, deg = 0;
-      if (p < k) {
-        u = L.slist[p];
-        a0 = T.aoff[u];
-        deg = T.aoff[u + 1] - a0;
-      }
-      uint32_t tot;
-      const uint32_t base = R + block_excl_scan<WG>(deg, SH.scan, tot);
-      if (p < k) {
-        L.flg[u] = kLzPopped;
-        for (uint32_t i = 0; i < deg; ++i) L.rk[base + i] = a0 + i;
-      }
-      R += tot;
-    }
+    const uint32_t R = k < ns ? L.mbase[k] : RA;
+    for (uint32_t p = tid; p < k; p += WG) L.flg[L.slist[p]] = kLzPopped;
     if (tid == 0) SH.count = 0;
     __syncthreads();
     // (6) first touches; tight targets become active; survivors of the old list stay
     for (uint32_t r = tid; r < R; r += WG) {
-      const uint32_t a = L.rk[r], x = T.anext[a];
+      const uint32_t a = L.rk[r];
+      if (a & kLzHdr) continue;
+      const uint32_t x = T.anext[a];
       if (L.lid[x] == ~0u) atomicMin(&L.touch[x], r);
       if (okey(w_times(dminw, T.aw[a])) == ld_agent(&T.nd[x]) &&
           (ld_agent(&L.flg[x]) & kLzPopped) == 0) {
@@ -578,8 +621,9 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
 #pragma unroll
       for (uint32_t q = 0; q < K; ++q) {
         const uint32_t r = r0 + q;
-        if (r < R) {
-          const uint32_t x = T.anext[L.rk[r]];
+        const uint32_t a = r < R ? L.rk[r] : kLzHdr;
+        if (!(a & kLzHdr)) {
+          const uint32_t x = T.anext[a];
           if (ld_agent(&L.touch[x]) == r && L.lid[x] == ~0u) {
             mask |= 1u << q;
             ++nf;
@@ -614,6 +658,7 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
       break;
     }
   }
+  prof_mark(prof, 2, tp);
   if (fail == kPathOk && (popped != n_nodes || nxt != n_nodes)) fail = kPathInternal;
   if (fail != kPathOk) {
     if (tid == 0) write_status(out, si, fail, n_nodes, n_arcs);
@@ -626,6 +671,36 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
     const double ds = from_okey(ld_agent(&T.nd[s]));
     const uint32_t a0 = T.aoff[s], a1 = T.aoff[s + 1];
     const unsigned long long ls = (unsigned long long)L.lid[s] << 32;
+    if (a1 - a0 <= 8) {  // registers: independent loads, then a tight-arc bitmask
+      constexpr int M = 8;
+      uint32_t nx[M], tight = 0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) nx[i] = a0 + i < a1 ? T.anext[a0 + i] : ~0u;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (nx[i] == ~0u) continue;
+        if (okey(w_times(ds, T.aw[a0 + i])) == ld_agent(&T.nd[nx[i]])) tight |= 1u << i;
+      }
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (!(tight & (1u << i))) continue;
+        uint32_t rivals = 0;  // other tight arcs of s into the same target
+#pragma unroll
+        for (int c = 0; c < M; ++c)
+          if (c != i && (tight & (1u << c)) && nx[c] == nx[i]) rivals |= 1u << c;
+        bool win = true;
+        if (rivals) {
+          const uint32_t il = T.ail[a0 + i], ol = T.aol[a0 + i];
+          for (int c = 0; c < M && win; ++c) {
+            if (!(rivals & (1u << c))) continue;
+            const uint32_t cil = T.ail[a0 + c], col = T.aol[a0 + c];
+            if (cil < il || (cil == il && (col < ol || (col == ol && c < i)))) win = false;
+          }
+        }
+        if (win) atomicMin(&T.nback[nx[i]], ls | (uint32_t)i);
+      }
+      continue;
+    }
     for (uint32_t a = a0; a < a1; ++a) {
       const uint32_t x = T.anext[a];
       const unsigned long long dx = ld_agent(&T.nd[x]);
@@ -725,6 +800,7 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
   BfsTables T = bfs_carve(ws.slab + (size_t)blockIdx.x * ws.stride, ws.ncap, ws.acap, ws.hcap,
                           ws.lcap);
   uint32_t* hdr = ws.hdr + (size_t)blockIdx.x * 8;
+  unsigned long long* prof = ws.prof ? ws.prof + (size_t)blockIdx.x * 8 : nullptr;
   const uint32_t num_items = num_items_dev ? *num_items_dev : num_items_host;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t hmask = ws.hcap - 1;
@@ -740,6 +816,8 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
     if (item >= num_items) break;
     const uint32_t si = items ? items[item] : item;
 
+    unsigned long long tp = __builtin_amdgcn_s_memrealtime();
+    prof_add(prof, 4, 1);
     BfsLhs<kGraph> lhs;
     lhs.g = graph;
     lhs.labels = nullptr;
@@ -782,6 +860,7 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       T.hkey[h] = k0;
       T.hval[h] = 0;
       T.nkey[0] = k0;
+      T.nd[0] = okey(w_one());
       T.lvl[0] = 0;
       T.lvl[1] = 1;
       T.aoff[0] = 0;
@@ -789,6 +868,8 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
     __syncthreads();
     uint32_t n_nodes = 1, n_arcs = 0, level = 0;
     int32_t fail = kPathOk;
+    if (tid == 0) SH.changed = 0;  // (E) sets it on a backward arc
+    __syncthreads();
     while (true) {
       const uint32_t f0 = level == 0 ? 0u : ld_agent(&T.lvl[level]);
       const uint32_t f1 = n_nodes;
@@ -885,6 +966,7 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
                 const uint32_t id = n_nodes + newc + rank++;
                 T.hval[slot] = id;
                 T.nkey[id] = ld_agent(&T.hkey[slot]);
+                T.nd[id] = okey(w_zero());
               }
             }
           }
@@ -899,6 +981,22 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       }
       // (D) arc targets
       for (uint32_t a = c0 + tid; a < c1; a += WG) T.anext[a] = ld_agent(&T.hval[T.cslot[a]]);
+      // (E) relax the level's arcs in level order (exact for a DAG by levels: no arc into
+      // this or an earlier level); a backward arc leaves the rest to bfs_fixpoint's sweeps
+      if (!ws.lattice_only) {
+        __syncthreads();
+        bool back = false;
+        for (uint32_t p = f0 + tid; p < f1; p += WG) {
+          const double ds = from_okey(ld_agent(&T.nd[p]));
+          const uint32_t a1 = T.aoff[p + 1];
+          for (uint32_t a = T.aoff[p]; a < a1; ++a) {
+            const uint32_t x = T.anext[a];
+            back |= x < f1;
+            if (!w_is_zero(ds)) atomicMin(&T.nd[x], okey(w_times(ds, T.aw[a])));
+          }
+        }
+        if (back) SH.changed = 1;  // reset before the level loop
+      }
       n_arcs = c1;
       n_nodes += newc;
       ++level;
@@ -914,6 +1012,9 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       }
     }
     const uint32_t n_levels = level;
+    prof_mark(prof, 0, &tp);
+    __syncthreads();
+    const bool dag = SH.changed == 0;
 
     if (ws.lattice_only) {
       if (tid == 0) {
@@ -930,12 +1031,13 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       continue;
     }
 
-    if (ws.lazy)
+    if (ws.lazy) {
       bfs_lazy_path<WG>(T, ws.ncap, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
-                        t0 + 2 * ws.wd_ticks);
-    else
+                        t0 + 2 * ws.wd_ticks, prof, &tp, dag);
+      prof_mark(prof, 3, &tp);
+    } else
       bfs_shortest_path<WG>(T, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
-                            t0 + 2 * ws.wd_ticks);
+                            t0 + 2 * ws.wd_ticks, false, dag);
   }
 }
 

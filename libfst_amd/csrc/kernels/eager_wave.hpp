@@ -63,23 +63,9 @@ __device__ __forceinline__ uint32_t wave_excl_scan_small(uint32_t v, uint32_t& t
   return pre;
 }
 
-// arcsByIlabel (src/fst.zig:112-136) with the per-state summary: one 16-B load when all
-// arcs of the state share an ilabel (or it has none), binary search otherwise.
 __device__ __forceinline__ void wave_span(const RhsView& r, uint32_t s, uint32_t label,
                                           uint32_t& lo, uint32_t& cnt) {
-  const uint4 ss = r.sspan[FB(s, r.num_states, 30)];
-  if (ss.z == label) {
-    lo = ss.x;
-    cnt = ss.y;
-  } else if (ss.z != kSpanMixed) {
-    lo = ss.x;
-    cnt = 0;
-  } else {
-    uint32_t a, b;
-    span_by_ilabel(r, s, label, a, b);
-    lo = a;
-    cnt = b - a;
-  }
+  span_summary(r, s, label, lo, cnt);
 }
 
 // Spans of the owned tuples for `label` (row e holds position e*64 + lane), then the
