@@ -13,6 +13,7 @@
 
 #include "host_fst.hpp"
 #include "kernels/eager_bfs.hpp"
+#include "kernels/lazy_layered.hpp"
 #include "kernels/eager_layered.hpp"
 #include "kernels/eager_wave.hpp"
 #include "kernels/lazy_wave.hpp"
@@ -171,6 +172,11 @@ constexpr int kEwFcap = 64 * kEwEmax;
 constexpr int kEwHcap = 512;
 constexpr int kEwKmax = 5;
 
+// Item counters and list counts, one 256-B block shared by the engines (word ranges):
+// run_chain [0..4], lazy replay retry tiers [6..13], run_bfs_chain [8..11] (never in the
+// same call as the replay tiers), run_lazy_layered [32].
+constexpr size_t kCounterBytes = 256;
+
 enum Scratch : size_t {
   kCounter = 0,
   kElBack,
@@ -194,6 +200,14 @@ enum Scratch : size_t {
   kBfsList2,
   kProjCount,
   kProjTemp,
+  kLlDk,
+  kLlBack,
+  kLlLidf,
+  kLlFlg,
+  kLlNodes,
+  kLlInv,
+  kLlLoff,
+  kLlAct,
   kNumScratch
 };
 
@@ -319,7 +333,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                                    int semantics, const BatchOutDev& out, hipStream_t stream,
                                    LaunchStats* stats) {
   HIP_TRY(hipSetDevice(dev_));
-  unsigned int* counter = (unsigned int*)scratch(kCounter, 64);
+  unsigned int* counter = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!counter) return hipErrorOutOfMemory;
   HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
   HIP_TRY(hipMemsetAsync(out.cursor, 0, sizeof(unsigned long long), stream));
@@ -458,14 +472,32 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   // Lazy semantics.  Finite weights >= 0 -> the parallel rounds engine (eager_bfs.hpp,
   // bfs_lazy_path), one workgroup per string.  Otherwise (+inf arcs, negative weights),
   // or with FSTAMD_LAZY_ENGINE=replay, the exact replay, one wavefront per string.
+  // Unset: rounds for layered lattices and for large ones; small non-layered lattices
+  // ((max_len + 1) * NS <= 16K bounds the tuples, e.g. config 4's tagger) replay faster.
+  // FSTAMD_LAZY_ENGINE=rounds | replay forces one engine (A/B runs, tests).
   const char* le = std::getenv("FSTAMD_LAZY_ENGINE");
-  const bool use_rounds = rhs.nonneg && rhs.finite && !(le && std::strcmp(le, "replay") == 0);
+  const bool force_rounds = le && std::strcmp(le, "rounds") == 0;
+  const bool force_replay = le && std::strcmp(le, "replay") == 0;
+  const bool small = (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
+  const bool use_rounds = rhs.nonneg && rhs.finite && !force_replay &&
+                          (force_rounds || !rhs.has_eps || !small);
   if (use_rounds) {
     if (stats) {
       stats->engine = 3;
       HIP_TRY(hipEventRecord(ev0_, stream));
     }
-    HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, true, true));
+    // Layered lattices (no rhs input epsilon; label-0 inputs are sent on as UNSUPPORTED):
+    // the one-wave dense engine (kernels/lazy_layered.hpp), FSTAMD_LAZY_LAYERED=0 skips
+    // it; the general rounds engine takes everything else and its leftovers.
+    const char* ll = std::getenv("FSTAMD_LAZY_LAYERED");
+    const bool layered = !rhs.has_eps && rhs.view.max_span <= kLlSpanMax &&
+                         (uint64_t)(in.max_len + 1) * rhs.view.num_states <= kLlDenseMax &&
+                         !(ll && std::strcmp(ll, "0") == 0);
+    if (layered) {
+      if (stats) stats->engine = 4;
+      HIP_TRY(run_lazy_layered(rhs, in, n, out, stream));
+    }
+    HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !layered, true));
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
@@ -603,10 +635,70 @@ __global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_
   if (i < *in_count && status[in_list[i]] == code) list[atomicAdd(count, 1u)] = in_list[i];
 }
 
+// One-wave dense lazy engine for layered lattices.  Its per-wave dense arrays are left
+// clean by every string, so they are initialised only when (re)allocated.
+hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput& in,
+                                          uint32_t n, const BatchOutDev& out,
+                                          hipStream_t stream) {
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [32] is ours
+  if (!ctr) return hipErrorOutOfMemory;
+  LlWs ws{};
+  ws.lcap = in.max_len;
+  ws.dn = (uint64_t)(in.max_len + 1) * rhs.view.num_states;
+  ws.ncap = (uint32_t)ws.dn;
+  ws.wd_ticks = watchdog_ticks();
+  ws.acap = (uint32_t)std::min<uint64_t>(ws.dn, 1u << 15);
+  const uint64_t per_wave = ws.dn * (8 + 8 + 4 + 4 + 4 + 4) + ((uint64_t)ws.lcap + 2) * 4 +
+                            (uint64_t)ws.acap * 32;
+  const uint64_t budget = 48ull << 30;  // of the 288 GB: all 16 waves per CU at the metric
+  uint32_t grid = (uint32_t)std::min<uint64_t>(
+      {(uint64_t)num_cus_ * 16, (uint64_t)in.num_strings, std::max<uint64_t>(1, budget / per_wave)});
+  grid = std::max<uint32_t>(grid, 1);
+  const size_t g = grid;
+  ws.dk = (unsigned long long*)scratch(kLlDk, g * ws.dn * 8);
+  ws.back = (unsigned long long*)scratch(kLlBack, g * ws.dn * 8);
+  ws.lidf = (uint32_t*)scratch(kLlLidf, g * ws.dn * 4);
+  ws.flg = (uint32_t*)scratch(kLlFlg, g * ws.dn * 4);
+  ws.nodes = (uint32_t*)scratch(kLlNodes, g * ws.dn * 4);
+  ws.inv = (uint32_t*)scratch(kLlInv, g * ws.dn * 4);
+  ws.loff = (uint32_t*)scratch(kLlLoff, g * ((size_t)ws.lcap + 2) * 4);
+  ws.act = (uint4*)scratch(kLlAct, g * 2 * (size_t)ws.acap * sizeof(uint4));
+  if (!ws.dk || !ws.back || !ws.lidf || !ws.flg || !ws.nodes || !ws.inv || !ws.loff || !ws.act)
+    return hipErrorOutOfMemory;
+  if (ll_clean_ != bufs_[kLlDk] || ll_clean_bytes_ != sizes_[kLlDk]) {  // new allocation
+    HIP_TRY(hipMemsetAsync(ws.dk, 0xFF, sizes_[kLlDk], stream));
+    HIP_TRY(hipMemsetAsync(ws.back, 0xFF, sizes_[kLlBack], stream));
+    HIP_TRY(hipMemsetAsync(ws.lidf, 0xFF, sizes_[kLlLidf], stream));
+    HIP_TRY(hipMemsetAsync(ws.flg, 0, sizes_[kLlFlg], stream));
+    ll_clean_ = bufs_[kLlDk];
+    ll_clean_bytes_ = sizes_[kLlDk];
+  }
+  HIP_TRY(hipMemsetAsync(ctr + 32, 0, 4, stream));
+  const bool prof = std::getenv("FSTAMD_BFS_PROF") != nullptr;
+  ws.prof = prof ? (unsigned long long*)scratch(kDebug, g * 64) : nullptr;
+  if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, g * 64, stream));
+  lazy_layered_kernel<<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr + 32, ws, out);
+  HIP_TRY(hipGetLastError());
+  if (ws.prof) {  // phase profile: sums over waves, ticks at 100 MHz
+    std::vector<unsigned long long> h(g * 8);
+    HIP_TRY(hipMemcpyAsync(h.data(), ws.prof, h.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    unsigned long long sum[8] = {};
+    for (size_t i = 0; i < h.size(); ++i) sum[i % 8] += h[i];
+    const double it = (double)std::max(1ull, sum[4]);
+    std::fprintf(stderr,
+                 "[lazy-layered prof] grid %u items %llu | us/item: layers %.1f rounds %.1f "
+                 "back/best/out %.1f reset %.1f | rounds/item %.1f\n",
+                 grid, sum[4], sum[0] / 100.0 / it, sum[1] / 100.0 / it, sum[2] / 100.0 / it,
+                 sum[3] / 100.0 / it, sum[5] / it);
+  }
+  return hipSuccess;
+}
+
 hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                        const BatchOutDev& out, hipStream_t stream, bool all,
                                        bool lazy) {
-  unsigned int* ctr = (unsigned int*)scratch(kCounter, 64);  // [8..15] are ours
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [8..15] are ours
   uint32_t* list = (uint32_t*)scratch(kBfsList, (size_t)in.num_strings * 4);
   uint32_t* list2 = (uint32_t*)scratch(kBfsList2, (size_t)in.num_strings * 4);
   if (!ctr || !list || !list2) return hipErrorOutOfMemory;
@@ -691,7 +783,7 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
 hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput& lhs,
                                          HostLattice* lat, LaunchStats* stats) {
   HIP_TRY(hipSetDevice(dev_));
-  unsigned int* ctr = (unsigned int*)scratch(kCounter, 64);
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!ctr) return hipErrorOutOfMemory;
   BatchOutDev none_out{};
   for (int tier = 1;; ++tier) {  // one lattice: start at 128K tuples
@@ -855,7 +947,7 @@ hipError_t DeviceEngine::project_output(const BatchOutDev& stage, uint32_t num,
                                         hipStream_t stream) {
   HIP_TRY(hipSetDevice(dev_));
   uint64_t* counts = (uint64_t*)scratch(kProjCount, ((size_t)num + 1) * 8 + 16);
-  uint32_t* ml = (uint32_t*)scratch(kCounter, 64) + 15;
+  uint32_t* ml = (uint32_t*)scratch(kCounter, kCounterBytes) + 15;
   if (!counts || !ml) return hipErrorOutOfMemory;
   HIP_TRY(hipMemsetAsync(ml, 0, 4, stream));
   project_count_kernel<<<(num + 256) / 256, 256, 0, stream>>>(stage, num, counts, proj_status,
@@ -879,7 +971,7 @@ hipError_t DeviceEngine::run_graph(const DeviceFst& rhs, const GraphInput& in, u
                                    LaunchStats* stats) {
   HIP_TRY(hipSetDevice(dev_));
   if (semantics != 0) return hipErrorInvalidValue;
-  unsigned int* counter = (unsigned int*)scratch(kCounter, 64);
+  unsigned int* counter = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!counter) return hipErrorOutOfMemory;
   HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
   HIP_TRY(hipMemsetAsync(out.cursor, 0, sizeof(unsigned long long), stream));

@@ -155,6 +155,10 @@ class DeviceEngine {
   hipError_t run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                            const BatchOutDev& out, hipStream_t stream, bool all,
                            bool lazy = false);
+  // composeShortestPath on layered lattices (kernels/lazy_layered.hpp); strings it does
+  // not take end UNSUPPORTED / OVERFLOW for run_bfs_chain.
+  hipError_t run_lazy_layered(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                              const BatchOutDev& out, hipStream_t stream);
   void* scratch(size_t idx, size_t bytes);
   int dev_;
   int num_cus_ = 0;
@@ -164,6 +168,8 @@ class DeviceEngine {
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
   size_t lazy_hash_bytes_ = 0;   // hash table stamps are valid for this allocation
   uint32_t lazy_stamp_ = 0;      // next stamp base (bumped per launch)
+  void* ll_clean_ = nullptr;     // lazy-layered dense arrays initialised for this allocation
+  size_t ll_clean_bytes_ = 0;
 };
 
 }  // namespace fstamd

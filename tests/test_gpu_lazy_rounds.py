@@ -1,9 +1,11 @@
-"""GPU parity of the parallel lazy engine (kernels/eager_bfs.hpp, bfs_lazy_path) and of the
-replay engine it replaces for finite weights >= 0 (kernels/lazy_wave.hpp), both against
-the oracle's sequential composeShortestPath (src/ops/compose-shortest-path.zig:26-401).
+"""GPU parity of the lazy engines against the oracle's sequential composeShortestPath
+(src/ops/compose-shortest-path.zig:26-401): the parallel rounds engines -- layered
+(kernels/lazy_layered.hpp) and general (kernels/eager_bfs.hpp, bfs_lazy_path) -- and the
+replay (kernels/lazy_wave.hpp).
 
-FSTAMD_LAZY_ENGINE=replay forces the replay; unset, the rounds engine takes every rhs
-with finite arc weights >= 0 (engine 3 in fst_last_launch_stats)."""
+FSTAMD_LAZY_ENGINE=replay | rounds forces one engine (FSTAMD_LAZY_LAYERED=0 keeps the
+rounds on the general engine); unset, the engine is chosen by the rhs and batch shape
+(fst_last_launch_stats().engine: 1 replay, 3 general rounds, 4 layered + general)."""
 import math
 
 import numpy as np
@@ -16,18 +18,23 @@ from test_gpu_parity import LAZY, check, csr, load_blob, random_rhs
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["rounds", "replay"])
+@pytest.fixture(params=["rounds", "general", "replay"])
 def engine(request, monkeypatch):
+    monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
+    monkeypatch.delenv("FSTAMD_LAZY_LAYERED", raising=False)
     if request.param == "replay":
         monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
-    else:
-        monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
-    return request.param
+        return "replay"
+    monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "rounds")
+    if request.param == "general":  # general rounds engine only (no layered engine)
+        monkeypatch.setenv("FSTAMD_LAZY_LAYERED", "0")
+    return "rounds"
 
 
 def expect_engine(engine):
     st = F.last_launch_stats()
-    assert st.engine == (3 if engine == "rounds" else 1)
+    # 3 = general rounds engine, 4 = layered engine first (rhs without input epsilons)
+    assert st.engine in ((3, 4) if engine == "rounds" else (1,))
 
 
 @pytest.mark.parametrize("seed", range(16))
@@ -93,7 +100,7 @@ def test_engines_agree_on_a_large_varied_batch(monkeypatch):
     rng = np.random.default_rng(77)
     seqs = [[int(x) for x in (rng.random(int(L)) < 0.02) + 1] for L in rng.integers(0, 65, 2048)]
     labels, offsets = csr(seqs)
-    monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
+    monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "rounds")
     a = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, LAZY)
     monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
     b = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, LAZY)
