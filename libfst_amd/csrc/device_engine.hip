@@ -16,6 +16,7 @@
 #include "kernels/lazy_layered.hpp"
 #include "kernels/eager_layered.hpp"
 #include "kernels/eager_wave.hpp"
+#include "kernels/eager_window.hpp"
 #include "kernels/lazy_wave.hpp"
 
 #define HIP_TRY(x)                              \
@@ -171,6 +172,14 @@ constexpr int kEwEmax = 5;
 constexpr int kEwFcap = 64 * kEwEmax;
 constexpr int kEwHcap = 512;
 constexpr int kEwKmax = 5;
+// eager-window geometry (tier A0): one wavefront per string, direct-mapped target window of
+// kEwinW = 64 * kEwinRows states, <= 64 * kEwinEmax tuples in a layer that is expanded,
+// <= kEwinKmax same-label arcs per tuple, kEwinWaves waves per SIMD.
+constexpr int kEwinEmax = 4;
+constexpr int kEwinRows = 5;
+constexpr int kEwinW = 64 * kEwinRows;
+constexpr int kEwinKmax = 5;
+constexpr int kEwinWaves = 3;
 
 // Item counters and list counts, one 256-B block shared by the engines (word ranges):
 // run_chain [0..4], lazy replay retry tiers [6..13], run_bfs_chain [8..11] (never in the
@@ -208,6 +217,8 @@ enum Scratch : size_t {
   kLlInv,
   kLlLoff,
   kLlAct,
+  kElBackW,
+  kItems3,
   kNumScratch
 };
 
@@ -364,24 +375,37 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     // Tier chain for layered lattices (each tier takes the strings the previous one
     // reports as OVERFLOW, through a device-side list):
-    //   A  one wavefront per string, LDS tables, <= kEwFcap tuples/layer, spans <= kEwKmax
+    //   A0 one wavefront per string, direct-mapped LDS window of kEwinW target states
+    //   A  one wavefront per string, LDS hash, <= kEwFcap tuples/layer, spans <= kEwKmax
     //   B  256 threads per string, LDS tables, <= kElFcap tuples/layer, spans <= kElKmax
     //   C  256 threads per string, HBM tables sized by the rhs (any layer)
-    // FSTAMD_EAGER_TIER1=wg starts at B (A/B comparisons).  A tier is skipped when the
-    // previous one provably cannot overflow on this rhs.
+    // FSTAMD_EAGER_TIER1=wave starts at A, =wg at B (A/B comparisons).  A tier is skipped
+    // when the previous one provably cannot overflow on this rhs.
     const char* t1 = std::getenv("FSTAMD_EAGER_TIER1");
-    const bool use_a = !(t1 && std::strcmp(t1, "wg") == 0);
+    const bool start_b = t1 && std::strcmp(t1, "wg") == 0;
+    const bool use_w = !start_b && !(t1 && std::strcmp(t1, "wave") == 0);
     const uint32_t ns = rhs.view.num_states, ms = rhs.view.max_span;
     auto back_cap_for = [&](uint32_t fcap, uint64_t limit, bool* capped) {
       const uint64_t want = (uint64_t)(in.max_len + 1) * fcap;
       *capped = want > limit;
       return (uint32_t)std::min<uint64_t>(want, limit);
     };
-    bool cap_a = false, cap_b = false;
+    bool cap_w = false, cap_a = false, cap_b = false;
+    const uint32_t back_cap_w = back_cap_for(kEwinW, 1u << 22, &cap_w);
     const uint32_t back_cap_a = back_cap_for(kEwFcap, 1u << 22, &cap_a);
     const uint32_t back_cap_b = back_cap_for(kElFcap, 1u << 22, &cap_b);
-    const bool need_b = !use_a || ns > (uint32_t)kEwFcap || ms > (uint32_t)kEwKmax || cap_a;
+    // A0 overflows on a window wider than kEwinW or an expanded layer of more than
+    // 64 * kEwinEmax tuples (both impossible with <= 64 * kEwinEmax states), on a span
+    // longer than kEwinKmax and on its back slab; only the first two are A's business.
+    const bool use_a = !start_b && (!use_w || ns > (uint32_t)(64 * kEwinEmax));
+    const bool need_b = !(use_w || use_a) || ns > (uint32_t)kEwFcap || ms > (uint32_t)kEwKmax ||
+                        (use_a && cap_a) || (use_w && (ms > (uint32_t)kEwinKmax || cap_w));
     const bool need_c = need_b && (ns > (uint32_t)kElFcap || ms > (uint32_t)kElKmax || cap_b);
+    auto k_win = eager_window_kernel<kEwinEmax, kEwinRows, kEwinKmax, kEwinWaves>;
+    if (const char* ww = std::getenv("FSTAMD_EWIN_WAVES")) {  // occupancy experiments
+      if (std::strcmp(ww, "2") == 0) k_win = eager_window_kernel<kEwinEmax, kEwinRows, kEwinKmax, 2>;
+      if (std::strcmp(ww, "4") == 0) k_win = eager_window_kernel<kEwinEmax, kEwinRows, kEwinKmax, 4>;
+    }
     auto k_wave = eager_wave_kernel<kEwFcap, kEwHcap, kEwEmax, kEwKmax>;
     auto k_wg = eager_layered_lds_kernel<kElWG, kElFcap, kElHcap, kElKmax>;
     auto grid_for = [&](const void* k, int block, uint32_t back_cap) -> uint32_t {
@@ -392,15 +416,23 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       while (g > 1 && (uint64_t)g * back_cap * sizeof(uint2) > (4ull << 30)) g /= 2;
       return std::max<uint32_t>(g, 1);
     };
+    const uint32_t grid_w = use_w ? grid_for((const void*)k_win, 64, back_cap_w) : 0;
     const uint32_t grid_a = use_a ? grid_for((const void*)k_wave, 64, back_cap_a) : 0;
     const uint32_t grid_b = need_b ? grid_for((const void*)k_wg, kElWG, back_cap_b) : 0;
+    uint2* back_w = use_w ? (uint2*)scratch(kElBackW, (size_t)grid_w * back_cap_w * 8) : nullptr;
     uint2* back_a = use_a ? (uint2*)scratch(kElBack, (size_t)grid_a * back_cap_a * 8) : nullptr;
     uint2* back_b = need_b ? (uint2*)scratch(kElBackB, (size_t)grid_b * back_cap_b * 8) : nullptr;
-    if ((use_a && !back_a) || (need_b && !back_b)) return hipErrorOutOfMemory;
-    uint32_t* list_ab = (use_a && need_b) ? (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4)
-                                          : nullptr;
+    if ((use_w && !back_w) || (use_a && !back_a) || (need_b && !back_b))
+      return hipErrorOutOfMemory;
+    uint32_t* list_wa = (use_w && use_a) ? (uint32_t*)scratch(kItems3, (size_t)in.num_strings * 4)
+                                         : nullptr;
+    uint32_t* list_ab = ((use_w || use_a) && need_b)
+                            ? (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4)
+                            : nullptr;
     uint32_t* list_bc = need_c ? (uint32_t*)scratch(kItems2, (size_t)in.num_strings * 4) : nullptr;
-    if ((use_a && need_b && !list_ab) || (need_c && !list_bc)) return hipErrorOutOfMemory;
+    if ((use_w && use_a && !list_wa) || ((use_w || use_a) && need_b && !list_ab) ||
+        (need_c && !list_bc))
+      return hipErrorOutOfMemory;
     uint32_t grid_c = 0, fcap_c = 0, hcap_c = 0, back_cap_c = 0;
     uint8_t* slab_c = nullptr;
     uint2* back_c = nullptr;
@@ -416,15 +448,34 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     if (stats) {
       stats->engine = 0;
-      stats->grid = use_a ? grid_a : grid_b;
-      stats->launches = (use_a ? 1 : 0) + (need_b ? (use_a ? 2 : 1) : 0) + (need_c ? 2 : 0);
+      stats->grid = use_w ? grid_w : use_a ? grid_a : grid_b;
+      stats->launches = (use_w ? 1 : 0) + (use_a ? (use_w ? 2 : 1) : 0) +
+                        (need_b ? ((use_w || use_a) ? 2 : 1) : 0) + (need_c ? 2 : 0);
       HIP_TRY(hipEventRecord(ev0_, stream));
     }
     const unsigned long long wd = watchdog_ticks();
     const uint32_t blocks = (in.num_strings + 255) / 256;
-    // counters: [0..2] item counters of tiers A, B, C; [3] |list_ab|; [4] |list_bc|
+    // counters: [5] item counter of tier A0, [6] |list_wa|; [0..2] item counters of tiers
+    // A, B, C; [3] |list_ab|; [4] |list_bc|
+    if (use_w) {
+      EagerLaunch lw{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_w, back_cap_w, wd};
+#ifdef FSTAMD_DEBUG_WAIT
+      HIP_TRY(debug_trace_arm());
+#endif
+      k_win<<<grid_w, 64, 0, stream>>>(rhs.view, in, n, counter + 5, lw, out);
+      HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_DEBUG_WAIT
+      HIP_TRY(debug_wait(stream, grid_w, "tierA0"));
+#endif
+    }
     if (use_a) {
       EagerLaunch la{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_a, back_cap_a, wd};
+      if (use_w) {
+        collect_status_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
+                                                          kPathOverflow, list_wa, counter + 6);
+        la.items = list_wa;
+        la.num_items_dev = counter + 6;
+      }
 #ifdef FSTAMD_DEBUG_WAIT
       HIP_TRY(debug_trace_arm());
 #endif
@@ -436,7 +487,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     if (need_b) {
       EagerLaunch lb{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_b, back_cap_b, wd};
-      if (use_a) {
+      if (use_w || use_a) {
         collect_status_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
                                                           kPathOverflow, list_ab, counter + 3);
         lb.items = list_ab;

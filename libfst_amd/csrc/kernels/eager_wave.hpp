@@ -125,6 +125,99 @@ __device__ __forceinline__ uint32_t wave_slot(uint32_t t) {
   return (t ^ (t >> kBits) ^ (t >> (2 * kBits))) & (HCAP - 1);
 }
 
+// Best final = lexmin (total, position) over the last layer (shortest-path.zig:88-104).
+// `best_w` / `bestp_w` are the wave's LDS reduction words.
+// One final candidate of a lane: tuple at position p with state s and distance d.  Keeps
+// the lane's lexmin (total, position); positions must arrive in ascending order.
+__device__ __forceinline__ void wave_final_candidate(const RhsView& rhs, uint32_t p, uint32_t s,
+                                                     double d, unsigned long long& mykey,
+                                                     uint32_t& myp, double& myfw) {
+  const double fw2 = rhs.final_w[FB(s, rhs.num_states, 33)];
+  if (!w_is_zero(d) && !w_is_zero(fw2)) {
+    const unsigned long long kk = okey(d + fw2);  // times(d, times(One, fw2))
+    if (kk < mykey) {
+      mykey = kk;
+      myp = p;
+      myfw = fw2;
+    }
+  }
+}
+
+// The lanes' final candidates -> the wave's best (lexmin (total, position)), then the
+// backtrace through the back slab (shortest-path.zig:109-136) by lane 0.
+__device__ __forceinline__ void wave_pick_and_backtrace(
+    const RhsView& rhs, const ChainInput& in, const BatchOutDev& out, const uint2* back,
+    uint32_t back_cap, unsigned long long& best_w, uint32_t& bestp_w, uint32_t si, uint64_t off,
+    uint32_t L, uint32_t lane, uint32_t cur_base, unsigned long long mykey, uint32_t myp,
+    double myfw, uint32_t tuples, uint32_t relax) {
+  if (lane == 0) {
+    best_w = kMaxU64;
+    bestp_w = kEmptyKey;
+  }
+  wave_lds_sync();
+  if (mykey != kMaxU64) atomicMin(&best_w, mykey);
+  wave_lds_sync();
+  const unsigned long long best = best_w;
+  if (best != kMaxU64 && mykey == best) atomicMin(&bestp_w, myp);
+  wave_lds_sync();
+  const uint32_t bp = bestp_w;
+  const bool hit = best != kMaxU64;
+  // final weight of the best tuple: its owner lane (bp % 64) has myp == bp; readlane
+  // moves 32 bits, so the f64 goes as two words
+  const uint32_t bl = bp & 63u;
+  const unsigned long long fwbits = (unsigned long long)__double_as_longlong(myfw);
+  const uint32_t fw_lo = __builtin_amdgcn_readlane((uint32_t)fwbits, bl);
+  const uint32_t fw_hi = __builtin_amdgcn_readlane((uint32_t)(fwbits >> 32), bl);
+  const double fw2 = __longlong_as_double((long long)(((unsigned long long)fw_hi << 32) | fw_lo));
+
+  if (lane == 0) {
+    if (!hit) {
+      write_status(out, si, kPathEmpty, tuples, relax);
+    } else {
+      const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
+      if (o + L > out.arc_cap) {
+        write_status(out, si, kPathOutputFull, tuples, relax);
+      } else {
+        uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
+        for (uint32_t k = L; k > 0; --k) {
+          const uint2 b = back[FB(id, back_cap, 34)];
+          const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
+          out.out_il[o + k - 1] = in.labels[off + k - 1];
+          out.out_ol[o + k - 1] = r.olabel;
+          out.out_w[o + k - 1] = r.weight;  // times(One, w) == w for w >= +0
+          id = b.x;
+        }
+        out.status[si] = kPathOk;
+        out.path_len[si] = L;
+        out.path_off[si] = o;
+        out.final_w[si] = fw2;  // compose.zig:73: times(One, fw2) == fw2
+        if (out.work) {
+          out.work[2 * si] = tuples;
+          out.work[2 * si + 1] = relax;
+        }
+      }
+    }
+  }
+}
+
+template <int EMAX>
+__device__ __forceinline__ void wave_best_and_backtrace(
+    const RhsView& rhs, const ChainInput& in, const BatchOutDev& out, const uint2* back,
+    uint32_t back_cap, unsigned long long& best_w, uint32_t& bestp_w, uint32_t si, uint64_t off,
+    uint32_t L, uint32_t lane, uint32_t n_cur, uint32_t cur_base, const uint32_t (&s2)[EMAX],
+    const double (&dd)[EMAX], uint32_t tuples, uint32_t relax) {
+  unsigned long long mykey = kMaxU64;
+  uint32_t myp = kEmptyKey;
+  double myfw = 0.0;
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) {  // e ascending = position ascending within the lane
+    const uint32_t p = e * 64 + lane;
+    if (p < n_cur) wave_final_candidate(rhs, p, s2[e], dd[e], mykey, myp, myfw);
+  }
+  wave_pick_and_backtrace(rhs, in, out, back, back_cap, best_w, bestp_w, si, off, L, lane,
+                          cur_base, mykey, myp, myfw, tuples, relax);
+}
+
 template <int FCAP, int HCAP, int EMAX, int KMAX>
 __global__ void __launch_bounds__(64, 3)
 eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
@@ -139,6 +232,8 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
   __shared__ WaveLds<FCAP, HCAP> S;
   const uint32_t lane = threadIdx.x;
   uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
+  const uint32_t num_items = __builtin_amdgcn_readfirstlane(
+      lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 
 #pragma unroll 1
@@ -160,9 +255,9 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
         (uint32_t)(__ffsll((long long)__ballot(1)) - 1))
       item = atomicAdd(next_item, 1u);
     item = __builtin_amdgcn_readlane(item, __ffsll((long long)__ballot(1)) - 1);
-    if (item >= lp.num_items) break;
+    if (item >= num_items) break;
     FT(item, 0xFFFFFFFFu, 0, 0);
-    const uint32_t si = item;
+    const uint32_t si = __builtin_amdgcn_readfirstlane(lp.items ? lp.items[item] : item);
     // every value that steers control flow is made provably wave-uniform (SGPR), so the
     // compiler emits scalar branches and no divergent-loop structure
     const uint64_t off0 = in.offsets[si];
@@ -394,74 +489,8 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     }
 
     FT(item, si, L, 7);
-    // ---- best final: lexmin (total, position) over the last layer (shortest-path.zig:88-104)
-    unsigned long long mykey = kMaxU64;
-    uint32_t myp = kEmptyKey;
-    double myfw = 0.0;
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-      const uint32_t p = e * 64 + lane;
-      if (p < n_cur) {
-        const double fw2 = rhs.final_w[FB(s2[e], rhs.num_states, 33)];
-        if (!w_is_zero(dd[e]) && !w_is_zero(fw2)) {
-          const unsigned long long kk = okey(dd[e] + fw2);  // times(d, times(One, fw2))
-          if (kk < mykey) {  // e ascending = p ascending within the lane
-            mykey = kk;
-            myp = p;
-            myfw = fw2;
-          }
-        }
-      }
-    }
-    if (lane == 0) {
-      S.best = kMaxU64;
-      S.bestp = kEmptyKey;
-    }
-    wave_lds_sync();
-    if (mykey != kMaxU64) atomicMin(&S.best, mykey);
-    wave_lds_sync();
-    const unsigned long long best = S.best;
-    if (best != kMaxU64 && mykey == best) atomicMin(&S.bestp, myp);
-    wave_lds_sync();
-    const uint32_t bp = S.bestp;
-    const bool hit = best != kMaxU64;
-    // final weight of the best tuple: its owner lane (bp % 64) has myp == bp; readlane
-    // moves 32 bits, so the f64 goes as two words
-    const uint32_t bl = bp & 63u;
-    const unsigned long long fwbits = (unsigned long long)__double_as_longlong(myfw);
-    const uint32_t fw_lo = __builtin_amdgcn_readlane((uint32_t)fwbits, bl);
-    const uint32_t fw_hi = __builtin_amdgcn_readlane((uint32_t)(fwbits >> 32), bl);
-    const double fw2 = __longlong_as_double((long long)(((unsigned long long)fw_hi << 32) | fw_lo));
-
-    if (lane == 0) {
-      if (!hit) {
-        write_status(out, si, kPathEmpty, tuples, relax);
-      } else {
-        const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
-        if (o + L > out.arc_cap) {
-          write_status(out, si, kPathOutputFull, tuples, relax);
-        } else {
-          FT(item, si, L, 8);
-          uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
-          for (uint32_t k = L; k > 0; --k) {
-            const uint2 b = back[FB(id, lp.back_cap, 34)];
-            const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
-            out.out_il[o + k - 1] = in.labels[off + k - 1];
-            out.out_ol[o + k - 1] = r.olabel;
-            out.out_w[o + k - 1] = r.weight;  // times(One, w) == w for w >= +0
-            id = b.x;
-          }
-          out.status[si] = kPathOk;
-          out.path_len[si] = L;
-          out.path_off[si] = o;
-          out.final_w[si] = fw2;  // compose.zig:73: times(One, fw2) == fw2
-          if (out.work) {
-            out.work[2 * si] = tuples;
-            out.work[2 * si + 1] = relax;
-          }
-        }
-      }
-    }
+    wave_best_and_backtrace<EMAX>(rhs, in, out, back, lp.back_cap, S.best, S.bestp, si, off, L,
+                                  lane, n_cur, cur_base, s2, dd, tuples, relax);
   }
 }
 

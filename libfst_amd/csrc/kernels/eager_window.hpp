@@ -1,0 +1,300 @@
+// eager_window.hpp -- eager compose + shortestPath on layered lattices, one wavefront per
+// string, with a DIRECT-MAPPED target window instead of a hash (gfx950 / CDNA4).  Tier A0
+// of the eager engine: it runs first and hands the strings it cannot hold to the hashed
+// wave tier (eager_wave.hpp) through a device-side list.
+//
+// Results: identical to eager_wave.hpp (same candidate enumeration, same first-occurrence
+// ids, same tight-candidate back-pointers, same best final), so the proof in
+// eager_layered.hpp / DESIGN.md §4.1 carries over unchanged.  What differs is the table:
+//
+//   * Per layer the wave reduces the min and max target state of its candidates.  If they
+//     span fewer than W = 64 * EW states, target t lives in slot t - tmin: no keys, no
+//     compare-and-swap, no probing, and the next layer's state is tmin + slot.  (A layer of
+//     a banded transducer -- the reference bench's ambiguous chain, a tagger's left-to-right
+//     states -- always fits: the metric's widest layer spans 257 states.)  A wider layer
+//     reports OVERFLOW and the string moves on to the hashed tier.
+//   * Candidates that do not exist (j >= span count) aim their LDS atomics at a per-lane
+//     trash slot W + lane instead of branching, so the phase loops carry no exec-mask
+//     branches at all.
+//   * At most W distinct targets fit a window, so a layer never holds more than W tuples.
+//     Only layers that are expanded again live in registers (<= 64 * EMAX tuples); the
+//     last layer (the metric's 257 tuples) is reduced to its best final straight from the
+//     LDS table, so EMAX = 4 rows suffice for the metric and the wave fits 128 VGPRs.
+//
+// The LDS image is 8.3 KB per wave (12.9 KB for the hashed tier), so LDS no longer caps
+// the wave count: registers do (__launch_bounds__ below).
+#pragma once
+
+#include "device_common.hpp"
+#include "eager_layered.hpp"  // EagerLaunch, write_status
+#include "eager_wave.hpp"     // wave_lds_sync, wave_excl_scan_small, wave_load_layer,
+                              // wave_final_candidate, wave_pick_and_backtrace
+
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
+
+namespace fstamd {
+
+template <int W>
+struct WindowLds {
+  uint32_t first[W + 64];            // first (smallest) candidate index reaching the slot
+  unsigned long long dmin[W + 64];   // okey of the minimum candidate distance
+  unsigned long long bpack[W + 64];  // (index << 48) | (source position << 32) | rhs arc of
+                                     // the tight candidate with the smallest index
+  uint16_t nslot[W];                 // next-layer rank -> slot
+  unsigned long long best;           // best-final reduction words
+  uint32_t bestp;
+};
+
+// EMAX: register rows of a layer that is expanded (<= 64 * EMAX tuples); EW: rows of the
+// window (W = 64 * EW target states, so <= W tuples in the last layer, which is never
+// expanded: its best final is taken straight from the LDS table).
+template <int EMAX, int EW, int KMAX, int WAVES_PER_EU>
+__global__ void __launch_bounds__(64, WAVES_PER_EU)
+eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
+                    EagerLaunch lp, BatchOutDev out) {
+  constexpr int W = 64 * EW;
+  static_assert(EW >= EMAX, "the window holds every expandable layer");
+  static_assert(EMAX * KMAX <= 64, "creator mask is 64 bits");
+  static_assert(KMAX <= kRecPad, "arc mirror padding covers KMAX records");
+  constexpr unsigned long long kFree = ~0ull;
+  constexpr int kRowBits = 32 - __builtin_clz((unsigned)KMAX);
+  __shared__ WindowLds<W> S;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t trash = W + lane;  // where non-existent candidates aim their atomics
+  uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
+  const uint32_t num_items = __builtin_amdgcn_readfirstlane(
+      lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+#pragma unroll 1
+  for (uint32_t i = lane; i < (uint32_t)W + 64; i += 64) {
+    S.first[i] = kEmptyKey;
+    S.dmin[i] = kFree;
+    S.bpack[i] = kFree;
+  }
+  wave_lds_sync();
+
+  for (;;) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * lp.wd_ticks) return;
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(next_item, 1u);
+    item = __builtin_amdgcn_readfirstlane(item);
+    if (item >= num_items) break;
+    const uint32_t si = __builtin_amdgcn_readfirstlane(lp.items ? lp.items[item] : item);
+    const uint64_t off0 = in.offsets[si];
+    const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
+                         __builtin_amdgcn_readfirstlane((uint32_t)off0);
+    const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)(in.offsets[si + 1] - off));
+
+    if (rhs.start == kNoState || n_best != 1) {  // compose.zig:33-35, shortest-path.zig:21-24
+      if (lane == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+      if (lane == 0) write_status(out, si, kPathInternal, 0, 0);
+      continue;
+    }
+
+    uint32_t n_cur = 1, cur_base = 0;
+    uint32_t tuples = 1, relax = 0;
+    uint32_t s2[EMAX];
+    double dd[EMAX];
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      s2[e] = rhs.start;
+      dd[e] = w_one();
+    }
+    int32_t fail = kPathOk;
+    unsigned long long mykey = kMaxU64;  // this lane's best final candidate
+    uint32_t myp = kEmptyKey;
+    double myfw = 0.0;
+
+    // the string's labels, 64 at a time, one per lane (no load on the layer's chain)
+    uint32_t labs = 0;
+    for (uint32_t k = 0; k < L; ++k) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+        fail = kPathInternal;
+        break;
+      }
+      if ((k & 63u) == 0) labs = k + lane < L ? in.labels[off + k + lane] : 0u;
+      const uint32_t lab = __builtin_amdgcn_readlane(labs, k & 63u);
+      if (lab == kEpsilon) {  // lhs epsilon output: not a layered lattice
+        fail = kPathUnsupported;
+        break;
+      }
+      uint32_t lo[EMAX], cnt[EMAX];
+      uint32_t ct[EMAX][KMAX];
+      double cw[EMAX][KMAX];
+      if (__ballot(wave_load_layer<EMAX, KMAX>(rhs, lab, lane, n_cur, s2, lo, cnt, ct, cw))) {
+        fail = kPathOverflow;
+        break;
+      }
+      const uint32_t rows = (n_cur + 63) / 64;
+      uint32_t cbase[EMAX];
+      uint32_t rbase = 0;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        uint32_t tot = 0;
+        cbase[e] = rbase;
+        if ((uint32_t)e < rows) {
+          cbase[e] += wave_excl_scan_small<kRowBits>(cnt[e], tot);
+          rbase += tot;
+        }
+      }
+      relax += rbase;
+      if (rbase == 0) {  // no candidate: the lattice dies here, no final is reachable
+        n_cur = 0;
+        break;
+      }
+
+      // ---- window of this layer's targets ----
+      uint32_t mn = kEmptyKey, mx = 0;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if ((uint32_t)e >= rows) continue;  // uniform
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          const bool v = (uint32_t)j < cnt[e];
+          mn = v ? min(mn, ct[e][j]) : mn;
+          mx = v ? max(mx, ct[e][j]) : mx;
+        }
+      }
+      const uint32_t tmin = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(mn));
+      const uint32_t tmax = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(mx));
+      if (tmax - tmin >= (uint32_t)W) {
+        fail = kPathOverflow;  // the hashed tier takes the string
+        break;
+      }
+
+      // ---- (B) first occurrence and minimum distance per slot ----
+      // Tier A0 only sees rhs weights >= +0 (no -0, NaN, -inf): there
+      // times(d, times(One, w)) (compose.zig:104, shortest-path.zig:72) is exactly d + w.
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if ((uint32_t)e >= rows) continue;  // uniform
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          const uint32_t slot = (uint32_t)j < cnt[e] ? ct[e][j] - tmin : trash;
+          ct[e][j] = slot;
+          cw[e][j] = dd[e] + cw[e][j];
+          atomicMin(&S.first[slot], cbase[e] + j);
+          atomicMin(&S.dmin[slot], (unsigned long long)okey(cw[e][j]));
+        }
+      }
+      wave_lds_sync();
+
+      // ---- (C) tight candidates -> packed back-pointer; creators ----
+      unsigned long long creators = 0;
+      uint32_t nf[EMAX];
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        nf[e] = 0;
+        if ((uint32_t)e >= rows) continue;  // uniform
+        unsigned long long dm[KMAX];
+        uint32_t fi[KMAX];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          dm[j] = S.dmin[ct[e][j]];
+          fi[j] = S.first[ct[e][j]];
+        }
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+          const bool v = (uint32_t)j < cnt[e];
+          const uint32_t ci = cbase[e] + j;
+          const bool tight = v && okey(cw[e][j]) == dm[j];
+          atomicMin(&S.bpack[tight ? ct[e][j] : trash],
+                    ((unsigned long long)ci << 48) |
+                        ((unsigned long long)(e * 64 + lane) << 32) | (lo[e] + j));
+          const bool cr = v && fi[j] == ci;
+          creators |= (unsigned long long)cr << (e * KMAX + j);
+          nf[e] += cr ? 1u : 0u;
+        }
+      }
+      // ---- (D) ranks of the created tuples (candidate order = row, lane, j) ----
+      uint32_t n_next = 0;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if ((uint32_t)e < rows) {
+          uint32_t tot;
+          uint32_t rank = n_next + wave_excl_scan_small<kRowBits>(nf[e], tot);
+          n_next += tot;
+#pragma unroll
+          for (int j = 0; j < KMAX; ++j)
+            if (creators & (1ull << (e * KMAX + j))) S.nslot[rank++] = (uint16_t)ct[e][j];
+        }
+      }
+      const bool last = k + 1 == L;
+      if ((!last && n_next > (uint32_t)(64 * EMAX)) ||
+          (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
+        fail = kPathOverflow;
+        break;
+      }
+      wave_lds_sync();
+
+      // ---- (E) next layer: back records, slot reset (rank e * 64 + lane); the rows of
+      // the next layer, or on the last layer its final candidates ----
+      const uint32_t next_base = cur_base + n_cur;
+      const uint32_t rows_n = (n_next + 63) / 64;
+      uint32_t es[EW];
+      unsigned long long edm[EW], ebp[EW];
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        const uint32_t r = e * 64 + lane;
+        es[e] = (uint32_t)e < rows_n && r < n_next ? (uint32_t)S.nslot[r] : trash;
+      }
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        if ((uint32_t)e < rows_n) {
+          edm[e] = S.dmin[es[e]];
+          ebp[e] = S.bpack[es[e]];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        const uint32_t r = e * 64 + lane;
+        if ((uint32_t)e < rows_n) {
+          if (r < n_next)
+            back[FB(next_base + r, lp.back_cap, 40)] =
+                make_uint2(cur_base + (uint32_t)((ebp[e] >> 32) & 0xFFFFu), (uint32_t)ebp[e]);
+          S.first[es[e]] = kEmptyKey;
+          S.dmin[es[e]] = kFree;
+          S.bpack[es[e]] = kFree;
+          if (last) {
+            if (r < n_next)  // e ascending = position ascending within the lane
+              wave_final_candidate(rhs, r, tmin + es[e], from_okey(edm[e]), mykey, myp, myfw);
+          } else if (e < EMAX) {
+            s2[e] = tmin + es[e];
+            dd[e] = from_okey(edm[e]);
+          }
+        }
+      }
+      cur_base = next_base;
+      n_cur = n_next;
+      tuples += n_next;
+      wave_lds_sync();
+    }
+
+    if (fail != kPathOk) {
+      // leave the table clean for the next string
+      wave_lds_sync();
+#pragma unroll 1
+      for (uint32_t i = lane; i < (uint32_t)W + 64; i += 64) {
+        S.first[i] = kEmptyKey;
+        S.dmin[i] = kFree;
+        S.bpack[i] = kFree;
+      }
+      wave_lds_sync();
+      if (lane == 0) write_status(out, si, fail, tuples, relax);
+      continue;
+    }
+    if (L == 0 && lane == 0)  // the start tuple is the whole lattice
+      wave_final_candidate(rhs, 0, rhs.start, w_one(), mykey, myp, myfw);
+    wave_pick_and_backtrace(rhs, in, out, back, lp.back_cap, S.best, S.bestp, si, off, L, lane,
+                            cur_base, mykey, myp, myfw, tuples, relax);
+  }
+}
+
+}  // namespace fstamd

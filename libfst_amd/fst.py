@@ -121,6 +121,15 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it first (python -c 'import __graft_entry__ as g; "
                 "g.build()'); libfst_amd has no CPU fallback")
+        # One HIP runtime per process: torch ships its own libamdhip64 (same soname
+        # libamdhip64.so.7, but torch links it by the bare name), so if this library
+        # loaded /opt/rocm's copy first, a later `import torch` would bring a second
+        # runtime and one of the two would see no device.  Loading torch first makes
+        # our DT_NEEDED resolve to the copy torch already holds.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
