@@ -41,7 +41,7 @@ struct WindowLds {
   unsigned long long dmin[W + 64];   // okey of the minimum candidate distance
   unsigned long long bpack[W + 64];  // (index << 48) | (source position << 32) | rhs arc of
                                      // the tight candidate with the smallest index
-  uint16_t nslot[W];                 // next-layer rank -> slot
+  uint16_t nslot[W + 64];            // next-layer rank -> slot (+ trash slots)
   unsigned long long best;           // best-final reduction words
   uint32_t bestp;
 };
@@ -222,8 +222,11 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
           uint32_t rank = n_next + wave_excl_scan_small<kRowBits>(nf[e], tot);
           n_next += tot;
 #pragma unroll
-          for (int j = 0; j < KMAX; ++j)
-            if (creators & (1ull << (e * KMAX + j))) S.nslot[rank++] = (uint16_t)ct[e][j];
+          for (int j = 0; j < KMAX; ++j) {  // branch-free: non-creators write a trash slot
+            const uint32_t cr = (uint32_t)(creators >> (e * KMAX + j)) & 1u;
+            S.nslot[cr ? rank : trash] = (uint16_t)ct[e][j];
+            rank += cr;
+          }
         }
       }
       const bool last = k + 1 == L;
