@@ -416,10 +416,22 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       while (g > 1 && (uint64_t)g * back_cap * sizeof(uint2) > (4ull << 30)) g /= 2;
       return std::max<uint32_t>(g, 1);
     };
-    const uint32_t grid_w = use_w ? grid_for((const void*)k_win, 64, back_cap_w) : 0;
+    // A0 keeps kChaseBatch back slabs per wave (backtraces are walked in batches)
+    uint32_t grid_w = 0;
+    if (use_w) {
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_win, 64, 0) !=
+          hipSuccess)
+        occ = 1;
+      grid_w = (uint32_t)std::min<uint64_t>((uint64_t)std::max(occ, 1) * num_cus_, in.num_strings);
+      while (grid_w > 1 && (uint64_t)grid_w * kChaseBatch * back_cap_w * 8 > (24ull << 30))
+        grid_w /= 2;
+      grid_w = std::max<uint32_t>(grid_w, 1);
+    }
     const uint32_t grid_a = use_a ? grid_for((const void*)k_wave, 64, back_cap_a) : 0;
     const uint32_t grid_b = need_b ? grid_for((const void*)k_wg, kElWG, back_cap_b) : 0;
-    uint2* back_w = use_w ? (uint2*)scratch(kElBackW, (size_t)grid_w * back_cap_w * 8) : nullptr;
+    uint2* back_w =
+        use_w ? (uint2*)scratch(kElBackW, (size_t)grid_w * kChaseBatch * back_cap_w * 8) : nullptr;
     uint2* back_a = use_a ? (uint2*)scratch(kElBack, (size_t)grid_a * back_cap_a * 8) : nullptr;
     uint2* back_b = need_b ? (uint2*)scratch(kElBackB, (size_t)grid_b * back_cap_b * 8) : nullptr;
     if ((use_w && !back_w) || (use_a && !back_a) || (need_b && !back_b))

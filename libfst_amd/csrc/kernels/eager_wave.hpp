@@ -143,13 +143,13 @@ __device__ __forceinline__ void wave_final_candidate(const RhsView& rhs, uint32_
   }
 }
 
-// The lanes' final candidates -> the wave's best (lexmin (total, position)), then the
-// backtrace through the back slab (shortest-path.zig:109-136) by lane 0.
-__device__ __forceinline__ void wave_pick_and_backtrace(
-    const RhsView& rhs, const ChainInput& in, const BatchOutDev& out, const uint2* back,
-    uint32_t back_cap, unsigned long long& best_w, uint32_t& bestp_w, uint32_t si, uint64_t off,
-    uint32_t L, uint32_t lane, uint32_t cur_base, unsigned long long mykey, uint32_t myp,
-    double myfw, uint32_t tuples, uint32_t relax) {
+// The lanes' final candidates -> the wave's best (lexmin (total, position)).  Returns
+// whether there is one; `bp` = its position in the last layer, `fw2` = its rhs final weight
+// (uniform).
+__device__ __forceinline__ bool wave_pick_best(unsigned long long& best_w, uint32_t& bestp_w,
+                                               uint32_t lane, unsigned long long mykey,
+                                               uint32_t myp, double myfw, uint32_t& bp,
+                                               double& fw2) {
   if (lane == 0) {
     best_w = kMaxU64;
     bestp_w = kEmptyKey;
@@ -160,15 +160,27 @@ __device__ __forceinline__ void wave_pick_and_backtrace(
   const unsigned long long best = best_w;
   if (best != kMaxU64 && mykey == best) atomicMin(&bestp_w, myp);
   wave_lds_sync();
-  const uint32_t bp = bestp_w;
-  const bool hit = best != kMaxU64;
+  bp = __builtin_amdgcn_readfirstlane(bestp_w);
   // final weight of the best tuple: its owner lane (bp % 64) has myp == bp; readlane
   // moves 32 bits, so the f64 goes as two words
   const uint32_t bl = bp & 63u;
   const unsigned long long fwbits = (unsigned long long)__double_as_longlong(myfw);
   const uint32_t fw_lo = __builtin_amdgcn_readlane((uint32_t)fwbits, bl);
   const uint32_t fw_hi = __builtin_amdgcn_readlane((uint32_t)(fwbits >> 32), bl);
-  const double fw2 = __longlong_as_double((long long)(((unsigned long long)fw_hi << 32) | fw_lo));
+  fw2 = __longlong_as_double((long long)(((unsigned long long)fw_hi << 32) | fw_lo));
+  return best != kMaxU64;
+}
+
+// The lanes' final candidates -> the wave's best (lexmin (total, position)), then the
+// backtrace through the back slab (shortest-path.zig:109-136) by lane 0.
+__device__ __forceinline__ void wave_pick_and_backtrace(
+    const RhsView& rhs, const ChainInput& in, const BatchOutDev& out, const uint2* back,
+    uint32_t back_cap, unsigned long long& best_w, uint32_t& bestp_w, uint32_t si, uint64_t off,
+    uint32_t L, uint32_t lane, uint32_t cur_base, unsigned long long mykey, uint32_t myp,
+    double myfw, uint32_t tuples, uint32_t relax) {
+  uint32_t bp;
+  double fw2;
+  const bool hit = wave_pick_best(best_w, bestp_w, lane, mykey, myp, myfw, bp, fw2);
 
   if (lane == 0) {
     if (!hit) {
@@ -179,6 +191,7 @@ __device__ __forceinline__ void wave_pick_and_backtrace(
         write_status(out, si, kPathOutputFull, tuples, relax);
       } else {
         uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
+#ifndef FSTAMD_EXP_NO_BACKTRACE
         for (uint32_t k = L; k > 0; --k) {
           const uint2 b = back[FB(id, back_cap, 34)];
           const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
@@ -187,6 +200,13 @@ __device__ __forceinline__ void wave_pick_and_backtrace(
           out.out_w[o + k - 1] = r.weight;  // times(One, w) == w for w >= +0
           id = b.x;
         }
+#else  // timing experiment only: the cost of the dependent backtrace chain
+        for (uint32_t k = L; k > 0; --k) {
+          out.out_il[o + k - 1] = 1;
+          out.out_ol[o + k - 1] = 1;
+          out.out_w[o + k - 1] = 0.0;
+        }
+#endif
         out.status[si] = kPathOk;
         out.path_len[si] = L;
         out.path_off[si] = o;

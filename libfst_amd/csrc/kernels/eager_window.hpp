@@ -35,6 +35,18 @@ extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
 
 namespace fstamd {
 
+// Backtraces are walked in batches: a wave finishes kChaseBatch strings (each into its own
+// back slab), then lane r walks the path of string r -- the 1-dependent-load-per-arc chase
+// (shortest-path.zig:109-136) is paid once per batch instead of once per string.
+constexpr int kChaseBatch = 16;
+
+// A finished string whose backtrace is pending (see the batched chase in the kernel).
+struct ChaseJob {
+  uint32_t si, L, id, tuples, relax, pad;
+  unsigned long long o, off;
+  double fw;
+};
+
 template <int W>
 struct WindowLds {
   uint32_t first[W + 64];            // first (smallest) candidate index reaching the slot
@@ -42,8 +54,11 @@ struct WindowLds {
   unsigned long long bpack[W + 64];  // (index << 48) | (source position << 32) | rhs arc of
                                      // the tight candidate with the smallest index
   uint16_t nslot[W + 64];            // next-layer rank -> slot (+ trash slots)
+  double dcur[W];                    // distance of each position of the current layer
+                                     // (LDS, not registers: it lives across the loads)
   unsigned long long best;           // best-final reduction words
   uint32_t bestp;
+  ChaseJob job[kChaseBatch];         // strings whose backtrace is pending, one slab each
 };
 
 // EMAX: register rows of a layer that is expanded (<= 64 * EMAX tuples); EW: rows of the
@@ -62,7 +77,44 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
   __shared__ WindowLds<W> S;
   const uint32_t lane = threadIdx.x;
   const uint32_t trash = W + lane;  // where non-existent candidates aim their atomics
-  uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
+  uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
+  uint32_t njobs = 0;  // uniform: pending backtraces (slab j belongs to job j)
+  // lane r < njobs walks job r's path: outputs, status, final weight, work counters
+  auto chase_batch = [&]() {
+    wave_lds_sync();
+    uint32_t maxL = 0;
+    ChaseJob jb{};
+    if (lane < njobs) {
+      jb = S.job[lane];
+      maxL = jb.L;
+    }
+    maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
+    const uint2* sl = slabs + (size_t)lane * lp.back_cap;
+    uint32_t id = jb.id;
+    for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
+      if (lane < njobs && t < jb.L) {
+        const uint32_t k = jb.L - 1 - t;
+        const uint2 b = sl[FB(id, lp.back_cap, 34)];
+        const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
+        out.out_il[jb.o + k] = in.labels[jb.off + k];
+        out.out_ol[jb.o + k] = r.olabel;
+        out.out_w[jb.o + k] = r.weight;  // times(One, w) == w for w >= +0
+        id = b.x;
+      }
+    }
+    if (lane < njobs) {
+      out.status[jb.si] = kPathOk;
+      out.path_len[jb.si] = jb.L;
+      out.path_off[jb.si] = jb.o;
+      out.final_w[jb.si] = jb.fw;  // compose.zig:73: times(One, fw2) == fw2
+      if (out.work) {
+        out.work[2 * jb.si] = jb.tuples;
+        out.work[2 * jb.si + 1] = jb.relax;
+      }
+    }
+    njobs = 0;
+    wave_lds_sync();
+  };
   const uint32_t num_items = __builtin_amdgcn_readfirstlane(
       lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -82,6 +134,7 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
     item = __builtin_amdgcn_readfirstlane(item);
     if (item >= num_items) break;
     const uint32_t si = __builtin_amdgcn_readfirstlane(lp.items ? lp.items[item] : item);
+    uint2* const back = slabs + (size_t)njobs * lp.back_cap;
     const uint64_t off0 = in.offsets[si];
     const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
                          __builtin_amdgcn_readfirstlane((uint32_t)off0);
@@ -101,12 +154,9 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
     uint32_t n_cur = 1, cur_base = 0;
     uint32_t tuples = 1, relax = 0;
     uint32_t s2[EMAX];
-    double dd[EMAX];
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-      s2[e] = rhs.start;
-      dd[e] = w_one();
-    }
+    for (int e = 0; e < EMAX; ++e) s2[e] = rhs.start;
+    if (lane == 0) S.dcur[0] = w_one();  // the start tuple
     int32_t fail = kPathOk;
     unsigned long long mykey = kMaxU64;  // this lane's best final candidate
     uint32_t myp = kEmptyKey;
@@ -175,11 +225,12 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
         if ((uint32_t)e >= rows) continue;  // uniform
+        const double de = S.dcur[e * 64 + lane];
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           const uint32_t slot = (uint32_t)j < cnt[e] ? ct[e][j] - tmin : trash;
           ct[e][j] = slot;
-          cw[e][j] = dd[e] + cw[e][j];
+          cw[e][j] = de + cw[e][j];
           atomicMin(&S.first[slot], cbase[e] + j);
           atomicMin(&S.dmin[slot], (unsigned long long)okey(cw[e][j]));
         }
@@ -270,7 +321,7 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
               wave_final_candidate(rhs, r, tmin + es[e], from_okey(edm[e]), mykey, myp, myfw);
           } else if (e < EMAX) {
             s2[e] = tmin + es[e];
-            dd[e] = from_okey(edm[e]);
+            S.dcur[e * 64 + lane] = from_okey(edm[e]);
           }
         }
       }
@@ -295,9 +346,34 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
     }
     if (L == 0 && lane == 0)  // the start tuple is the whole lattice
       wave_final_candidate(rhs, 0, rhs.start, w_one(), mykey, myp, myfw);
-    wave_pick_and_backtrace(rhs, in, out, back, lp.back_cap, S.best, S.bestp, si, off, L, lane,
-                            cur_base, mykey, myp, myfw, tuples, relax);
+    uint32_t bp;
+    double fw2;
+    if (!wave_pick_best(S.best, S.bestp, lane, mykey, myp, myfw, bp, fw2)) {
+      if (lane == 0) write_status(out, si, kPathEmpty, tuples, relax);
+      continue;
+    }
+    unsigned long long o = 0;
+    if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
+    o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((uint32_t)o);
+    if (o + L > out.arc_cap) {
+      if (lane == 0) write_status(out, si, kPathOutputFull, tuples, relax);
+      continue;
+    }
+    if (lane == 0) {
+      ChaseJob& j = S.job[njobs];
+      j.si = si;
+      j.L = L;
+      j.id = cur_base + bp;  // shortest-path.zig:109-136 starts at the best final
+      j.tuples = tuples;
+      j.relax = relax;
+      j.o = o;
+      j.off = off;
+      j.fw = fw2;
+    }
+    if (++njobs == (uint32_t)kChaseBatch) chase_batch();
   }
+  if (njobs) chase_batch();
 }
 
 }  // namespace fstamd

@@ -1,0 +1,73 @@
+"""Config 3 (compose_frozen_lazy_shortest_path_epsilon_dense) toward its full size.
+
+BASELINE.json config 3 is 1M strings of length 11..251 (fixed seed) against the eps-dense
+transducer with T = 65,536 states, lazy semantics.  One such string is a lattice of about
+17M tuples and 220M relaxations, so the full batch is ~2e14 relaxations:
+this script measures a few strings of the real length distribution at growing T (one
+pass each, GPU and the single-thread oracle restatement side by side) and prints one JSON
+line per T, so the full-size rate can be read off and extrapolated.
+
+usage: python scripts/config3_scaling.py [--ts 4096,16384,65536] [--n 4] [--cpu-max-t 16384]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import bench  # noqa: E402
+import libfst_amd as F  # noqa: E402
+from libfst_amd import dist as D  # noqa: E402
+import oracle_ffi as O  # noqa: E402  (CPU baseline / checker only)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ts", default="4096,16384,65536")
+    ap.add_argument("--n", type=int, default=4)
+    ap.add_argument("--cpu-max-t", type=int, default=16384)
+    a = ap.parse_args()
+    rng = np.random.default_rng(0x5EED)
+    lens = rng.integers(11, 252, a.n)
+    for T in [int(x) for x in a.ts.split(",")]:
+        fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, 12)
+        blob = D.blob_bytes(fz)
+        rhs = D.adopt_on_device(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to("cuda:0"), 0)
+        b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = b.run(rhs, F.FST_SEM_LAZY, 0, stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        status = b.status.cpu().numpy()
+        work = b.work.cpu().numpy().astype(np.int64)
+        line = {"config": 3, "T": T, "strings": a.n, "lengths": [int(x) for x in lens],
+                "gpu_s": wall, "kernel_ms": st.kernel_ms, "gpu_strings_per_s": a.n / wall,
+                "status": [int(x) for x in status],
+                "tuples_per_string": float(work[0::2].mean()),
+                "relax_per_string": float(work[1::2].mean())}
+        if T <= a.cpu_max_t:
+            L0 = int(lens[0])
+            labels = np.ones(L0, np.uint32)
+            offs = np.array([0, L0], np.uint64)
+            secs, _ = O.batch_time(blob, labels, offs, 0, 1)
+            ref = O.batch_run(blob, labels, offs, 0)
+            got_ok = status[0] == F.FST_PATH_OK
+            line["cpu_s_first_string"] = secs
+            line["cpu_kind"] = "port (oracle/fst_oracle.c -O3), 1 thread, first string"
+            line["parity_first_string"] = bool(got_ok and ref.empty[0] == 0 and int(
+                b.plen[0].item()) == int(ref.offsets[1] - ref.offsets[0]))
+        print(json.dumps(line), flush=True)
+        del b, rhs
+
+
+if __name__ == "__main__":
+    main()
