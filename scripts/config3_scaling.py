@@ -65,6 +65,8 @@ def main():
             line["cpu_kind"] = "port (oracle/fst_oracle.c -O3), 1 thread, first string"
             line["parity_first_string"] = bool(got_ok and ref.empty[0] == 0 and int(
                 b.plen[0].item()) == int(ref.offsets[1] - ref.offsets[0]))
+        line["lengths"] = f"{len(lens)} strings, L uniform 11..251 (seed 0x5EED), first {list(map(int, lens[:4]))}"
+        line["status"] = {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))}
         print(json.dumps(line), flush=True)
         del b, rhs
 
