@@ -243,7 +243,7 @@ def main():
     if rank == 0:
         traffic, traffic_src = measured_traffic(args, sem)
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(args, blob_host, 1 if sem == F.FST_SEM_EAGER else 0)
         line = {
             "metric": "strings/sec, compose_frozen_shortest_path_ambiguous len=64 batch=1M",
