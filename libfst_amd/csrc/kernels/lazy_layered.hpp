@@ -137,9 +137,16 @@ __device__ __forceinline__ void global_sync() {  // this wave's global stores ->
 // dependent round trip per kind of word, not one per arc.  rec[lo + c] is in bounds for
 // c < cnt + kRecPad (padded mirror), so chunk loads are unconditional and masked.
 constexpr int kLlKB = 8;
+
+// Waves per SIMD the layered rounds engine is compiled for (5 and 6 measured the same as
+// 4 on the metric: the rounds are bound by the memory system's scattered transactions,
+// not by resident waves).
+#ifndef FSTAMD_LL_WAVES
+#define FSTAMD_LL_WAVES 4
+#endif
 static_assert(kLlKB <= (int)kRecPad, "chunk loads rely on the mirror padding");
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, FSTAMD_LL_WAVES)
 lazy_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
                     LlWs ws, BatchOutDev out) {
   __shared__ LlLds S;
