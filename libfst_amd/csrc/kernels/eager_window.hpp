@@ -246,6 +246,10 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
         if ((uint32_t)e >= rows) continue;  // uniform
         unsigned long long dm[KMAX];
         uint32_t fi[KMAX];
+        // opaque copy: stops the compiler from keeping phase B's cbase + j values alive
+        // across the sync (16 VGPRs at the register peak); recomputing costs 1 VALU each
+        uint32_t cb = cbase[e], lc = lo[e];
+        asm volatile("" : "+v"(cb), "+v"(lc));
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           dm[j] = S.dmin[ct[e][j]];
@@ -254,11 +258,11 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           const bool v = (uint32_t)j < cnt[e];
-          const uint32_t ci = cbase[e] + j;
+          const uint32_t ci = cb + j;
           const bool tight = v && okey(cw[e][j]) == dm[j];
           atomicMin(&S.bpack[tight ? ct[e][j] : trash],
                     ((unsigned long long)ci << 48) |
-                        ((unsigned long long)(e * 64 + lane) << 32) | (lo[e] + j));
+                        ((unsigned long long)(e * 64 + lane) << 32) | (lc + j));
           const bool cr = v && fi[j] == ci;
           creators |= (unsigned long long)cr << (e * KMAX + j);
           nf[e] += cr ? 1u : 0u;
