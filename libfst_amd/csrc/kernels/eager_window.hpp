@@ -250,6 +250,7 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
         // across the sync (16 VGPRs at the register peak); recomputing costs 1 VALU each
         uint32_t cb = cbase[e], lc = lo[e];
         asm volatile("" : "+v"(cb), "+v"(lc));
+        const uint32_t phi = (cb << 16) | (uint32_t)(e * 64 + lane);
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           dm[j] = S.dmin[ct[e][j]];
@@ -260,9 +261,10 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
           const bool v = (uint32_t)j < cnt[e];
           const uint32_t ci = cb + j;
           const bool tight = v && okey(cw[e][j]) == dm[j];
+          // (index << 48) | (position << 32) | rhs arc, from a per-row high word
+          const uint32_t hi = phi + ((uint32_t)j << 16);
           atomicMin(&S.bpack[tight ? ct[e][j] : trash],
-                    ((unsigned long long)ci << 48) |
-                        ((unsigned long long)(e * 64 + lane) << 32) | (lc + j));
+                    ((unsigned long long)hi << 32) | (lc + j));
           const bool cr = v && fi[j] == ci;
           creators |= (unsigned long long)cr << (e * KMAX + j);
           nf[e] += cr ? 1u : 0u;
