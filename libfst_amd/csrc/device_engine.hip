@@ -104,10 +104,19 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
     DeviceFst::destroy(d);
     return nullptr;
   }
-  uint32_t max_span = 0;
+  uint32_t max_span = 0, jb = 0, jf = 0;
   const StateEntry* se = f.states();
-  for (uint32_t i = 0; i < ns; ++i) max_span = std::max(max_span, se[i].num_arcs);
-  d->view = RhsView{d->span, d->final_w, d->il, d->rec, d->sspan, ns, na, h.start_state, max_span};
+  const PackedArc* pa = f.arcs();
+  for (uint32_t i = 0; i < ns; ++i) {
+    max_span = std::max(max_span, se[i].num_arcs);
+    for (uint32_t a = se[i].arc_offset; a < se[i].arc_offset + se[i].num_arcs; ++a) {
+      const uint32_t t = pa[a].nextstate;
+      if (t >= i) jf = std::max(jf, t - i);
+      else jb = std::max(jb, i - t);
+    }
+  }
+  d->view = RhsView{d->span, d->final_w, d->il,       d->rec,        d->sspan,
+                    ns,      na,         h.start_state, max_span,   jb, jf};
   d->has_eps = f.has_epsilon_input();
   d->nonneg = f.weights_nonnegative();
   d->finite = f.arc_weights_finite();

@@ -43,6 +43,9 @@ struct RhsView {
   uint32_t num_arcs;
   uint32_t start;
   uint32_t max_span;        // largest per-state arc count
+  uint32_t jump_back;       // max (s - t) over arcs s -> t (0 if none goes backwards)
+  uint32_t jump_fwd;        // max (t - s) over arcs s -> t: a layer's targets lie within
+                            // [min state - jump_back, max state + jump_fwd]
 };
 
 struct DeviceFst {

@@ -158,6 +158,7 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
     for (int e = 0; e < EMAX; ++e) s2[e] = rhs.start;
     if (lane == 0) S.dcur[0] = w_one();  // the start tuple
     int32_t fail = kPathOk;
+    uint32_t cmin = rhs.start, cmax = rhs.start;  // bounds of the current layer's states
     unsigned long long mykey = kMaxU64;  // this lane's best final candidate
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
@@ -201,19 +202,32 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
       }
 
       // ---- window of this layer's targets ----
-      uint32_t mn = kEmptyKey, mx = 0;
+      // Banded rhs (RhsView::jump_*): the targets lie in [cmin - jump_back, cmax +
+      // jump_fwd], where [cmin, cmax] bounds this layer's states; if that fits the window
+      // no per-candidate pass is needed.  Otherwise the exact min / max of the targets.
+      uint32_t tmin, tmax;
+      {
+        const uint32_t blo = cmin >= rhs.jump_back ? cmin - rhs.jump_back : 0u;
+        const uint64_t bhi = min((uint64_t)cmax + rhs.jump_fwd, (uint64_t)rhs.num_states - 1);
+        if (bhi - blo < (uint64_t)W) {
+          tmin = blo;
+          tmax = (uint32_t)bhi;
+        } else {
+          uint32_t mn = kEmptyKey, mx = 0;
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        if ((uint32_t)e >= rows) continue;  // uniform
+          for (int e = 0; e < EMAX; ++e) {
+            if ((uint32_t)e >= rows) continue;  // uniform
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-          const bool v = (uint32_t)j < cnt[e];
-          mn = v ? min(mn, ct[e][j]) : mn;
-          mx = v ? max(mx, ct[e][j]) : mx;
+            for (int j = 0; j < KMAX; ++j) {
+              const bool v = (uint32_t)j < cnt[e];
+              mn = v ? min(mn, ct[e][j]) : mn;
+              mx = v ? max(mx, ct[e][j]) : mx;
+            }
+          }
+          tmin = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(mn));
+          tmax = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(mx));
         }
       }
-      const uint32_t tmin = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(mn));
-      const uint32_t tmax = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(mx));
       if (tmax - tmin >= (uint32_t)W) {
         fail = kPathOverflow;  // the hashed tier takes the string
         break;
@@ -237,12 +251,11 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
       }
       wave_lds_sync();
 
-      // ---- (C) tight candidates -> packed back-pointer; creators ----
-      unsigned long long creators = 0;
-      uint32_t nf[EMAX];
+      // ---- (C) tight candidates -> packed back-pointer; creators; (D) their ranks
+      // (candidate order = row, lane, j), one row at a time ----
+      uint32_t n_next = 0;
 #pragma unroll
       for (int e = 0; e < EMAX; ++e) {
-        nf[e] = 0;
         if ((uint32_t)e >= rows) continue;  // uniform
         unsigned long long dm[KMAX];
         uint32_t fi[KMAX];
@@ -256,6 +269,8 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
           dm[j] = S.dmin[ct[e][j]];
           fi[j] = S.first[ct[e][j]];
         }
+        bool cr[KMAX];
+        uint32_t nf = 0;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
           const bool v = (uint32_t)j < cnt[e];
@@ -265,25 +280,16 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
           const uint32_t hi = phi + ((uint32_t)j << 16);
           atomicMin(&S.bpack[tight ? ct[e][j] : trash],
                     ((unsigned long long)hi << 32) | (lc + j));
-          const bool cr = v && fi[j] == ci;
-          creators |= (unsigned long long)cr << (e * KMAX + j);
-          nf[e] += cr ? 1u : 0u;
+          cr[j] = v && fi[j] == ci;
+          nf += cr[j] ? 1u : 0u;
         }
-      }
-      // ---- (D) ranks of the created tuples (candidate order = row, lane, j) ----
-      uint32_t n_next = 0;
+        uint32_t tot;
+        uint32_t rank = n_next + wave_excl_scan_small<kRowBits>(nf, tot);
+        n_next += tot;
 #pragma unroll
-      for (int e = 0; e < EMAX; ++e) {
-        if ((uint32_t)e < rows) {
-          uint32_t tot;
-          uint32_t rank = n_next + wave_excl_scan_small<kRowBits>(nf[e], tot);
-          n_next += tot;
-#pragma unroll
-          for (int j = 0; j < KMAX; ++j) {  // branch-free: non-creators write a trash slot
-            const uint32_t cr = (uint32_t)(creators >> (e * KMAX + j)) & 1u;
-            S.nslot[cr ? rank : trash] = (uint16_t)ct[e][j];
-            rank += cr;
-          }
+        for (int j = 0; j < KMAX; ++j) {  // branch-free: non-creators write a trash slot
+          S.nslot[cr[j] ? rank : trash] = (uint16_t)ct[e][j];
+          rank += cr[j] ? 1u : 0u;
         }
       }
       const bool last = k + 1 == L;
@@ -334,6 +340,8 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
       cur_base = next_base;
       n_cur = n_next;
       tuples += n_next;
+      cmin = tmin;  // the next layer's states lie within this layer's target window
+      cmax = tmax;
       wave_lds_sync();
     }
 

@@ -7,6 +7,8 @@ the chain at A and =wg at B, so each tier is checked on its own as well as behin
 others, against the oracle's compose + shortestPath (compose.zig:29-198,
 shortest-path.zig:18-139), bit-exact.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -80,4 +82,25 @@ def test_long_spans_overflow_to_wide_tiers(tier):
             f.add_arc(s, 1, b + 1, float(b % 3), (s + b) % ns)
     blob = O.freeze(f)
     seqs = [[1] * L for L in (0, 1, 5, 12, 30)]
+    check(blob, *csr(seqs), EAGER)
+
+
+@pytest.mark.parametrize("jump", [3, 40, 200, 400])
+def test_banded_and_long_jump_transducers(tier, jump):
+    # Forward arcs i -> i+1..i+3 plus one long jump i -> i+jump and a backward arc: A0's
+    # banded window (RhsView::jump_*) holds for small jumps, and falls back to the exact
+    # per-candidate window (or hands the string on) when the band outgrows 320 states.
+    f = O.Fst()
+    ns = 700
+    for i in range(ns):
+        f.add_state(float(i % 3) if i % 5 else math.inf)
+    f.start = 0
+    rng = np.random.default_rng(jump)
+    for i in range(ns):
+        for b in range(1, 4):
+            f.add_arc(i, 1 + (i + b) % 2, b, float(rng.integers(0, 3)), min(i + b, ns - 1))
+        f.add_arc(i, 1, 7, 1.0, min(i + jump, ns - 1))
+        f.add_arc(i, 2, 8, 0.5, max(i - 2, 0))
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(1, 3, int(rng.integers(0, 40)))] for _ in range(48)]
     check(blob, *csr(seqs), EAGER)
