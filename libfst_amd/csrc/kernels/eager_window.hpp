@@ -166,7 +166,8 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
     // the string's labels, 64 at a time, one per lane (no load on the layer's chain)
     uint32_t labs = 0;
     for (uint32_t k = 0; k < L; ++k) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+      // watchdog every 16 layers (the clock read is an SMEM round trip)
+      if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
         fail = kPathInternal;
         break;
       }
