@@ -191,7 +191,6 @@ __device__ __forceinline__ void wave_pick_and_backtrace(
         write_status(out, si, kPathOutputFull, tuples, relax);
       } else {
         uint32_t id = cur_base + bp;  // shortest-path.zig:109-136
-#ifndef FSTAMD_EXP_NO_BACKTRACE
         for (uint32_t k = L; k > 0; --k) {
           const uint2 b = back[FB(id, back_cap, 34)];
           const ArcRec r = rhs.rec[FB(b.y, rhs.num_arcs, 35)];
@@ -200,13 +199,6 @@ __device__ __forceinline__ void wave_pick_and_backtrace(
           out.out_w[o + k - 1] = r.weight;  // times(One, w) == w for w >= +0
           id = b.x;
         }
-#else  // timing experiment only: the cost of the dependent backtrace chain
-        for (uint32_t k = L; k > 0; --k) {
-          out.out_il[o + k - 1] = 1;
-          out.out_ol[o + k - 1] = 1;
-          out.out_w[o + k - 1] = 0.0;
-        }
-#endif
         out.status[si] = kPathOk;
         out.path_len[si] = L;
         out.path_off[si] = o;
