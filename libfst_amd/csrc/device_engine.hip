@@ -13,6 +13,7 @@
 
 #include "host_fst.hpp"
 #include "kernels/eager_bfs.hpp"
+#include "kernels/lazy_dense.hpp"
 #include "kernels/lazy_layered.hpp"
 #include "kernels/eager_layered.hpp"
 #include "kernels/eager_wave.hpp"
@@ -192,7 +193,7 @@ constexpr int kEwinWaves = 3;
 
 // Item counters and list counts, one 256-B block shared by the engines (word ranges):
 // run_chain [0..4], lazy replay retry tiers [6..13], run_bfs_chain [8..11] (never in the
-// same call as the replay tiers), run_lazy_layered [32].
+// same call as the replay tiers), run_lazy_layered [32], run_lazy_dense [33].
 constexpr size_t kCounterBytes = 256;
 
 enum Scratch : size_t {
@@ -228,6 +229,11 @@ enum Scratch : size_t {
   kLlAct,
   kElBackW,
   kItems3,
+  kLdRec,
+  kLdBarc,
+  kLdIds,
+  kLdLeaf,
+  kLdFut,
   kNumScratch
 };
 
@@ -541,18 +547,38 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     return hipSuccess;
   }
 
-  // Lazy semantics.  Finite weights >= 0 -> the parallel rounds engine (eager_bfs.hpp,
-  // bfs_lazy_path), one workgroup per string.  Otherwise (+inf arcs, negative weights),
-  // or with FSTAMD_LAZY_ENGINE=replay, the exact replay, one wavefront per string.
-  // Unset: rounds for layered lattices and for large ones; small non-layered lattices
-  // ((max_len + 1) * NS <= 16K bounds the tuples, e.g. config 4's tagger) replay faster.
-  // FSTAMD_LAZY_ENGINE=rounds | replay forces one engine (A/B runs, tests).
+  // Lazy semantics.  Finite weights >= 0 -> the parallel rounds engines or the dense
+  // replay; otherwise (+inf arcs, negative weights) the hashed exact replay.
+  //  * rhs without input epsilons: the layered rounds engine (kernels/lazy_layered.hpp),
+  //    then the general rounds engine (eager_bfs.hpp, bfs_lazy_path) for its leftovers;
+  //  * rhs with input epsilons: the dense replay (kernels/lazy_dense.hpp) -- on epsilon-
+  //    dense lattices nearly every tuple sits at one distance and the rounds degenerate to
+  //    one pop each -- with the general rounds engine for its leftovers; small lattices
+  //    ((max_len + 1) * NS <= 16K, e.g. config 4's tagger) go to the hashed replay.
+  // FSTAMD_LAZY_ENGINE=rounds | replay | dense forces one engine (A/B runs, tests).
   const char* le = std::getenv("FSTAMD_LAZY_ENGINE");
   const bool force_rounds = le && std::strcmp(le, "rounds") == 0;
   const bool force_replay = le && std::strcmp(le, "replay") == 0;
+  const bool force_dense = le && std::strcmp(le, "dense") == 0;
   const bool small = (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
-  const bool use_rounds = rhs.nonneg && rhs.finite && !force_replay &&
-                          (force_rounds || !rhs.has_eps || !small);
+  const bool exact_ok = rhs.nonneg && rhs.finite && !force_replay;
+  const bool use_dense = exact_ok && !force_rounds && (force_dense || (rhs.has_eps && !small));
+  const bool use_rounds = exact_ok && !use_dense && (force_rounds || !rhs.has_eps || !small);
+  if (use_dense) {
+    if (stats) {
+      stats->engine = 5;
+      HIP_TRY(hipEventRecord(ev0_, stream));
+    }
+    bool ran = false;
+    HIP_TRY(run_lazy_dense(rhs, in, n, out, stream, &ran));
+    if (!std::getenv("FSTAMD_DENSE_NOFALLBACK"))  // debug: leave UNSUPPORTED strings
+      HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !ran, true));
+    if (stats) {
+      HIP_TRY(hipEventRecord(ev1_, stream));
+      HIP_TRY(finish_stats(ev0_, ev1_, stats));
+    }
+    return hipSuccess;
+  }
   if (use_rounds) {
     if (stats) {
       stats->engine = 3;
@@ -763,6 +789,77 @@ hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput
                  "back/best/out %.1f reset %.1f | rounds/item %.1f\n",
                  grid, sum[4], sum[0] / 100.0 / it, sum[1] / 100.0 / it, sum[2] / 100.0 / it,
                  sum[3] / 100.0 / it, sum[5] / it);
+  }
+  return hipSuccess;
+}
+
+// Dense lazy replay (kernels/lazy_dense.hpp).  Per wave: rec 16 B + back arc 4 B + id map
+// 4 B per dense tuple, the bitmap, and a future list of a quarter of the dense tuples
+// (compacted when full; a string that still overflows goes to the rounds engine).  The
+// dense arrays are left clean by every string, so they are initialised only when
+// (re)allocated.  *ran = false when the lattice is too large for the engine at all.
+hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                        const BatchOutDev& out, hipStream_t stream, bool* ran) {
+  *ran = false;
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [33] is ours
+  if (!ctr) return hipErrorOutOfMemory;
+  LdWs ws{};
+  ws.lcap = std::max<uint32_t>(in.max_len, 1);
+  ws.dn = (uint64_t)(ws.lcap + 1) * 2 * rhs.view.num_states;
+  if (ws.dn > kLdDenseMax) return hipSuccess;
+  ws.nleaf = (uint32_t)((ws.dn + 63) / 64);
+  ws.nsum = (ws.nleaf + 63) / 64;
+  const size_t lds = (size_t)ws.nsum * 8 + (size_t)ws.lcap * 4;
+  if (lds > 48 * 1024) return hipSuccess;
+  ws.fcap = (uint32_t)std::max<uint64_t>(4096, ws.dn / 4);
+  ws.wd_ticks = watchdog_ticks();
+  const uint64_t per_wave = ws.dn * (16 + 4 + 4) + (uint64_t)ws.nleaf * 8 + (uint64_t)ws.fcap * 16;
+  const uint64_t budget = 64ull << 30;  // of the 288 GB
+  uint32_t grid = (uint32_t)std::min<uint64_t>(
+      {(uint64_t)num_cus_ * 16, (uint64_t)in.num_strings, std::max<uint64_t>(1, budget / per_wave)});
+  if (const char* ge = std::getenv("FSTAMD_DENSE_GRID"))  // debug: fewer waves
+    grid = std::min<uint32_t>(grid, (uint32_t)std::max(1, std::atoi(ge)));
+  grid = std::max<uint32_t>(grid, 1);
+  const size_t g = grid;
+  ws.rec = (uint4*)scratch(kLdRec, g * ws.dn * 16);
+  ws.barc = (uint32_t*)scratch(kLdBarc, g * ws.dn * 4);
+  ws.ids = (uint32_t*)scratch(kLdIds, g * ws.dn * 4);
+  ws.leaf = (unsigned long long*)scratch(kLdLeaf, g * ws.nleaf * 8);
+  ws.fut = (uint4*)scratch(kLdFut, g * ws.fcap * 16);
+  if (!ws.rec || !ws.barc || !ws.ids || !ws.leaf || !ws.fut) return hipErrorOutOfMemory;
+  if (ld_clean_ != bufs_[kLdRec] || ld_clean_bytes_ != sizes_[kLdRec] ||
+      ld_leaf_ != bufs_[kLdLeaf] || ld_leaf_bytes_ != sizes_[kLdLeaf]) {  // new allocation
+    HIP_TRY(hipMemsetAsync(ws.rec, 0xFF, sizes_[kLdRec], stream));
+    HIP_TRY(hipMemsetAsync(ws.leaf, 0, sizes_[kLdLeaf], stream));
+    ld_clean_ = bufs_[kLdRec];
+    ld_clean_bytes_ = sizes_[kLdRec];
+    ld_leaf_ = bufs_[kLdLeaf];
+    ld_leaf_bytes_ = sizes_[kLdLeaf];
+  }
+  HIP_TRY(hipMemsetAsync(ctr + 33, 0, 4, stream));
+  const bool prof = std::getenv("FSTAMD_BFS_PROF") != nullptr;
+  ws.prof = prof ? (unsigned long long*)scratch(kDebug, g * 64) : nullptr;
+  if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, g * 64, stream));
+#ifdef FSTAMD_DEBUG_WAIT
+  HIP_TRY(debug_trace_arm());
+#endif
+  lazy_dense_kernel<<<grid, 64, lds, stream>>>(rhs.view, in, n, ctr + 33, ws, out);
+  HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_DEBUG_WAIT
+  HIP_TRY(debug_wait(stream, grid, "lazy_dense"));
+#endif
+  *ran = true;
+  if (ws.prof) {
+    std::vector<unsigned long long> h(g * 8);
+    HIP_TRY(hipMemcpyAsync(h.data(), ws.prof, h.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    unsigned long long sum[8] = {};
+    for (size_t i = 0; i < h.size(); ++i) sum[i % 8] += h[i];
+    const double it = (double)std::max(1ull, sum[3]);
+    std::fprintf(stderr,
+                 "[lazy-dense prof] grid %u items %llu | per item: pops %.0f advances %.1f "
+                 "future entries scanned %.0f\n",
+                 grid, sum[3], sum[0] / it, sum[1] / it, sum[2] / it);
   }
   return hipSuccess;
 }

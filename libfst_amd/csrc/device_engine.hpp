@@ -162,6 +162,11 @@ class DeviceEngine {
   // not take end UNSUPPORTED / OVERFLOW for run_bfs_chain.
   hipError_t run_lazy_layered(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                               const BatchOutDev& out, hipStream_t stream);
+  // composeShortestPath as a dense-indexed exact replay (kernels/lazy_dense.hpp), for rhs
+  // with input epsilons; strings it does not take end UNSUPPORTED / OVERFLOW for
+  // run_bfs_chain.  *ran = false: it took none (the lattice exceeds its dense index).
+  hipError_t run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                            const BatchOutDev& out, hipStream_t stream, bool* ran);
   void* scratch(size_t idx, size_t bytes);
   int dev_;
   int num_cus_ = 0;
@@ -173,6 +178,10 @@ class DeviceEngine {
   uint32_t lazy_stamp_ = 0;      // next stamp base (bumped per launch)
   void* ll_clean_ = nullptr;     // lazy-layered dense arrays initialised for this allocation
   size_t ll_clean_bytes_ = 0;
+  void* ld_clean_ = nullptr;     // lazy-dense rec / leaf arrays initialised for these allocations
+  size_t ld_clean_bytes_ = 0;
+  void* ld_leaf_ = nullptr;
+  size_t ld_leaf_bytes_ = 0;
 };
 
 }  // namespace fstamd

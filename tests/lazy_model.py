@@ -137,3 +137,115 @@ def lazy_via_rounds(lhs: O.Fst, blob: bytes):
     arcs.reverse()
     return ([a[0] for a in arcs], [a[1] for a in arcs], [a[2] for a in arcs],
             lat.finals[best[1]]), rounds
+
+
+# ---------------------------------------------------------------------------------
+# Bucket replay (kernels/lazy_dense.hpp): the reference's own pop sequence, with the
+# heap split into (a) the set of open tuples at the current distance dcur, as a bitmap
+# over ids (pop = lowest set bit), and (b) an unsorted list of (dist, tuple) entries
+# above dcur, scanned when the bitmap empties (dcur advances to the smallest valid
+# entry; every valid entry at that distance moves into the bitmap).
+# ---------------------------------------------------------------------------------
+def lazy_via_buckets(labels, rhs: O.Fst, stats=None):
+    """composeShortestPath(chain(labels), frozen(rhs), 1) for finite weights >= 0 and
+    labels != 0.  Returns the oracle_ffi.chain tuple, None (empty) or "cycle"."""
+    L = len(labels)
+    NS = rhs.num_states
+    if rhs.start == O.NO_STATE:
+        return None
+    # fromMutable sorts by (il, ol, w, next): arc.zig:46-54
+    arcs = [sorted(a, key=lambda t: (t[0], t[1], t[2], t[3])) for a in rhs.arcs]
+    idx_of = []                       # id -> (k, s, f)
+    rec = {}                          # (k, s, f) -> [dist, id, settled, back]
+    bucket = set()                    # ids open at dcur
+    future = []                       # (dist, tuple)
+    st = {"pops": 0, "advances": 0, "scanned": 0, "future_max": 0, "bucket_max": 0}
+
+    def touch(t):
+        r = rec.get(t)
+        if r is None:
+            r = [math.inf, len(idx_of), False, None]
+            rec[t] = r
+            idx_of.append(t)
+            return r, True
+        return r, False
+
+    t0 = (0, rhs.start, 0)
+    r0, _ = touch(t0)
+    r0[0] = 0.0
+    dcur = 0.0
+    bucket.add(0)
+    best = None                       # (total, id, fw)
+    while True:
+        if not bucket:               # advance: scan + compact the future list
+            st["advances"] += 1
+            st["scanned"] += len(future)
+            live = [(d, t) for (d, t) in future if not rec[t][2] and rec[t][0] == d]
+            if not live:
+                break
+            dcur = min(d for d, _ in live)
+            future = [(d, t) for (d, t) in live if d != dcur]
+            for d, t in live:
+                if d == dcur:
+                    bucket.add(rec[t][1])
+        st["bucket_max"] = max(st["bucket_max"], len(bucket))
+        pid = min(bucket)
+        bucket.discard(pid)
+        st["pops"] += 1
+        if stats is not None and "order" in stats:
+            stats["order"].append(pid)
+        t = idx_of[pid]
+        r = rec[t]
+        assert r[0] == dcur and not r[2]
+        r[2] = True
+        k, s, f = t
+        fw1 = 0.0 if k == L else math.inf
+        fw2 = rhs.finals[s]
+        if not math.isinf(fw1) and not math.isinf(fw2):
+            total = dcur + (fw1 + fw2)
+            if best is None or total < best[0] or (total == best[0] and pid < best[1]):
+                best = (total, pid, fw1 + fw2)
+        cands = []                    # (target, il, ol, w) in the reference's phase order
+        if k < L:
+            cands += [((k + 1, a[3], 0), a[0], a[1], 0.0 + a[2])
+                      for a in arcs[s] if a[0] == labels[k]]
+        if f != 2:
+            cands += [((k, a[3], 0 if False else 1), 0, a[1], a[2])
+                      for a in arcs[s] if a[0] == 0]
+        for (x, il, ol, w) in cands:
+            rx, new = touch(x)
+            nd = dcur + w
+            od = rx[0]
+            take = math.isinf(od) or nd < od
+            if not take and nd == od:
+                b = rx[3]
+                take = b is None or pid < b[0] or (pid == b[0] and (il, ol) < (b[1], b[2]))
+            if not take:
+                continue
+            rx[0] = nd
+            rx[3] = (pid, il, ol, w)
+            if rx[2] or nd == od:
+                continue                  # settled, or already queued at this distance
+            if nd == dcur:
+                bucket.add(rx[1])
+            else:
+                future.append((nd, x))
+        st["future_max"] = max(st["future_max"], len(future))
+    if stats is not None:
+        stats.update(st)
+    if best is None:
+        return None
+    out = []
+    cur = best[1]
+    for _ in range(len(idx_of) + 1):
+        if cur == 0:
+            break
+        b = rec[idx_of[cur]][3]
+        if b is None:
+            return None
+        out.append(b[1:])
+        cur = b[0]
+    else:
+        return "cycle"
+    out.reverse()
+    return ([a[0] for a in out], [a[1] for a in out], [a[2] for a in out], best[2])

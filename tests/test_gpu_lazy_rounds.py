@@ -1,11 +1,12 @@
 """GPU parity of the lazy engines against the oracle's sequential composeShortestPath
 (src/ops/compose-shortest-path.zig:26-401): the parallel rounds engines -- layered
 (kernels/lazy_layered.hpp) and general (kernels/eager_bfs.hpp, bfs_lazy_path) -- and the
-replay (kernels/lazy_wave.hpp).
+replay (kernels/lazy_wave.hpp) and the dense replay (kernels/lazy_dense.hpp).
 
-FSTAMD_LAZY_ENGINE=replay | rounds forces one engine (FSTAMD_LAZY_LAYERED=0 keeps the
+FSTAMD_LAZY_ENGINE=replay | rounds | dense forces one engine (FSTAMD_LAZY_LAYERED=0 keeps the
 rounds on the general engine); unset, the engine is chosen by the rhs and batch shape
-(fst_last_launch_stats().engine: 1 replay, 3 general rounds, 4 layered + general)."""
+(fst_last_launch_stats().engine: 1 replay, 3 general rounds, 4 layered + general,
+5 dense replay + general rounds for its leftovers)."""
 import math
 
 import numpy as np
@@ -18,13 +19,13 @@ from test_gpu_parity import LAZY, check, csr, load_blob, random_rhs
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["rounds", "general", "replay"])
+@pytest.fixture(params=["rounds", "general", "replay", "dense"])
 def engine(request, monkeypatch):
     monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
     monkeypatch.delenv("FSTAMD_LAZY_LAYERED", raising=False)
-    if request.param == "replay":
-        monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
-        return "replay"
+    if request.param in ("replay", "dense"):
+        monkeypatch.setenv("FSTAMD_LAZY_ENGINE", request.param)
+        return request.param
     monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "rounds")
     if request.param == "general":  # general rounds engine only (no layered engine)
         monkeypatch.setenv("FSTAMD_LAZY_LAYERED", "0")
@@ -34,7 +35,7 @@ def engine(request, monkeypatch):
 def expect_engine(engine):
     st = F.last_launch_stats()
     # 3 = general rounds engine, 4 = layered engine first (rhs without input epsilons)
-    assert st.engine in ((3, 4) if engine == "rounds" else (1,))
+    assert st.engine in {"rounds": (3, 4), "replay": (1,), "dense": (5,)}[engine]
 
 
 @pytest.mark.parametrize("seed", range(16))
@@ -109,3 +110,21 @@ def test_engines_agree_on_a_large_varied_batch(monkeypatch):
     assert np.array_equal(a.ilabels, b.ilabels) and np.array_equal(a.olabels, b.olabels)
     assert np.array_equal(a.weights.view(np.uint64), b.weights.view(np.uint64))
     assert np.array_equal(a.finals.view(np.uint64), b.finals.view(np.uint64))
+
+
+def test_wide_states(engine):
+    # states with more than 64 arcs: candidates are enumerated in chunks of 64 (dense
+    # replay) and relaxations of one pop hit the same target across chunks
+    rng = np.random.default_rng(4242)
+    f = O.Fst()
+    for _ in range(6):
+        f.add_state(float(rng.integers(0, 3)))
+    f.start = 0
+    for s in range(6):
+        for _ in range(int(rng.integers(60, 140))):
+            f.add_arc(s, int(rng.integers(0, 3)), int(rng.integers(0, 4)),
+                      float(rng.integers(0, 3)), int(rng.integers(0, 6)))
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(1, 3, int(rng.integers(0, 6)))] for _ in range(24)]
+    check(blob, *csr(seqs), LAZY)
+    expect_engine(engine)

@@ -53,3 +53,29 @@ def test_model_bench_shapes(name, T, L, max_rounds):
     if max_rounds is not None:
         # 4 pops' worth of depth per input symbol: the metric's 8385 pops in 257 rounds
         assert rounds <= max_rounds
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_bucket_model_random(block):
+    """The dense replay's model (kernels/lazy_dense.hpp: open-at-dcur bitmap + future list)
+    gives the oracle's exact lazy result on chain inputs without label 0."""
+    for seed in range(block * 200, block * 200 + 200):
+        rng = np.random.default_rng(5000 + seed)
+        rhs = random_rhs(rng, int(rng.integers(1, 15)), int(rng.integers(1, 60)), 3, eps=True,
+                         wmax=2, frac=seed % 3 == 0)
+        labels = [int(x) for x in rng.integers(1, 4, size=int(rng.integers(0, 9)))]
+        blob = O.freeze(rhs)
+        assert M.lazy_via_buckets(labels, rhs) == oracle_lazy(chain_of(labels), blob), seed
+
+
+@pytest.mark.parametrize("name,T,L", [("eps_dense", 64, 12), ("eps_dense", 256, 24),
+                                      ("ambiguous", 4096, 64)])
+def test_bucket_model_bench_shapes(name, T, L):
+    rhs = O.gen(name, T, 12)
+    st = {"order": []}
+    got = M.lazy_via_buckets([1] * L, rhs, st)
+    assert got == oracle_lazy(chain_of([1] * L), O.freeze(rhs))
+    # pops run in near-id order: the cached lowest leaf serves almost every pop
+    o = st["order"]
+    leaf_changes = sum(1 for a, b in zip(o, o[1:]) if a // 64 != b // 64)
+    assert leaf_changes <= len(o) // 8
