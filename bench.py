@@ -80,7 +80,7 @@ def dev_ptr(t):
 class DeviceBatch:
     """Device-resident inputs + outputs of one batch (torch tensors as plumbing)."""
 
-    def __init__(self, lengths, label_fn, dev):
+    def __init__(self, lengths, label_fn, dev, arc_factor=1):
         B = len(lengths)
         lens = torch.as_tensor(lengths, dtype=torch.int64)
         self.offsets = torch.zeros(B + 1, dtype=torch.int64)
@@ -90,7 +90,9 @@ class DeviceBatch:
         self.offsets = self.offsets.to(dev)
         self.num = B
         self.max_len = int(lens.max()) if B else 0
-        self.cap = max(total + 64, 1024)
+        # path arena: L arcs per string on the metric; epsilon lattices (arc_factor > 1)
+        # can produce longer paths
+        self.cap = max(arc_factor * total + 64, 1024)
         self.status = torch.empty(B, dtype=torch.int32, device=dev)
         self.plen = torch.empty(B, dtype=torch.int32, device=dev)
         self.poff = torch.empty(B, dtype=torch.int64, device=dev)

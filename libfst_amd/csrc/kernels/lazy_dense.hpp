@@ -60,7 +60,12 @@ constexpr uint32_t kLdSettled = 0x80000000u;
 constexpr uint32_t kLdNoPrev = 0xFFFFFFFFu;     // no back-pointer (the start; new tuples)
 constexpr uint64_t kLdDenseMax = 0x7FFFFF00ull;  // ids and dense indices fit 31 bits
 
+// The id -> dense index map of the newest kLdRing ids also lives in LDS: pops follow the
+// creation frontier closely (near-id order), so most pops find their tuple there.
+constexpr uint32_t kLdRing = 2048;
+
 struct LdLds {
+  uint32_t ring[kLdRing];  // ids[id] for id >= nn - kLdRing
   uint32_t x[64];    // candidates in relax order: target dense index
   uint32_t a[64];    // rhs arc index
   uint32_t il[64];
@@ -159,6 +164,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
   if (lane == 0) {
     R[x0] = ld_rec(w_one(), 0u, kLdNoPrev);
     ids[0] = x0;
+    S.ring[0] = x0;
     leaf[0] = 1ull;
     sum[0] = 1ull;
   }
@@ -193,7 +199,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
     // ---- the lowest open id at dcur ----
     bool have = uni(cache && cur_bits != 0ull ? 1u : 0u) != 0u;
     while (!have) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * ws.wd_ticks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {
         fail = kPathInternal;
         site = 1;
         break;
@@ -274,12 +280,11 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
     }
 
     // ---- pop (:159-163: an open id is never stale nor settled) ----
-    // The previous pop's stores (records, id map) must be complete before this pop's
-    // loads read them: s_waitcnt on the wave's outstanding memory operations.
-    ld_drain();
+    // (No wait for the previous pop's stores: a wave's vector memory operations to one
+    // address are performed in order, so its later loads see them.)
     const uint32_t pid = uni(cur_leaf * 64 + (uint32_t)__ffsll((long long)cur_bits) - 1);
     cur_bits = uni64(cur_bits & (cur_bits - 1));
-    const uint32_t x = uni(ids[pid]);
+    const uint32_t x = uni(pid + kLdRing >= nn ? S.ring[pid & (kLdRing - 1)] : ids[pid]);
     if (lane == 0) {
       atomicAnd(&leaf[cur_leaf], ~(1ull << (pid & 63)));
       if (cur_bits == 0ull) atomicAnd(&sum[cur_leaf >> 6], ~(1ull << (cur_leaf & 63)));
@@ -287,7 +292,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
     }
     ++pops;
     FT(item, si, pops, 3);
-    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2 * ws.wd_ticks) {
+    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {
       fail = kPathInternal;
       site = 2;
       break;
@@ -449,7 +454,10 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
       if (took) {
         R[tx] = ld_rec(cd, untouched ? id : rv.z, pid);
         barc[tx] = ba;
-        if (fresh) ids[id] = tx;
+        if (fresh) {
+          ids[id] = tx;
+          S.ring[id & (kLdRing - 1)] = tx;
+        }
       }
       // push (:136-140): open at dcur -> bitmap, above -> future list.  An equal-dist
       // take (a tie) is already queued at that distance.
@@ -569,14 +577,15 @@ lazy_dense_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
   for (uint32_t i = lane; i < ws.nsum; i += 64) sum[i] = 0ull;
   wave_lds_sync();
 
+  uint32_t passes = 0;
   for (;;) {
     // The structurizer may turn this loop into nested divergent loops in which lane 0
     // leaves to fetch work while the others re-run the old item (it did, with a lane-0
     // fetch + shfl: a wave replayed item 0 forever).  Hence the first-active-lane fetch
     // below (tier-A post-mortem).
-    // hard stop: even a wave whose control flow went wrong ends (the host reads its
-    // strings' statuses as they are)
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 3 * ws.wd_ticks) return;
+    // hard stop: every pass of this loop consumes a fresh item, so a wave whose control
+    // flow went wrong (re-running an item) ends after num_strings passes
+    if (++passes > in.num_strings + 1) return;
     // work item: fetched by the FIRST ACTIVE lane and broadcast with readlane, so every
     // subset of lanes the compiler's loop structure may run fetches its own item
     uint32_t item = 0;
@@ -594,8 +603,7 @@ lazy_dense_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       pre = (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN;
     else if (L > ws.lcap)
       pre = kPathUnsupported;
-    else if (__builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks)
-      pre = kPathInternal;
+    V.t0 = __builtin_amdgcn_s_memrealtime();  // the string's watchdog starts now
     if (pre == kPathOk) {
       bool zero_label = false;
       for (uint32_t i = lane; i < L; i += 64) {

@@ -116,12 +116,13 @@ def config2(n=65536, L=64):
     return out
 
 
-def config3(T=256, n=256):
+def config3(T=1024, n=4096):
     fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, 12)
     rhs, blob = dev_rhs(fz)
     rng = np.random.default_rng(0x5EED)
     lens = rng.integers(11, 252, n)
-    b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0")
+    b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0",
+                              arc_factor=4)
     wall, kms = timed_device(b, rhs, F.FST_SEM_LAZY, steps=1)
     st = b.status.cpu().numpy()
     labels = np.ones(int(lens[:8].sum()), np.uint32)

@@ -40,7 +40,8 @@ def main():
         fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, 12)
         blob = D.blob_bytes(fz)
         rhs = D.adopt_on_device(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to("cuda:0"), 0)
-        b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0")
+        b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0",
+                              arc_factor=4)
         stream = torch.cuda.current_stream().cuda_stream
         torch.cuda.synchronize()
         t0 = time.perf_counter()
