@@ -814,7 +814,7 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
   ws.fcap = (uint32_t)std::max<uint64_t>(4096, ws.dn / 4);
   ws.wd_ticks = watchdog_ticks();
   const uint64_t per_wave = ws.dn * (16 + 4 + 4) + (uint64_t)ws.nleaf * 8 + (uint64_t)ws.fcap * 16;
-  const uint64_t budget = 96ull << 30;  // of the 288 GB: latency-bound, so many waves
+  const uint64_t budget = 128ull << 30;  // of the 288 GB: latency-bound, so many waves
   uint32_t grid = (uint32_t)std::min<uint64_t>(
       {(uint64_t)num_cus_ * 16, (uint64_t)in.num_strings, std::max<uint64_t>(1, budget / per_wave)});
   if (const char* ge = std::getenv("FSTAMD_DENSE_GRID"))  // debug: fewer waves

@@ -62,7 +62,7 @@ constexpr uint64_t kLdDenseMax = 0x7FFFFF00ull;  // ids and dense indices fit 31
 
 // The id -> dense index map of the newest kLdRing ids also lives in LDS: pops follow the
 // creation frontier closely (near-id order), so most pops find their tuple there.
-constexpr uint32_t kLdRing = 2048;
+constexpr uint32_t kLdRing = 512;
 
 struct LdLds {
   uint32_t ring[kLdRing];  // ids[id] for id >= nn - kLdRing
@@ -189,10 +189,13 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
       atomicOr(&leaf[li], bit);
       atomicOr(&sum[li >> 6], 1ull << (li & 63));
     }
-    const unsigned long long add = wave_or_u64(ins && li == cur_leaf ? bit : 0ull);
-    cur_bits = uni64(cur_bits | add);
-    if (__ballot(ins && li < cur_leaf)) cache = false;
-    scur = min(scur, uni(wave_min_u32d(ins ? (li >> 6) : ~0u)));
+    // ids at or above the cached leaf keep it the lowest non-empty one (scur <= its
+    // summary word already); only an id below it forces a rescan (rare: a joiner)
+    if (__ballot(ins && li == cur_leaf)) cur_bits = uni64(cur_bits | wave_or_u64(ins && li == cur_leaf ? bit : 0ull));
+    if (__ballot(ins && li < cur_leaf)) {
+      cache = false;
+      scur = min(scur, uni(wave_min_u32d(ins ? (li >> 6) : ~0u)));
+    }
   };
 
   for (;;) {
