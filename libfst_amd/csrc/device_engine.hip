@@ -234,6 +234,7 @@ enum Scratch : size_t {
   kLdIds,
   kLdLeaf,
   kLdFut,
+  kLdItems,
   kNumScratch
 };
 
@@ -803,30 +804,94 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
   *ran = false;
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [33] is ours
   if (!ctr) return hipErrorOutOfMemory;
-  LdWs ws{};
-  ws.lcap = std::max<uint32_t>(in.max_len, 1);
-  ws.dn = (uint64_t)(ws.lcap + 1) * 2 * rhs.view.num_states;
-  if (ws.dn > kLdDenseMax) return hipSuccess;
-  ws.nleaf = (uint32_t)((ws.dn + 63) / 64);
-  ws.nsum = (ws.nleaf + 63) / 64;
-  const size_t lds = (size_t)ws.nsum * 8 + (size_t)ws.lcap * 4;
-  if (lds > 48 * 1024) return hipSuccess;
-  ws.fcap = (uint32_t)std::max<uint64_t>(4096, ws.dn / 4);
-  ws.wd_ticks = watchdog_ticks();
-  const uint64_t per_wave = ws.dn * (16 + 4 + 4) + (uint64_t)ws.nleaf * 8 + (uint64_t)ws.fcap * 16;
+  // One launch plan: the per-wave dense state is sized by the longest string it takes.
+  struct Plan {
+    uint32_t lcap, nleaf, nsum, fcap, grid, first, count;  // [first, first + count) of items
+    uint64_t dn;
+    size_t lds;
+  };
   const uint64_t budget = 128ull << 30;  // of the 288 GB: latency-bound, so many waves
-  uint32_t grid = (uint32_t)std::min<uint64_t>(
-      {(uint64_t)num_cus_ * 16, (uint64_t)in.num_strings, std::max<uint64_t>(1, budget / per_wave)});
-  if (const char* ge = std::getenv("FSTAMD_DENSE_GRID"))  // debug: fewer waves
-    grid = std::min<uint32_t>(grid, (uint32_t)std::max(1, std::atoi(ge)));
-  grid = std::max<uint32_t>(grid, 1);
-  const size_t g = grid;
-  ws.rec = (uint4*)scratch(kLdRec, g * ws.dn * 16);
-  ws.barc = (uint32_t*)scratch(kLdBarc, g * ws.dn * 4);
-  ws.ids = (uint32_t*)scratch(kLdIds, g * ws.dn * 4);
-  ws.leaf = (unsigned long long*)scratch(kLdLeaf, g * ws.nleaf * 8);
-  ws.fut = (uint4*)scratch(kLdFut, g * ws.fcap * 16);
-  if (!ws.rec || !ws.barc || !ws.ids || !ws.leaf || !ws.fut) return hipErrorOutOfMemory;
+  const uint32_t max_waves = (uint32_t)num_cus_ * 16;
+  const char* ge = std::getenv("FSTAMD_DENSE_GRID");  // debug: fewer waves
+  auto make_plan = [&](uint32_t max_len, uint32_t count, Plan& p) -> bool {
+    p.lcap = std::max<uint32_t>(max_len, 1);
+    p.dn = (uint64_t)(p.lcap + 1) * 2 * rhs.view.num_states;
+    if (p.dn > kLdDenseMax) return false;
+    p.nleaf = (uint32_t)((p.dn + 63) / 64);
+    p.nsum = (p.nleaf + 63) / 64;
+    p.lds = (size_t)p.nsum * 8 + (size_t)p.lcap * 4;
+    if (p.lds > 48 * 1024) return false;
+    p.fcap = (uint32_t)std::max<uint64_t>(4096, p.dn / 4);
+    const uint64_t per_wave = p.dn * (16 + 4 + 4) + (uint64_t)p.nleaf * 8 + (uint64_t)p.fcap * 16;
+    p.grid = (uint32_t)std::min<uint64_t>(
+        {(uint64_t)max_waves, (uint64_t)count, std::max<uint64_t>(1, budget / per_wave)});
+    if (ge) p.grid = std::min<uint32_t>(p.grid, (uint32_t)std::max(1, std::atoi(ge)));
+    p.grid = std::max<uint32_t>(p.grid, 1);
+    p.count = count;
+    p.first = 0;
+    return true;
+  };
+  Plan whole;
+  if (!make_plan(in.max_len, in.num_strings, whole)) return hipSuccess;
+  // Length buckets.  When the dense state of the longest string caps the waves in flight
+  // (budget / per-wave < max_waves: large rhs, e.g. config 3 at T >= 4096), the strings are
+  // launched in buckets of similar length, each sized by its own longest string, so short
+  // strings run many more waves at once.  Results do not depend on the launch a string is
+  // in.  FSTAMD_DENSE_BUCKETS=k forces k buckets (tests), =1 turns them off.
+  std::vector<Plan> plans;
+  std::vector<uint32_t> order;  // string indices, bucket by bucket
+  // Only for batches that refill every bucket's waves many times over: with fewer strings
+  // a bucket runs one string per wave and its tail dominates (T = 4096, 4096 strings:
+  // 14.1 s bucketed vs 9.2 s in one launch).
+  uint32_t nb = (whole.grid < max_waves && in.num_strings >= 8ull * max_waves) ? 4u : 1u;
+  if (const char* be = std::getenv("FSTAMD_DENSE_BUCKETS"))
+    nb = (uint32_t)std::max(1, std::atoi(be));
+  nb = std::min<uint32_t>(nb, std::max<uint32_t>(in.num_strings, 1));
+  if (nb > 1) {
+    std::vector<uint64_t> off((size_t)in.num_strings + 1);
+    HIP_TRY(hipMemcpyAsync(off.data(), in.offsets, off.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    order.resize(in.num_strings);
+    for (uint32_t i = 0; i < in.num_strings; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      return off[a + 1] - off[a] < off[b + 1] - off[b];
+    });
+    for (uint32_t b = 0; b < nb; ++b) {  // equal-count buckets of the sorted lengths
+      const uint32_t lo = (uint32_t)((uint64_t)in.num_strings * b / nb);
+      const uint32_t hi = (uint32_t)((uint64_t)in.num_strings * (b + 1) / nb);
+      if (hi == lo) continue;
+      const uint32_t last = order[hi - 1];
+      // a length above max_len (caller's bound) keeps the whole plan: the kernel passes
+      // such a string on (UNSUPPORTED) exactly as without buckets
+      const uint32_t blen = (uint32_t)std::min<uint64_t>(off[last + 1] - off[last], in.max_len);
+      Plan p;
+      if (!make_plan(blen, hi - lo, p)) p = whole;
+      p.first = lo;
+      p.count = hi - lo;
+      plans.push_back(p);
+    }
+  } else {
+    plans.push_back(whole);
+  }
+  // one allocation per array, sized for the largest launch
+  uint64_t need_rec = 0, need_leaf = 0, need_fut = 0;
+  for (const Plan& p : plans) {
+    need_rec = std::max<uint64_t>(need_rec, (uint64_t)p.grid * p.dn);
+    need_leaf = std::max<uint64_t>(need_leaf, (uint64_t)p.grid * p.nleaf);
+    need_fut = std::max<uint64_t>(need_fut, (uint64_t)p.grid * p.fcap);
+  }
+  LdWs ws{};
+  ws.rec = (uint4*)scratch(kLdRec, need_rec * 16);
+  ws.barc = (uint32_t*)scratch(kLdBarc, need_rec * 4);
+  ws.ids = (uint32_t*)scratch(kLdIds, need_rec * 4);
+  ws.leaf = (unsigned long long*)scratch(kLdLeaf, need_leaf * 8);
+  ws.fut = (uint4*)scratch(kLdFut, need_fut * 16);
+  uint32_t* d_order = nullptr;
+  if (!order.empty()) d_order = (uint32_t*)scratch(kLdItems, order.size() * 4);
+  if (!ws.rec || !ws.barc || !ws.ids || !ws.leaf || !ws.fut || (!order.empty() && !d_order))
+    return hipErrorOutOfMemory;
+  // every string leaves the rec / leaf words it touched clean, whatever the launch's
+  // partition of the buffers, so they are initialised once per allocation
   if (ld_clean_ != bufs_[kLdRec] || ld_clean_bytes_ != sizes_[kLdRec] ||
       ld_leaf_ != bufs_[kLdLeaf] || ld_leaf_bytes_ != sizes_[kLdLeaf]) {  // new allocation
     HIP_TRY(hipMemsetAsync(ws.rec, 0xFF, sizes_[kLdRec], stream));
@@ -836,18 +901,37 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     ld_leaf_ = bufs_[kLdLeaf];
     ld_leaf_bytes_ = sizes_[kLdLeaf];
   }
-  HIP_TRY(hipMemsetAsync(ctr + 33, 0, 4, stream));
+  if (d_order) {  // pageable source: wait for the copy before `order` goes away
+    HIP_TRY(hipMemcpyAsync(d_order, order.data(), order.size() * 4, hipMemcpyHostToDevice,
+                           stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
   const bool prof = std::getenv("FSTAMD_BFS_PROF") != nullptr;
-  ws.prof = prof ? (unsigned long long*)scratch(kDebug, g * 64) : nullptr;
-  if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, g * 64, stream));
+  uint32_t gmax = 0;
+  for (const Plan& p : plans) gmax = std::max(gmax, p.grid);
+  ws.prof = prof ? (unsigned long long*)scratch(kDebug, (size_t)gmax * 64) : nullptr;
+  if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)gmax * 64, stream));
+  for (const Plan& p : plans) {
+    ws.lcap = p.lcap;
+    ws.dn = p.dn;
+    ws.nleaf = p.nleaf;
+    ws.nsum = p.nsum;
+    ws.fcap = p.fcap;
+    ws.wd_ticks = watchdog_ticks();
+    ws.items = d_order ? d_order + p.first : nullptr;
+    ws.num_items = p.count;
+    HIP_TRY(hipMemsetAsync(ctr + 33, 0, 4, stream));
 #ifdef FSTAMD_DEBUG_WAIT
-  HIP_TRY(debug_trace_arm());
+    HIP_TRY(debug_trace_arm());
 #endif
-  lazy_dense_kernel<<<grid, 64, lds, stream>>>(rhs.view, in, n, ctr + 33, ws, out);
-  HIP_TRY(hipGetLastError());
+    lazy_dense_kernel<<<p.grid, 64, p.lds, stream>>>(rhs.view, in, n, ctr + 33, ws, out);
+    HIP_TRY(hipGetLastError());
 #ifdef FSTAMD_DEBUG_WAIT
-  HIP_TRY(debug_wait(stream, grid, "lazy_dense"));
+    HIP_TRY(debug_wait(stream, p.grid, "lazy_dense"));
 #endif
+  }
+  const size_t g = gmax;
+  const uint32_t grid = gmax;
   *ran = true;
   if (ws.prof) {
     std::vector<unsigned long long> h(g * 8);

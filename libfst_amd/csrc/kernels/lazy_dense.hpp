@@ -53,6 +53,8 @@ struct LdWs {
   uint32_t nleaf, nsum, fcap, lcap;
   unsigned long long wd_ticks;
   unsigned long long* prof;   // [grid * 8] (FSTAMD_BFS_PROF): pops, advances, scanned, items
+  const uint32_t* items;      // this launch's strings (a length bucket), or nullptr = all
+  uint32_t num_items;         // entries of items (ignored when items is nullptr)
 };
 
 constexpr uint32_t kLdUntouched = 0xFFFFFFFFu;  // rec id word of an untouched tuple
@@ -137,7 +139,7 @@ struct LdWave {
   unsigned long long t0;
 };
 
-// One string, start to finish (called once per work item).
+// One string (index `item` into the batch), start to finish.
 __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const ChainInput& in,
                                                const LdWs& ws, const BatchOutDev& out,
                                                const LdWave& V, uint32_t item, uint32_t L) {
@@ -580,6 +582,7 @@ lazy_dense_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
   for (uint32_t i = lane; i < ws.nsum; i += 64) sum[i] = 0ull;
   wave_lds_sync();
 
+  const uint32_t num_items = ws.items ? ws.num_items : in.num_strings;
   uint32_t passes = 0;
   for (;;) {
     // The structurizer may turn this loop into nested divergent loops in which lane 0
@@ -588,7 +591,7 @@ lazy_dense_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     // below (tier-A post-mortem).
     // hard stop: every pass of this loop consumes a fresh item, so a wave whose control
     // flow went wrong (re-running an item) ends after num_strings passes
-    if (++passes > in.num_strings + 1) return;
+    if (++passes > num_items + 1) return;
     // work item: fetched by the FIRST ACTIVE lane and broadcast with readlane, so every
     // subset of lanes the compiler's loop structure may run fetches its own item
     uint32_t item = 0;
@@ -596,8 +599,8 @@ lazy_dense_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == first)
       item = atomicAdd(next_item, 1u);
     item = __builtin_amdgcn_readlane(item, first);
-    if (item >= in.num_strings) break;
-    const uint32_t si = item;
+    if (item >= num_items) break;
+    const uint32_t si = ws.items ? uni(ws.items[item]) : item;
     const uint64_t off = in.offsets[si];
     const uint32_t L = uni((uint32_t)(in.offsets[si + 1] - off));
     FT(item, si, L, 1);
@@ -623,7 +626,7 @@ lazy_dense_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       if (lane == 0) write_status(out, si, pre, 0, 0);
       FT(item, si, pre, 2);
     } else {
-      lazy_dense_string(rhs, in, ws, out, V, item, L);
+      lazy_dense_string(rhs, in, ws, out, V, si, L);
     }
   }
   FT(0xFFFFFFFFu, 0, 0, 8);

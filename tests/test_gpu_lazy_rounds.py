@@ -128,3 +128,24 @@ def test_wide_states(engine):
     seqs = [[int(x) for x in rng.integers(1, 3, int(rng.integers(0, 6)))] for _ in range(24)]
     check(blob, *csr(seqs), LAZY)
     expect_engine(engine)
+
+
+@pytest.mark.parametrize("buckets", [2, 3, 7])
+def test_dense_length_buckets(monkeypatch, buckets):
+    # Length buckets of the dense replay (device_engine.hip run_lazy_dense): the strings
+    # are sorted by length and launched per bucket, each launch sizing the per-wave dense
+    # state by its own longest string.  Forced here (on a large rhs they start by
+    # themselves); the answers must not depend on the partition.  Mixed lengths, label-0
+    # strings (passed on to the general rounds engine) and random tie-heavy rhs.
+    monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "dense")
+    monkeypatch.setenv("FSTAMD_DENSE_BUCKETS", str(buckets))
+    rng = np.random.default_rng(4100 + buckets)
+    blob = O.freeze(O.gen("eps_dense", 128, 12))
+    lens = [int(x) for x in rng.integers(0, 60, 40)]
+    check(blob, *csr([[1] * L for L in lens]), LAZY)
+    assert F.last_launch_stats().engine == 5
+    f = random_rhs(rng, 24, 90, 3, eps=True, wmax=2, frac=True)
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(0 if i % 9 == 0 else 1, 4, int(rng.integers(0, 14)))]
+            for i in range(64)]
+    check(blob, *csr(seqs), LAZY)
