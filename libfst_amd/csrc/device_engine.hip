@@ -847,7 +847,13 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
   if (const char* be = std::getenv("FSTAMD_DENSE_BUCKETS"))
     nb = (uint32_t)std::max(1, std::atoi(be));
   nb = std::min<uint32_t>(nb, std::max<uint32_t>(in.num_strings, 1));
-  if (nb > 1) {
+  // Longest first inside a launch: work items are taken in order, so when a launch has
+  // more strings than waves the long strings start first and the short ones fill the
+  // tail (list scheduling, longest processing time first).  FSTAMD_DENSE_LPT=0 turns it
+  // off (measurements).
+  bool lpt = in.num_strings > whole.grid;
+  if (const char* le = std::getenv("FSTAMD_DENSE_LPT")) lpt = lpt && std::atoi(le) != 0;
+  if (nb > 1 || lpt) {
     std::vector<uint64_t> off((size_t)in.num_strings + 1);
     HIP_TRY(hipMemcpyAsync(off.data(), in.offsets, off.size() * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -865,9 +871,10 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
       // such a string on (UNSUPPORTED) exactly as without buckets
       const uint32_t blen = (uint32_t)std::min<uint64_t>(off[last + 1] - off[last], in.max_len);
       Plan p;
-      if (!make_plan(blen, hi - lo, p)) p = whole;
+      if (nb == 1 || !make_plan(blen, hi - lo, p)) p = whole;
       p.first = lo;
       p.count = hi - lo;
+      if (lpt) std::reverse(order.begin() + lo, order.begin() + hi);
       plans.push_back(p);
     }
   } else {
