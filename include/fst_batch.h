@@ -131,7 +131,8 @@ typedef struct {
     double kernel_ms;           /* sum of kernel durations, HIP events on the launch stream */
     uint32_t launches;          /* kernel launches in the call */
     uint32_t engine;            /* 0 = eager-layered, 1 = lazy replay, 2 = eager-general,
-                                   3 = lazy rounds, 4 = lazy layered (+ rounds for the rest) */
+                                   3 = lazy rounds, 4 = lazy layered (+ rounds for the rest),
+                                   5 = lazy dense replay, 6 = shortest-path heap replay */
     uint32_t grid;              /* workgroups of the dominant kernel */
 } FstLaunchStats;
 FstError fst_last_launch_stats(FstLaunchStats* out);

@@ -209,6 +209,7 @@ struct GraphUpload {
   GraphInput g{};
   bool ok = false;
   bool nonneg = true;  // every arc and final weight >= +0.0 (no -0.0, no NaN)
+  bool nan = false;    // some arc or final weight is NaN
   explicit GraphUpload(const MutableFst& a)
       : off((a.num_states() + 1) * 4ull), il(a.total_arcs() * 4), ol(a.total_arcs() * 4),
         w(a.total_arcs() * 8), nx(a.total_arcs() * 4), fin(a.num_states() * 8ull) {
@@ -221,6 +222,7 @@ struct GraphUpload {
       soff[s] = (uint32_t)vil.size();
       vfin[s] = a.final_weight(s);
       if (neg(vfin[s])) nonneg = false;
+      if (std::isnan(vfin[s])) nan = true;
       maxdeg = std::max<uint32_t>(maxdeg, (uint32_t)a.arcs(s).size());
       for (const Arc& x : a.arcs(s)) {
         vil.push_back(x.ilabel);
@@ -228,6 +230,7 @@ struct GraphUpload {
         vw.push_back(x.weight);
         vnx.push_back(x.nextstate);
         if (neg(x.weight)) nonneg = false;
+        if (std::isnan(x.weight)) nan = true;
       }
     }
     soff[ns] = (uint32_t)vil.size();
@@ -703,9 +706,10 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
     const int dev = current_device();
     if (dev < 0) return kInvalid;
     GraphUpload up(*m);
-    // The GPU 1-best is exact for non-negative weights (eager_bfs.hpp); a negative
-    // weight (Dijkstra replay) is not covered yet: reported as an error.
-    if (!up.ok || !up.nonneg) return kInvalid;
+    // Non-negative weights: the parallel fixpoint (eager_bfs.hpp); a negative weight:
+    // the exact replay of the reference's heap order (sp_replay_kernel).  NaN has no
+    // order in the reference's compare (std.math.order): reported as an error.
+    if (!up.ok || up.nan) return kInvalid;
     const uint64_t cap = std::max<uint64_t>(m->num_states() + 16, 1024);
     DevOut out(1, cap);
     if (!out.ok()) return kInvalid;
@@ -714,7 +718,7 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
     {
       DeviceEngine& E = DeviceEngine::get(dev);
       std::lock_guard<std::mutex> lk(E.mutex());
-      if (E.shortest_path_graph(up.g, n, out.v, &st) != hipSuccess) return kInvalid;
+      if (E.shortest_path_graph(up.g, n, out.v, &st, up.nonneg) != hipSuccess) return kInvalid;
       if (!out.download(1, &hp)) return kInvalid;
     }
     t_last_stats = st;

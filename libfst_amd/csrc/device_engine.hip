@@ -1117,9 +1117,41 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
 }
 
 hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
-                                             const BatchOutDev& out, LaunchStats* stats) {
+                                             const BatchOutDev& out, LaunchStats* stats,
+                                             bool nonneg) {
   HIP_TRY(hipSetDevice(dev_));
   const uint32_t N = g.num_states;
+  if (!nonneg) {  // negative weights: exact replay of the heap order, one lane
+    uint32_t A = 0;
+    if (N) HIP_TRY(hipMemcpy(&A, g.state_off + N, 4, hipMemcpyDeviceToHost));
+    const uint64_t hcap = (uint64_t)A + 1;
+    const size_t nd_b = ((size_t)N * 16 + 255) & ~(size_t)255;
+    const size_t st_b = ((size_t)N + 255) & ~(size_t)255;
+    uint8_t* w = (uint8_t*)scratch(kBfsSlab, nd_b + st_b + hcap * sizeof(SpHeapEnt));
+    if (!w) return hipErrorOutOfMemory;
+    HIP_TRY(hipMemset(out.cursor, 0, 8));
+    BfsTables T{};
+    T.aoff = const_cast<uint32_t*>(g.state_off);
+    T.anext = const_cast<uint32_t*>(g.arc_next);
+    T.ail = const_cast<uint32_t*>(g.arc_il);
+    T.aol = const_cast<uint32_t*>(g.arc_ol);
+    T.aw = const_cast<double*>(g.arc_w);
+    T.nfin = const_cast<double*>(g.final_w);
+    T.nd = (unsigned long long*)w;
+    T.nback = (unsigned long long*)(w + (size_t)N * 8);
+    if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
+    sp_replay_kernel<<<1, 64, 0, nullptr>>>(T, N, g.start, n, (SpHeapEnt*)(w + nd_b + st_b),
+                                            hcap, w + nd_b, out, watchdog_ticks());
+    HIP_TRY(hipGetLastError());
+    if (stats) {
+      HIP_TRY(hipEventRecord(ev1_, nullptr));
+      HIP_TRY(finish_stats(ev0_, ev1_, stats));
+      stats->engine = 6;
+      stats->grid = 1;
+      stats->launches = 1;
+    }
+    return hipDeviceSynchronize();
+  }
   // work arrays: distances, back-pointers, the one "level" [0, N)
   uint8_t* w = (uint8_t*)scratch(kBfsSlab, (size_t)N * 16 + 256);
   uint32_t* lv = (uint32_t*)scratch(kBfsHdr, 16);

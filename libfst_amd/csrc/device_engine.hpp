@@ -142,9 +142,10 @@ class DeviceEngine {
                             uint64_t* next_offsets, int32_t* proj_status, uint32_t* max_len,
                             hipStream_t stream);
   // fst_shortest_path on an explicit graph; `g` holds the FST itself (CSR, arcs in
-  // insertion order).  Non-negative weights only (the caller checks).
+  // insertion order).  nonneg: every weight >= +0 (parallel fixpoint); otherwise the exact
+  // one-lane replay of the reference's heap order (sp_replay_kernel).  No NaN weights.
   hipError_t shortest_path_graph(const GraphInput& g, uint32_t n, const BatchOutDev& out,
-                                 LaunchStats* stats);
+                                 LaunchStats* stats, bool nonneg = true);
 
   int dev() const { return dev_; }
   std::mutex& mutex() { return mu_; }

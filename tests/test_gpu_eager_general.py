@@ -7,6 +7,8 @@
 * batch eager semantics on lattices the layered kernels do not take (rhs epsilons,
   label-0 inputs), bit-exact against oracle compose + shortestPath.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -123,10 +125,56 @@ def test_shortest_path_on_compose_result():
     assert sp.print_string(output_tape=True) == b"abc"
 
 
-def test_shortest_path_negative_weight_is_reported():
+def test_shortest_path_negative_weight_chain():
+    # a negative weight takes the exact heap replay (sp_replay_kernel)
     f = chain_of([1, 2])
     f.arcs[0][0] = (1, 1, -1.0, 1)
-    assert F.shortest_path(to_product(f), 1) is None
+    compare_sp(f)
+    assert F.last_launch_stats().engine == 6
+
+
+def negative_graph(rng, ns, na, frac):
+    # Forward arcs (s < next) carry weights in [-3, 3]; backward arcs and self-loops are
+    # heavier than any negative forward path (no negative cycle), so back-pointer chains
+    # end at the start.  A few -0.0 / -inf (a Zero) / -2.5 specials, negative finals.
+    f = O.Fst()
+    for _ in range(ns):
+        fin = float(rng.integers(-2, 3)) if rng.random() < 0.5 else math.inf
+        f.add_state(fin)
+    f.start = 0
+    specials = [-0.0, -math.inf, -2.5, 0.0]
+    for _ in range(na):
+        s, x = int(rng.integers(ns)), int(rng.integers(ns))
+        w = float(rng.integers(-3, 4)) if s < x else float(rng.integers(250, 254))
+        if frac:
+            w += float(rng.random()) * (1 if w >= 0 else -1)
+        if rng.random() < 0.06:
+            w = specials[int(rng.integers(len(specials)))] if s < x else 250.0
+        f.add_arc(s, int(rng.integers(0, 5)), int(rng.integers(0, 5)), w, x)
+    return f
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_shortest_path_negative_weights(seed):
+    # Dijkstra with negative arcs: settled states still move (shortest-path.zig:70-84) and
+    # the answer depends on the (dist, id) pop order -- replayed exactly, checked against
+    # the oracle's heap.  Back-pointer cycles (the reference would not terminate) are
+    # reported as errors on both sides.
+    rng = np.random.default_rng(6100 + seed)
+    f = negative_graph(rng, int(rng.integers(2, 60)), int(rng.integers(1, 240)), seed % 2 == 1)
+    compare_sp(f)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_shortest_path_negative_cycles(seed):
+    # unconstrained signs: mostly back-pointer cycles (zero-weight self-loops on the start,
+    # negative cycles), which both sides report, plus the occasional path
+    rng = np.random.default_rng(6200 + seed)
+    f = random_rhs(rng, int(rng.integers(1, 40)), int(rng.integers(0, 160)), 4, eps=True,
+                   frac=seed % 2 == 1)
+    for s in range(len(f.arcs)):
+        f.arcs[s] = [(il, ol, -w if rng.random() < 0.3 else w, nx) for il, ol, w, nx in f.arcs[s]]
+    compare_sp(f)
 
 
 # ---------------------------------------------------------------------------------------
