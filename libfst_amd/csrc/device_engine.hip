@@ -120,6 +120,7 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
                     ns,      na,         h.start_state, max_span,   jb, jf};
   d->has_eps = f.has_epsilon_input();
   d->nonneg = f.weights_nonnegative();
+  d->nan = f.has_nan_weight();
   d->finite = f.arc_weights_finite();
   d->weight_type = f.weight_type();
   return d;
@@ -235,6 +236,7 @@ enum Scratch : size_t {
   kLdLeaf,
   kLdFut,
   kLdItems,
+  kBfsHeap,
   kNumScratch
 };
 
@@ -370,12 +372,25 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
 
   // Eager semantics on a layered lattice -> eager-layered engine.
   if (semantics == 1) {
-    if (!rhs.nonneg) {
-      // Negative weights: shortest-path.zig's Dijkstra is then not the exact SSSP the
-      // eager engines compute (an exact replay is future work): UNSUPPORTED.
+    if (rhs.nan) {  // NaN has no order in the reference's compare: UNSUPPORTED
       mark_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(in.num_strings, n,
                                                                            rhs.view.start, out);
       return hipGetLastError();
+    }
+    if (!rhs.nonneg) {
+      // Negative weights: shortest-path.zig's Dijkstra is then not the exact SSSP the
+      // parallel engines compute; the general engine builds each lattice and replays
+      // the heap order on it (sp_replay, kernels/eager_bfs.hpp).
+      if (stats) {
+        stats->engine = 6;
+        HIP_TRY(hipEventRecord(ev0_, stream));
+      }
+      HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, true, false, true));
+      if (stats) {
+        HIP_TRY(hipEventRecord(ev1_, stream));
+        HIP_TRY(finish_stats(ev0_, ev1_, stats));
+      }
+      return hipSuccess;
     }
     if (rhs.has_eps) {  // not layered: the general BFS engine takes every string
       if (stats) {
@@ -957,7 +972,7 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
 
 hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                        const BatchOutDev& out, hipStream_t stream, bool all,
-                                       bool lazy) {
+                                       bool lazy, bool replay) {
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [8..15] are ours
   uint32_t* list = (uint32_t*)scratch(kBfsList, (size_t)in.num_strings * 4);
   uint32_t* list2 = (uint32_t*)scratch(kBfsList2, (size_t)in.num_strings * 4);
@@ -1001,6 +1016,11 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     ws.wd_ticks = watchdog_ticks();
     ws.lattice_only = 0;
     ws.lazy = lazy ? 1u : 0u;
+    if (replay && !lazy) {  // heap + settled flags per workgroup (kernels/eager_bfs.hpp)
+      ws.replay = (uint8_t*)scratch(kBfsHeap,
+                                    (size_t)grid * ((size_t)(c.acap + 1) * 16 + c.ncap));
+      if (!ws.replay) return hipErrorOutOfMemory;
+    }
     const bool prof = std::getenv("FSTAMD_BFS_PROF") != nullptr;
     ws.prof = prof ? (unsigned long long*)scratch(kDebug, (size_t)grid * 64) : nullptr;
     if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)grid * 64, stream));

@@ -60,6 +60,7 @@ struct DeviceFst {
   RhsView view{};
   bool has_eps = false;
   bool nonneg = true;        // every arc and final weight >= +0
+  bool nan = false;          // some arc or final weight is NaN
   bool finite = true;        // every arc weight finite
   uint8_t weight_type = 0;
 
@@ -158,7 +159,7 @@ class DeviceEngine {
   // Grows its per-string workspace in tiers.  Synchronises on `stream` to size the tiers.
   hipError_t run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                            const BatchOutDev& out, hipStream_t stream, bool all,
-                           bool lazy = false);
+                           bool lazy = false, bool replay = false);
   // composeShortestPath on layered lattices (kernels/lazy_layered.hpp); strings it does
   // not take end UNSUPPORTED / OVERFLOW for run_bfs_chain.
   hipError_t run_lazy_layered(const DeviceFst& rhs, const ChainInput& in, uint32_t n,

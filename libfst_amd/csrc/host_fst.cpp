@@ -138,6 +138,7 @@ std::shared_ptr<FrozenFst> FrozenFst::from_bytes(const uint8_t* bytes, size_t le
 void FrozenFst::analyze() {
   has_eps_ = false;
   nonneg_ = true;
+  nan_ = false;
   finite_ = true;
   const Header& h = header();
   const PackedArc* a = arcs();
@@ -145,12 +146,14 @@ void FrozenFst::analyze() {
     if (a[i].ilabel == kEpsilon) has_eps_ = true;
     const double w = a[i].weight;
     if (!(w >= 0.0) || std::signbit(w)) nonneg_ = false;  // negative, -0.0 or NaN
+    if (std::isnan(w)) nan_ = true;
     if (!std::isfinite(w)) finite_ = false;
   }
   const StateEntry* s = states();
   for (uint32_t i = 0; i < h.num_states; ++i) {
     const double w = s[i].final_weight;
     if (!(w >= 0.0) || std::signbit(w)) nonneg_ = false;
+    if (std::isnan(w)) nan_ = true;
   }
 }
 

@@ -94,6 +94,7 @@ class FrozenFst {
   // Properties the engines route on (computed once).
   bool has_epsilon_input() const { return has_eps_; }
   bool weights_nonnegative() const { return nonneg_; }
+  bool has_nan_weight() const { return nan_; }
   bool arc_weights_finite() const { return finite_; }
 
   // Lazily uploaded per-device copy (blob + SoA mirror); thread safe.
@@ -108,6 +109,7 @@ class FrozenFst {
   size_t size_ = 0;
   bool has_eps_ = false;
   bool nonneg_ = true;
+  bool nan_ = false;
   bool finite_ = true;
   std::mutex dev_mu_;
   std::vector<DeviceFst*> dev_;

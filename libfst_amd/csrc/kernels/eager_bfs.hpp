@@ -40,6 +40,8 @@ struct BfsWs {
   uint32_t lattice_only;    // 1: stop after compose (fst_compose_frozen)
   uint32_t lazy;            // 1: composeShortestPath semantics (bfs_lazy_path)
   unsigned long long* prof; // [grid * 8] phase ticks (FSTAMD_BFS_PROF) or null
+  uint8_t* replay;          // non-null: exact heap replay (negative weights); per workgroup
+                            // (acap + 1) * 16 B of heap, then ncap B of settled flags
 };
 
 // Phase profile (thread 0): prof[slot] += ticks since *tp; *tp = now.  Slots: 0 compose,
@@ -790,6 +792,149 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Exact replay of shortestPath (src/ops/shortest-path.zig:18-139) for weights of any sign
+// (fst_shortest_path, or the eager batch, with a negative weight).  With a negative arc Dijkstra is no longer
+// the least fixpoint: a settled state's dist and back-pointer still move (:70-84) but its
+// arcs are never relaxed again, so the answer depends on the pop order.  The queue order
+// is total -- (dist, state) lexicographic (:56-62) -- and two entries equal in both are
+// interchangeable (the second is skipped as settled), so any binary heap pops the same
+// sequence; one lane replays it.  Pushes happen once per relaxation of an unsettled
+// target, at most once per arc per settle, so the heap never holds more than
+// n_arcs + 1 entries.  Latency-bound by construction: it only serves rhs / graphs with a
+// negative weight, and the deadline turns a runaway into INTERNAL.
+// ---------------------------------------------------------------------------------------
+struct SpHeapEnt {
+  double d;
+  uint32_t s, pad;
+};
+__device__ __forceinline__ bool sp_heap_less(const SpHeapEnt& a, const SpHeapEnt& b) {
+  return a.d < b.d || (a.d == b.d && a.s < b.s);  // W.compare = IEEE order, then the id
+}
+
+// The whole workgroup calls it (it initialises with every thread); thread 0 replays.
+__device__ void sp_replay(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
+                          uint32_t start, SpHeapEnt* heap, uint64_t hcap, uint8_t* settled,
+                          const BatchOutDev& out, uint32_t si, unsigned long long deadline) {
+  const uint32_t lane = threadIdx.x;
+  double* dist = reinterpret_cast<double*>(T.nd);
+  for (uint32_t s = lane; s < n_nodes; s += blockDim.x) {  // :35-37, :45-49
+    dist[s] = __builtin_huge_val();
+    T.nback[s] = ~0ull;
+    settled[s] = 0;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  dist[start] = 0.0;
+  uint64_t hn = 1;
+  heap[0] = SpHeapEnt{0.0, start, 0};
+  uint64_t pops = 0;
+  while (hn > 0) {  // :65
+    const SpHeapEnt item = heap[0];
+    const SpHeapEnt last = heap[--hn];
+    uint64_t k = 0;  // sift `last` down from the root
+    for (;;) {
+      uint64_t c = 2 * k + 1;
+      if (c >= hn) break;
+      if (c + 1 < hn && sp_heap_less(heap[c + 1], heap[c])) ++c;
+      if (!sp_heap_less(heap[c], last)) break;
+      heap[k] = heap[c];
+      k = c;
+    }
+    if (hn) heap[k] = last;
+    if ((++pops & 1023) == 0 && __builtin_amdgcn_s_memrealtime() > deadline) {
+      write_status(out, si, kPathInternal, n_nodes, n_arcs);
+      return;
+    }
+    const uint32_t s = item.s;
+    if (settled[s]) continue;
+    if (!(item.d == dist[s])) continue;  // stale entry (:68)
+    settled[s] = 1;
+    const double ds = dist[s];
+    const uint32_t a0 = T.aoff[s], a1 = T.aoff[s + 1];
+    for (uint32_t a = a0; a < a1; ++a) {  // :71-84
+      const uint32_t x = T.anext[a];
+      const double nd = w_times(ds, T.aw[a]);
+      const double od = dist[x];
+      const unsigned long long b = T.nback[x];
+      const uint32_t prev = b == ~0ull ? kNoState : (uint32_t)(b >> 32);
+      const bool tie = nd == od && (prev == kNoState || s < prev);
+      if (w_is_zero(od) || nd < od || tie) {
+        dist[x] = nd;
+        T.nback[x] = ((unsigned long long)s << 32) | (a - a0);
+        if (!settled[x]) {
+          if (hn >= hcap) {  // cannot happen (<= one push per arc per settle + 1)
+            write_status(out, si, kPathInternal, n_nodes, n_arcs);
+            return;
+          }
+          uint64_t j = hn++;  // sift up
+          const SpHeapEnt e{nd, x, 0};
+          while (j > 0) {
+            const uint64_t pj = (j - 1) / 2;
+            if (!sp_heap_less(e, heap[pj])) break;
+            heap[j] = heap[pj];
+            j = pj;
+          }
+          heap[j] = e;
+        }
+      }
+    }
+  }
+  // best final: lexmin (total, id) over reachable states (:88-104)
+  uint32_t best = kNoState;
+  double bt = __builtin_huge_val();
+  for (uint32_t s = 0; s < n_nodes; ++s) {
+    if (w_is_zero(dist[s]) || w_is_zero(T.nfin[s])) continue;
+    const double t = w_times(dist[s], T.nfin[s]);
+    if (best == kNoState || t < bt) {  // equal totals keep the smaller id
+      best = s;
+      bt = t;
+    }
+  }
+  if (best == kNoState) {
+    write_status(out, si, kPathEmpty, n_nodes, n_arcs);
+    return;
+  }
+  uint32_t cur = best, hops = 0;  // backtrace (:109-122), bounded: a cycle reports CYCLE
+  for (;;) {
+    const unsigned long long b = T.nback[cur];
+    if (b == ~0ull) break;
+    if (++hops > n_nodes) {
+      write_status(out, si, kPathCycle, n_nodes, n_arcs);
+      return;
+    }
+    cur = (uint32_t)(b >> 32);
+  }
+  if (cur != start) {
+    write_status(out, si, kPathEmpty, n_nodes, n_arcs);
+    return;
+  }
+  const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)hops);
+  if (o + hops > out.arc_cap) {
+    write_status(out, si, kPathOutputFull, n_nodes, n_arcs);
+    return;
+  }
+  cur = best;
+  for (uint32_t k = hops; k > 0; --k) {
+    const unsigned long long b = T.nback[cur];
+    const uint32_t s = (uint32_t)(b >> 32);
+    const uint32_t a = T.aoff[s] + (uint32_t)b;
+    out.out_il[o + k - 1] = T.ail[a];
+    out.out_ol[o + k - 1] = T.aol[a];
+    out.out_w[o + k - 1] = T.aw[a];
+    cur = s;
+  }
+  out.status[si] = kPathOk;
+  out.path_len[si] = hops;
+  out.path_off[si] = o;
+  out.final_w[si] = T.nfin[best];
+  if (out.work) {
+    out.work[2 * si] = n_nodes;
+    out.work[2 * si + 1] = n_arcs;
+  }
+}
+
+
 template <int WG, bool kGraph>
 __global__ void __launch_bounds__(WG)
 eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
@@ -1035,6 +1180,10 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       bfs_lazy_path<WG>(T, ws.ncap, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
                         t0 + 2 * ws.wd_ticks, prof, &tp, dag);
       prof_mark(prof, 3, &tp);
+    } else if (ws.replay) {
+      uint8_t* r = ws.replay + (size_t)blockIdx.x * ((size_t)(ws.acap + 1) * 16 + ws.ncap);
+      sp_replay(T, n_nodes, n_arcs, 0u, (SpHeapEnt*)r, (uint64_t)ws.acap + 1,
+                r + (size_t)(ws.acap + 1) * 16, out, si, t0 + 2 * ws.wd_ticks);
     } else
       bfs_shortest_path<WG>(T, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
                             t0 + 2 * ws.wd_ticks, false, dag);
@@ -1060,156 +1209,20 @@ sp_graph_kernel(BfsTables T, uint32_t n_nodes, uint32_t start, uint32_t n_best, 
                         __builtin_amdgcn_s_memrealtime() + wd_ticks);
 }
 
-// ---------------------------------------------------------------------------------------
-// Exact replay of shortestPath (src/ops/shortest-path.zig:18-139) for weights of any sign
-// (fst_shortest_path with a negative weight).  With a negative arc Dijkstra is no longer
-// the least fixpoint: a settled state's dist and back-pointer still move (:70-84) but its
-// arcs are never relaxed again, so the answer depends on the pop order.  The queue order
-// is total -- (dist, state) lexicographic (:56-62) -- and two entries equal in both are
-// interchangeable (the second is skipped as settled), so any binary heap pops the same
-// sequence; one lane replays it.  Pushes happen once per relaxation of an unsettled
-// target, at most once per arc per settle, so the heap never holds more than
-// n_arcs + 1 entries.  Latency-bound by construction: it only serves the single-call
-// entry, and the deadline turns a runaway into INTERNAL.
-// ---------------------------------------------------------------------------------------
-struct SpHeapEnt {
-  double d;
-  uint32_t s, pad;
-};
-__device__ __forceinline__ bool sp_heap_less(const SpHeapEnt& a, const SpHeapEnt& b) {
-  return a.d < b.d || (a.d == b.d && a.s < b.s);  // W.compare = IEEE order, then the id
-}
-
 __global__ void __launch_bounds__(64)
 sp_replay_kernel(BfsTables T, uint32_t n_nodes, uint32_t start, uint32_t n_best,
                  SpHeapEnt* heap, uint64_t hcap, uint8_t* settled, BatchOutDev out,
                  unsigned long long wd_ticks) {
-  const uint32_t lane = threadIdx.x;
-  const uint32_t n_arcs = n_nodes ? T.aoff[n_nodes] : 0;
   if (start == kNoState || n_best == 0 || n_nodes == 0) {  // :21-23
-    if (lane == 0) write_status(out, 0, kPathEmpty, 0, 0);
+    if (threadIdx.x == 0) write_status(out, 0, kPathEmpty, 0, 0);
     return;
   }
   if (n_best != 1) {  // :24
-    if (lane == 0) write_status(out, 0, kPathErrorN, 0, 0);
+    if (threadIdx.x == 0) write_status(out, 0, kPathErrorN, 0, 0);
     return;
   }
-  double* dist = reinterpret_cast<double*>(T.nd);
-  for (uint32_t s = lane; s < n_nodes; s += 64) {  // :35-37, :45-49
-    dist[s] = __builtin_huge_val();
-    T.nback[s] = ~0ull;
-    settled[s] = 0;
-  }
-  __syncthreads();
-  if (lane != 0) return;
-  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + wd_ticks;
-  dist[start] = 0.0;
-  uint64_t hn = 1;
-  heap[0] = SpHeapEnt{0.0, start, 0};
-  uint64_t pops = 0;
-  while (hn > 0) {  // :65
-    const SpHeapEnt item = heap[0];
-    const SpHeapEnt last = heap[--hn];
-    uint64_t k = 0;  // sift `last` down from the root
-    for (;;) {
-      uint64_t c = 2 * k + 1;
-      if (c >= hn) break;
-      if (c + 1 < hn && sp_heap_less(heap[c + 1], heap[c])) ++c;
-      if (!sp_heap_less(heap[c], last)) break;
-      heap[k] = heap[c];
-      k = c;
-    }
-    if (hn) heap[k] = last;
-    if ((++pops & 1023) == 0 && __builtin_amdgcn_s_memrealtime() > deadline) {
-      write_status(out, 0, kPathInternal, n_nodes, n_arcs);
-      return;
-    }
-    const uint32_t s = item.s;
-    if (settled[s]) continue;
-    if (!(item.d == dist[s])) continue;  // stale entry (:68)
-    settled[s] = 1;
-    const double ds = dist[s];
-    const uint32_t a0 = T.aoff[s], a1 = T.aoff[s + 1];
-    for (uint32_t a = a0; a < a1; ++a) {  // :71-84
-      const uint32_t x = T.anext[a];
-      const double nd = w_times(ds, T.aw[a]);
-      const double od = dist[x];
-      const unsigned long long b = T.nback[x];
-      const uint32_t prev = b == ~0ull ? kNoState : (uint32_t)(b >> 32);
-      const bool tie = nd == od && (prev == kNoState || s < prev);
-      if (w_is_zero(od) || nd < od || tie) {
-        dist[x] = nd;
-        T.nback[x] = ((unsigned long long)s << 32) | (a - a0);
-        if (!settled[x]) {
-          if (hn >= hcap) {  // cannot happen (<= one push per arc per settle + 1)
-            write_status(out, 0, kPathInternal, n_nodes, n_arcs);
-            return;
-          }
-          uint64_t j = hn++;  // sift up
-          const SpHeapEnt e{nd, x, 0};
-          while (j > 0) {
-            const uint64_t pj = (j - 1) / 2;
-            if (!sp_heap_less(e, heap[pj])) break;
-            heap[j] = heap[pj];
-            j = pj;
-          }
-          heap[j] = e;
-        }
-      }
-    }
-  }
-  // best final: lexmin (total, id) over reachable states (:88-104)
-  uint32_t best = kNoState;
-  double bt = __builtin_huge_val();
-  for (uint32_t s = 0; s < n_nodes; ++s) {
-    if (w_is_zero(dist[s]) || w_is_zero(T.nfin[s])) continue;
-    const double t = w_times(dist[s], T.nfin[s]);
-    if (best == kNoState || t < bt) {  // equal totals keep the smaller id
-      best = s;
-      bt = t;
-    }
-  }
-  if (best == kNoState) {
-    write_status(out, 0, kPathEmpty, n_nodes, n_arcs);
-    return;
-  }
-  uint32_t cur = best, hops = 0;  // backtrace (:109-122), bounded: a cycle reports CYCLE
-  for (;;) {
-    const unsigned long long b = T.nback[cur];
-    if (b == ~0ull) break;
-    if (++hops > n_nodes) {
-      write_status(out, 0, kPathCycle, n_nodes, n_arcs);
-      return;
-    }
-    cur = (uint32_t)(b >> 32);
-  }
-  if (cur != start) {
-    write_status(out, 0, kPathEmpty, n_nodes, n_arcs);
-    return;
-  }
-  const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)hops);
-  if (o + hops > out.arc_cap) {
-    write_status(out, 0, kPathOutputFull, n_nodes, n_arcs);
-    return;
-  }
-  cur = best;
-  for (uint32_t k = hops; k > 0; --k) {
-    const unsigned long long b = T.nback[cur];
-    const uint32_t s = (uint32_t)(b >> 32);
-    const uint32_t a = T.aoff[s] + (uint32_t)b;
-    out.out_il[o + k - 1] = T.ail[a];
-    out.out_ol[o + k - 1] = T.aol[a];
-    out.out_w[o + k - 1] = T.aw[a];
-    cur = s;
-  }
-  out.status[0] = kPathOk;
-  out.path_len[0] = hops;
-  out.path_off[0] = o;
-  out.final_w[0] = T.nfin[best];
-  if (out.work) {
-    out.work[0] = n_nodes;
-    out.work[1] = n_arcs;
-  }
+  sp_replay(T, n_nodes, T.aoff[n_nodes], start, heap, hcap, settled, out, 0u,
+            __builtin_amdgcn_s_memrealtime() + wd_ticks);
 }
 
 }  // namespace fstamd

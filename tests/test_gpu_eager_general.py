@@ -203,3 +203,17 @@ def test_batch_eager_random_with_epsilons(seed):
     blob = O.freeze(f)
     seqs = [[int(x) for x in rng.integers(0, 5, int(rng.integers(0, 12)))] for _ in range(48)]
     check(blob, *csr(seqs), EAGER)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_batch_eager_negative_weights(seed):
+    # eager batch on an rhs with negative weights: the general engine builds each lattice
+    # (compose.zig ids) and replays shortestPath's heap order on it (sp_replay), checked
+    # bit-exact against the oracle's compose + heap Dijkstra, CYCLE statuses included
+    rng = np.random.default_rng(6300 + seed)
+    f = negative_graph(rng, int(rng.integers(2, 30)), int(rng.integers(4, 120)), seed % 2 == 1)
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(0 if i % 7 == 0 else 1, 5, int(rng.integers(0, 10)))]
+            for i in range(48)]
+    check(blob, *csr(seqs), EAGER)
+    assert F.last_launch_stats().engine == 6
