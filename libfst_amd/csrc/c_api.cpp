@@ -328,9 +328,12 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
   const uint32_t num = in.num_strings;
   // Arena: chains without rhs epsilons produce exactly L arcs per path.
   uint64_t arc_cap = std::max<uint64_t>(total_labels + 16, 1024);
+  if (const char* e = std::getenv("FSTAMD_ARENA_ARCS"))  // test override: first arena size
+    if (*e) arc_cap = std::max<uint64_t>(std::strtoull(e, nullptr, 10), 1);
   DeviceEngine& E = DeviceEngine::get(dev);
   std::lock_guard<std::mutex> lk(E.mutex());
-  for (int attempt = 0; attempt < 6; ++attempt, arc_cap *= 4) {
+  constexpr int kAttempts = 6;
+  for (int attempt = 0; attempt < kAttempts; ++attempt, arc_cap *= 4) {
     auto out = std::make_unique<DevOut>(num, arc_cap);
     if (!out->ok()) return FST_OOM;
     LaunchStats st;
@@ -351,12 +354,14 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
       return FST_OOM;
     }
     for (uint32_t i = 0; i < num; ++i) full |= h->status[i] == kPathOutputFull;
-    if (!full) {
+    // The last attempt's result stands: strings still OUTPUT_FULL keep that status (the
+    // caller sees FST_PATH_OUTPUT_FULL per string), and `keep` is always set on FST_OK.
+    if (!full || attempt + 1 == kAttempts) {
       if (keep) *keep = std::move(out);
       return FST_OK;
     }
   }
-  return FST_OK;
+  return FST_OOM;  // unreachable: the last attempt returns above
 }
 
 // HostPaths (engine order) -> FstBatchResult (malloc'ed CSR, fst_batch_result_free).
@@ -868,6 +873,7 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
     FstError e = run_chain_batch_dev(*D, in, in_total, n, semantics, dev, &h, last ? nullptr : &keep);
     if (e != FST_OK) return e;
     if (last) break;
+    if (!keep) return FST_OOM;  // run_chain_batch_dev sets it on FST_OK; never dereference null
     // project this stage's outputs into the next stage's inputs, on the device
     unsigned long long used = 0;
     if (hipMemcpy(&used, keep->v.cursor, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
@@ -955,6 +961,8 @@ FstHandle fst_device_adopt_blob(const void* d_blob, uint64_t len, int32_t device
     return kInvalid;
   Header h;
   std::memcpy(&h, bytes.data(), sizeof(h));
+  // as fst_batch_load_bytes: only the two semirings of weight.zig (fst.zig:43-47)
+  if (h.weight_type != kWeightTropical && h.weight_type != kWeightLog) return kInvalid;
   auto f = FrozenFst::from_bytes(bytes.data(), len, h.weight_type, nullptr);
   if (!f) return kInvalid;
   DeviceFst* D = DeviceFst::adopt(d_blob, *f, dev);

@@ -214,7 +214,7 @@ struct BfsShared {
   uint32_t scan[16];
   unsigned long long red[16];  // per-wave partials of block reductions
   uint32_t item;
-  uint32_t expired;
+  unsigned long long t_item;   // when thread 0 fetched the item: the per-string watchdog
   uint32_t flag;
   uint32_t changed;
   unsigned long long best;
@@ -947,18 +947,20 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
   uint32_t* hdr = ws.hdr + (size_t)blockIdx.x * 8;
   unsigned long long* prof = ws.prof ? ws.prof + (size_t)blockIdx.x * 8 : nullptr;
   const uint32_t num_items = num_items_dev ? *num_items_dev : num_items_host;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t hmask = ws.hcap - 1;
 
   for (;;) {
     __syncthreads();
     if (tid == 0) {
       SH.item = atomicAdd(next_item, 1u);
-      SH.expired = __builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks;
+      SH.t_item = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const uint32_t item = SH.item;
     if (item >= num_items) break;
+    // the watchdog is per string: each string gets the full limit from its own start,
+    // however long the launch has been running (INTERNAL past it)
+    const unsigned long long t0 = SH.t_item;
     const uint32_t si = items ? items[item] : item;
 
     unsigned long long tp = __builtin_amdgcn_s_memrealtime();
@@ -986,10 +988,6 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
         hdr[3] = kPathOk;
         hdr[4] = si;
       }
-      continue;
-    }
-    if (SH.expired) {
-      if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
       continue;
     }
 
@@ -1147,7 +1145,7 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       ++level;
       if (tid == 0) T.lvl[level + 1] = n_nodes;
       __syncthreads();
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * ws.wd_ticks) {  // uniform per wave...
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {  // uniform per wave...
         if (tid == 0) SH.flag = 1;
       }
       __syncthreads();
@@ -1178,15 +1176,15 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
 
     if (ws.lazy) {
       bfs_lazy_path<WG>(T, ws.ncap, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
-                        t0 + 2 * ws.wd_ticks, prof, &tp, dag);
+                        t0 + ws.wd_ticks, prof, &tp, dag);
       prof_mark(prof, 3, &tp);
     } else if (ws.replay) {
       uint8_t* r = ws.replay + (size_t)blockIdx.x * ((size_t)(ws.acap + 1) * 16 + ws.ncap);
       sp_replay(T, n_nodes, n_arcs, 0u, (SpHeapEnt*)r, (uint64_t)ws.acap + 1,
-                r + (size_t)(ws.acap + 1) * 16, out, si, t0 + 2 * ws.wd_ticks);
+                r + (size_t)(ws.acap + 1) * 16, out, si, t0 + ws.wd_ticks);
     } else
       bfs_shortest_path<WG>(T, n_nodes, n_arcs, n_levels, 0u, out, si, SH,
-                            t0 + 2 * ws.wd_ticks, false, dag);
+                            t0 + ws.wd_ticks, false, dag);
   }
 }
 

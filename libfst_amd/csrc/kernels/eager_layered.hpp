@@ -140,6 +140,8 @@ struct LayerShared {
   uint32_t scan[16];
   uint32_t item;
   uint32_t expired;  // watchdog verdict of thread 0 for this item (uniform for all waves)
+  unsigned long long t_item;  // when this item started (thread 0's clock): the watchdog
+                              // is per string, so every string gets the full limit
   uint32_t nnext;
   uint32_t flag;
   uint32_t bestp;
@@ -198,7 +200,6 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
   const uint32_t tid = threadIdx.x;
   uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
   const uint32_t num_items = lp.num_items_dev ? *lp.num_items_dev : lp.num_items;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 
   for (uint32_t i = tid; i < T.hcap; i += WG) tbl_clear_slot(T, i);
 
@@ -206,7 +207,8 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
     __syncthreads();
     if (tid == 0) {
       SH.item = atomicAdd(next_item, 1u);
-      SH.expired = __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks;
+      SH.expired = 0;
+      SH.t_item = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const uint32_t item = SH.item;
@@ -221,12 +223,6 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
       if (tid == 0)
         write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
                      0, 0);
-      continue;
-    }
-    // Watchdog: no bug may keep a workgroup resident forever (status INTERNAL).  The
-    // verdict comes from thread 0 through LDS, so every wave takes the same path.
-    if (SH.expired) {
-      if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
       continue;
     }
 
@@ -288,7 +284,16 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
           atomicMin(&T.h_dmin[slot], (unsigned long long)okey(nd));
         }
       }
+      // Watchdog, per string: no bug may keep a workgroup resident forever (INTERNAL).
+      // Thread 0's verdict goes through LDS, so every wave takes the same path.
+      if (tid == 0 && (k & 15u) == 0 &&
+          __builtin_amdgcn_s_memrealtime() - SH.t_item > lp.wd_ticks)
+        SH.expired = 1;
       __syncthreads();
+      if (SH.expired) {
+        fail = kPathInternal;
+        break;
+      }
       const uint32_t n_next = SH.nnext;
       if (SH.flag || (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
         fail = kPathOverflow;
@@ -474,7 +479,6 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
   T.hbits = __builtin_ctz(HCAP);
   const uint32_t tid = threadIdx.x;
   uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const uint32_t num_items = lp.num_items_dev ? *lp.num_items_dev : lp.num_items;
 
   for (uint32_t i = tid; i < HCAP; i += WG) tbl_clear_slot(T, i);
@@ -483,7 +487,8 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
     __syncthreads();
     if (tid == 0) {
       SH.item = atomicAdd(next_item, 1u);
-      SH.expired = __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks;
+      SH.expired = 0;
+      SH.t_item = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const uint32_t item = SH.item;
@@ -496,10 +501,6 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
       if (tid == 0)
         write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
                      0, 0);
-      continue;
-    }
-    if (SH.expired) {  // thread 0's verdict (LDS): every wave takes the same path
-      if (tid == 0) write_status(out, si, kPathInternal, 0, 0);
       continue;
     }
     if (tid == 0) {
@@ -577,7 +578,14 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
         }
         c += cnt[e];
       }
+      if (tid == 0 && (k & 15u) == 0 &&
+          __builtin_amdgcn_s_memrealtime() - SH.t_item > lp.wd_ticks)
+        SH.expired = 1;  // per-string watchdog, as in eager_layered_kernel
       __syncthreads();
+      if (SH.expired) {
+        fail = kPathInternal;
+        break;
+      }
       const uint32_t n_next = SH.nnext;
       if (SH.flag || (uint64_t)cur_base + n_cur + n_next > lp.back_cap) {
         fail = kPathOverflow;

@@ -246,7 +246,6 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
   uint2* back = lp.back_ws + (size_t)blockIdx.x * lp.back_cap;
   const uint32_t num_items = __builtin_amdgcn_readfirstlane(
       lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 
 #pragma unroll 1
   for (uint32_t i = lane; i < HCAP; i += 64) {
@@ -258,9 +257,6 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
   wave_lds_sync();
 
   for (;;) {
-    // hard stop: even a wave whose control flow went wrong ends (its strings keep the
-    // INTERNAL status the host pre-fills)
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * lp.wd_ticks) return;
     // work item: fetched by the first active lane, broadcast through an SGPR
     uint32_t item = 0;
     if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
@@ -283,10 +279,8 @@ eager_wave_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
                      0, 0);
       continue;
     }
-    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
-      if (lane == 0) write_status(out, si, kPathInternal, 0, 0);
-      continue;
-    }
+    // per-string watchdog: every string gets the full limit (INTERNAL past it)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 
     // layer 0: the start tuple, position 0 (lane 0, row 0)
     uint32_t n_cur = 1, cur_base = 0;

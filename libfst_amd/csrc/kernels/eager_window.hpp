@@ -117,7 +117,6 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
   };
   const uint32_t num_items = __builtin_amdgcn_readfirstlane(
       lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 64; i += 64) {
@@ -128,7 +127,6 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
   wave_lds_sync();
 
   for (;;) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * lp.wd_ticks) return;
     uint32_t item = 0;
     if (lane == 0) item = atomicAdd(next_item, 1u);
     item = __builtin_amdgcn_readfirstlane(item);
@@ -146,10 +144,9 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
                      0, 0);
       continue;
     }
-    if (__builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
-      if (lane == 0) write_status(out, si, kPathInternal, 0, 0);
-      continue;
-    }
+    // the watchdog is per string: every string gets the full limit, however long the
+    // launch has been running (a string that exceeds it reports INTERNAL)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 
     uint32_t n_cur = 1, cur_base = 0;
     uint32_t tuples = 1, relax = 0;

@@ -160,7 +160,6 @@ lazy_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
   uint32_t* inv = ws.inv + w * ws.ncap;
   uint32_t* loff = ws.loff + w * (ws.lcap + 2);
   const uint32_t NS = rhs.num_states;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long* prof = ws.prof ? ws.prof + w * 8 : nullptr;
 
   for (uint32_t guard = 0;; ++guard) {
@@ -179,10 +178,11 @@ lazy_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
                      0, 0);
       continue;
     }
-    if (L > ws.lcap || now0 - t0 > ws.wd_ticks) {
-      if (lane == 0) write_status(out, si, L > ws.lcap ? kPathOverflow : kPathInternal, 0, 0);
+    if (L > ws.lcap) {
+      if (lane == 0) write_status(out, si, kPathOverflow, 0, 0);
       continue;
     }
+    // per-string watchdog: the limit starts with the string, not with the launch
     const unsigned long long deadline = now0 + ws.wd_ticks;
     int32_t fail = kPathOk;
     uint64_t relax = 0;

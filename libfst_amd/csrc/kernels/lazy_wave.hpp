@@ -285,8 +285,10 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
   uint32_t* qid = ws.qid + w * ws.qcap;
   uint4* tbl = ws.gscratch + w * ws.gcap;
   const uint32_t hmask = ws.hcap - 1;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool dead = false;  // watchdog fired: drain the remaining items as INTERNAL
+  // per-string watchdog: both are reset when a string starts, so every string gets the
+  // full limit however long the launch has been running
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool dead = false;  // watchdog fired for the current string: it reports INTERNAL
   uint32_t dbg_pops = 0, dbg_cb = 0, dbg_C = 0, dbg_qn = 0, dbg_nn = 0;
 #define LZ_WD(code)                                                                  \
   if (!dead && wd_expired(t0, ws.wd_ticks)) {                                        \
@@ -308,15 +310,8 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
     item = __shfl(item, 0, 64);
     if (item >= num_items) break;
     const uint32_t si = items ? items[item] : item;
-    if (dead) {
-      if (lane == 0) {
-        out.status[si] = kPathInternal;
-        out.path_len[si] = 0;
-        out.path_off[si] = 0;
-        out.final_w[si] = w_zero();
-      }
-      continue;
-    }
+    t0 = __builtin_amdgcn_s_memrealtime();
+    dead = false;
     const uint32_t stamp = ws.stamp_base + item + 1;
 
     ChainLhs cl{nullptr, 0};
