@@ -123,6 +123,10 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   d->nan = f.has_nan_weight();
   d->finite = f.arc_weights_finite();
   d->weight_type = f.weight_type();
+  if (!build_reverse_mirror(d, f)) {  // pull tier (eager_pull.hip); false = device OOM
+    DeviceFst::destroy(d);
+    return nullptr;
+  }
   return d;
 }
 
@@ -163,6 +167,7 @@ void DeviceFst::destroy(DeviceFst* d) {
   if (d->il) (void)hipFree(d->il);
   if (d->rec) (void)hipFree(d->rec);
   if (d->sspan) (void)hipFree(d->sspan);
+  free_reverse_mirror(d);
   (void)hipSetDevice(cur);
   delete d;
 }
@@ -191,9 +196,10 @@ constexpr int kEwinRows = 5;
 constexpr int kEwinW = 64 * kEwinRows;
 constexpr int kEwinKmax = 5;
 constexpr int kEwinWaves = 3;
+static_assert((uint32_t)kEwinW == kPullW, "tiers P and A0 share the back slab geometry");
 
 // Item counters and list counts, one 256-B block shared by the engines (word ranges):
-// run_chain [0..4], lazy replay retry tiers [6..13], run_bfs_chain [8..11] (never in the
+// run_chain [0..6] and [14..15] (pull tier), lazy replay retry tiers [6..13], run_bfs_chain [8..11] (never in the
 // same call as the replay tiers), run_lazy_layered [32], run_lazy_dense [33].
 constexpr size_t kCounterBytes = 256;
 
@@ -237,6 +243,8 @@ enum Scratch : size_t {
   kLdFut,
   kLdItems,
   kBfsHeap,
+  kPullBack,
+  kItems4,
   kNumScratch
 };
 
@@ -406,15 +414,18 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     // Tier chain for layered lattices (each tier takes the strings the previous one
     // reports as OVERFLOW, through a device-side list):
+    //   P  one wavefront per string, pull over the reverse mirror, window of kPullW states
+    //      (when the rhs has one: DeviceFst::pull_ok)
     //   A0 one wavefront per string, direct-mapped LDS window of kEwinW target states
     //   A  one wavefront per string, LDS hash, <= kEwFcap tuples/layer, spans <= kEwKmax
     //   B  256 threads per string, LDS tables, <= kElFcap tuples/layer, spans <= kElKmax
     //   C  256 threads per string, HBM tables sized by the rhs (any layer)
-    // FSTAMD_EAGER_TIER1=wave starts at A, =wg at B (A/B comparisons).  A tier is skipped
-    // when the previous one provably cannot overflow on this rhs.
+    // FSTAMD_EAGER_TIER1=window starts at A0, =wave at A, =wg at B (A/B comparisons).  A
+    // tier is skipped when the previous one provably cannot overflow on this rhs.
     const char* t1 = std::getenv("FSTAMD_EAGER_TIER1");
     const bool start_b = t1 && std::strcmp(t1, "wg") == 0;
     const bool use_w = !start_b && !(t1 && std::strcmp(t1, "wave") == 0);
+    const bool use_p = use_w && rhs.pull_ok && !(t1 && std::strcmp(t1, "window") == 0);
     const uint32_t ns = rhs.view.num_states, ms = rhs.view.max_span;
     auto back_cap_for = [&](uint32_t fcap, uint64_t limit, bool* capped) {
       const uint64_t want = (uint64_t)(in.max_len + 1) * fcap;
@@ -459,6 +470,20 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
         grid_w /= 2;
       grid_w = std::max<uint32_t>(grid_w, 1);
     }
+    // P: kChaseBatch back slabs per wave too, kPullW slots per layer
+    uint32_t grid_p = 0;
+    uint2* back_p = nullptr;
+    uint32_t* list_pw = nullptr;
+    if (use_p) {
+      grid_p = (uint32_t)std::min<uint64_t>((uint64_t)pull_waves_per_cu(rhs) * num_cus_,
+                                            in.num_strings);
+      while (grid_p > 1 && (uint64_t)grid_p * kChaseBatch * back_cap_w * 8 > (24ull << 30))
+        grid_p /= 2;
+      grid_p = std::max<uint32_t>(grid_p, 1);
+      back_p = (uint2*)scratch(kPullBack, (size_t)grid_p * kChaseBatch * back_cap_w * 8);
+      list_pw = (uint32_t*)scratch(kItems4, (size_t)in.num_strings * 4);
+      if (!back_p || !list_pw) return hipErrorOutOfMemory;
+    }
     const uint32_t grid_a = use_a ? grid_for((const void*)k_wave, 64, back_cap_a) : 0;
     const uint32_t grid_b = need_b ? grid_for((const void*)k_wg, kElWG, back_cap_b) : 0;
     uint2* back_w =
@@ -491,17 +516,36 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     if (stats) {
       stats->engine = 0;
-      stats->grid = use_w ? grid_w : use_a ? grid_a : grid_b;
-      stats->launches = (use_w ? 1 : 0) + (use_a ? (use_w ? 2 : 1) : 0) +
+      stats->grid = use_p ? grid_p : use_w ? grid_w : use_a ? grid_a : grid_b;
+      stats->launches = (use_p ? 2 : 0) + (use_w ? 1 : 0) + (use_a ? (use_w ? 2 : 1) : 0) +
                         (need_b ? ((use_w || use_a) ? 2 : 1) : 0) + (need_c ? 2 : 0);
       HIP_TRY(hipEventRecord(ev0_, stream));
     }
     const unsigned long long wd = watchdog_ticks();
     const uint32_t blocks = (in.num_strings + 255) / 256;
-    // counters: [5] item counter of tier A0, [6] |list_wa|; [0..2] item counters of tiers
-    // A, B, C; [3] |list_ab|; [4] |list_bc|
+    // counters: [14] item counter of tier P, [15] |list_pw|; [5] item counter of tier A0,
+    // [6] |list_wa|; [0..2] item counters of tiers A, B, C; [3] |list_ab|; [4] |list_bc|
+    if (use_p) {
+      EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_p, back_cap_w, wd};
+      HIP_TRY(launch_eager_pull(rhs, in, n, counter + 14, lp, out, grid_p, stream));
+      // test hook: FSTAMD_EAGER_ONLY_FIRST leaves tier P's OVERFLOW / UNSUPPORTED strings
+      // as they are, so a test can tell what the tier itself took
+      if (std::getenv("FSTAMD_EAGER_ONLY_FIRST")) {
+        if (stats) {
+          HIP_TRY(hipEventRecord(ev1_, stream));
+          HIP_TRY(finish_stats(ev0_, ev1_, stats));
+        }
+        return hipSuccess;
+      }
+    }
     if (use_w) {
       EagerLaunch lw{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_w, back_cap_w, wd};
+      if (use_p) {
+        collect_status_kernel<<<blocks, 256, 0, stream>>>(out.status, in.num_strings,
+                                                          kPathOverflow, list_pw, counter + 15);
+        lw.items = list_pw;
+        lw.num_items_dev = counter + 15;
+      }
 #ifdef FSTAMD_DEBUG_WAIT
       HIP_TRY(debug_trace_arm());
 #endif

@@ -48,6 +48,27 @@ struct RhsView {
                             // [min state - jump_back, max state + jump_fwd]
 };
 
+// Reverse arc mirror for the pull tier (kernels/eager_pull.hpp): the in-arcs of every rhs
+// state t, grouped by ilabel, each group in padded blocks of `kp` records.  Record m of a
+// block: the source state, y = (j << 13) | (m << 9) with j = the arc's position in its
+// source's run of equal ilabels (the candidate order of compose.zig:93-121), and the
+// weight.  Padding records have src = kNoState.  Block 0 is all padding (the null block).
+struct RevRec {
+  uint32_t src;
+  uint32_t y;
+  double weight;
+};
+static_assert(sizeof(RevRec) == 16, "RevRec is one 16-byte load");
+struct RevView {
+  const uint4* rspan;     // [num_states] one group: {block, nblocks, ilabel, 0};
+                          // several: {first gtab entry, groups, kSpanMixed, 0}; none: kSpanNone
+  const uint4* gtab;      // groups of multi-label states {ilabel, block, nblocks, 0}, by ilabel
+  const RevRec* rrec;     // [nblocks * kp]
+  const uint32_t* rolab;  // [nblocks * kp] olabel of each record (backtrace only)
+  uint32_t kp;            // records per block
+  uint32_t gsearch;       // binary-search steps over the longest gtab run
+};
+
 struct DeviceFst {
   int dev = 0;
   uint8_t* blob = nullptr;  // the frozen blob itself, byte-identical to the host copy
@@ -63,6 +84,11 @@ struct DeviceFst {
   bool nan = false;          // some arc or final weight is NaN
   bool finite = true;        // every arc weight finite
   uint8_t weight_type = 0;
+  // pull tier (kernels/eager_pull.hpp): reverse mirror, built when the rhs qualifies
+  // (no input epsilon, weights >= +0, every same-ilabel run of a state <= 8 arcs)
+  bool pull_ok = false;
+  RevView rev{};
+  void* rev_bufs[4] = {nullptr, nullptr, nullptr, nullptr};
 
   static DeviceFst* create(const FrozenFst& f, int dev);
   // Blob already in device memory on `dev` (e.g. after an RCCL broadcast).
@@ -118,6 +144,21 @@ struct LaunchStats {
   uint32_t engine = 0;
   uint32_t grid = 0;
 };
+
+// ---- pull tier (eager_pull.hip, kernels/eager_pull.hpp) ----
+struct EagerLaunch;
+// Window rows of the pull tier: W = 64 * kPullRows target states per layer.
+constexpr int kPullRows = 5;
+constexpr uint32_t kPullW = 64 * kPullRows;
+// Builds d->rev from the host copy when the rhs qualifies (sets d->pull_ok); false only
+// on a device allocation failure.
+bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f);
+void free_reverse_mirror(DeviceFst* d);
+// Resident waves per CU of the pull kernel for this rhs.
+int pull_waves_per_cu(const DeviceFst& rhs);
+hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
+                             unsigned int* next_item, const EagerLaunch& lp,
+                             const BatchOutDev& out, uint32_t grid, hipStream_t stream);
 
 // Per-device engine state: persistent workspaces (grown on demand) and a lock,
 // since the C ABI may be called from several threads.

@@ -1,0 +1,189 @@
+// eager_pull.hip -- the pull tier's reverse arc mirror (host build + upload) and launches.
+// Kernel and proof: kernels/eager_pull.hpp.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "device_engine.hpp"
+#include "host_fst.hpp"
+#include "kernels/eager_pull.hpp"
+
+namespace fstamd {
+
+namespace {
+constexpr int kPullWaves = 4;
+
+template <int KP>
+const void* pull_kernel_ptr() {
+  return (const void*)eager_pull_kernel<kPullRows, KP, kPullWaves>;
+}
+const void* pull_kernel_for(uint32_t kp) {
+  switch (kp) {
+    case 4: return pull_kernel_ptr<4>();
+    case 5: return pull_kernel_ptr<5>();
+    default: return pull_kernel_ptr<8>();
+  }
+}
+}  // namespace
+
+void free_reverse_mirror(DeviceFst* d) {
+  for (void*& p : d->rev_bufs) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+  }
+  d->rev = RevView{};
+  d->pull_ok = false;
+}
+
+bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
+  d->pull_ok = false;
+  if (std::getenv("FSTAMD_NO_PULL")) return true;
+  // the pull tier's contract: layered lattices (no input epsilon) and the push tiers'
+  // weights (>= +0, no NaN)
+  if (d->has_eps || !d->nonneg || d->nan) return true;
+  const uint32_t ns = f.num_states(), na = f.header().num_arcs;
+  if (ns == 0 || ns >= kSpanMixed) return true;
+  const StateEntry* se = f.states();
+  const PackedArc* pa = f.arcs();
+
+  // j of every arc: its position in the source's run of equal ilabels (spans are sorted
+  // by ilabel, fst.zig:258-265).  A run longer than 8 does not fit the key's 3 bits.
+  std::vector<uint8_t> jpos(na);
+  std::vector<uint32_t> src(na);
+  std::vector<uint32_t> indeg(ns + 1, 0);
+  for (uint32_t s = 0; s < ns; ++s) {
+    uint32_t run = se[s].arc_offset;
+    for (uint32_t a = se[s].arc_offset; a < se[s].arc_offset + se[s].num_arcs; ++a) {
+      if (a > se[s].arc_offset && pa[a].ilabel != pa[a - 1].ilabel) run = a;
+      if (a - run >= 8) return true;
+      jpos[a] = (uint8_t)(a - run);
+      src[a] = s;
+      ++indeg[pa[a].nextstate];
+    }
+  }
+  // in-arcs by target (counting sort), then by (ilabel, source, j) within a target
+  std::vector<uint32_t> ioff(ns + 1, 0);
+  for (uint32_t t = 0; t < ns; ++t) ioff[t + 1] = ioff[t] + indeg[t];
+  std::vector<uint32_t> in(na), fill(ioff.begin(), ioff.end() - 1);
+  for (uint32_t a = 0; a < na; ++a) in[fill[pa[a].nextstate]++] = a;
+  for (uint32_t t = 0; t < ns; ++t)
+    std::sort(in.begin() + ioff[t], in.begin() + ioff[t + 1], [&](uint32_t x, uint32_t y) {
+      if (pa[x].ilabel != pa[y].ilabel) return pa[x].ilabel < pa[y].ilabel;
+      if (src[x] != src[y]) return src[x] < src[y];
+      return jpos[x] < jpos[y];
+    });
+  // groups: runs of equal ilabel within a target's in-arcs
+  struct Group { uint32_t t, label, first, n; };
+  std::vector<Group> groups;
+  for (uint32_t t = 0; t < ns; ++t)
+    for (uint32_t i = ioff[t]; i < ioff[t + 1];) {
+      uint32_t e = i + 1;
+      while (e < ioff[t + 1] && pa[in[e]].ilabel == pa[in[i]].ilabel) ++e;
+      groups.push_back(Group{t, pa[in[i]].ilabel, i, e - i});
+      i = e;
+    }
+  // block size: the fewest record slots, a further block of a group counted double (the
+  // kernel visits it in a separate loop)
+  uint32_t kp = 8;
+  uint64_t best_cost = ~0ull;
+  for (uint32_t cand : {4u, 5u, 8u}) {
+    uint64_t cost = 0;
+    for (const Group& g : groups) {
+      const uint64_t nb = (g.n + cand - 1) / cand;
+      cost += nb * cand + (nb - 1) * cand;
+    }
+    if (cost < best_cost) {
+      best_cost = cost;
+      kp = cand;
+    }
+  }
+  uint64_t nblocks = 1;  // block 0: the null block
+  for (const Group& g : groups) nblocks += (g.n + kp - 1) / kp;
+  if (nblocks * kp * sizeof(RevRec) > (4ull << 30) || nblocks * kp >= 0xFFFFFFFFull) return true;
+
+  std::vector<RevRec> rrec(nblocks * kp, RevRec{kNoState, 0u, 0.0});
+  std::vector<uint32_t> rolab(nblocks * kp, 0u);
+  std::vector<uint4> rspan(ns, make_uint4(0u, 0u, kSpanNone, 0u));
+  std::vector<uint4> gtab;
+  uint32_t max_groups = 1;
+  uint64_t blk = 1;
+  for (size_t gi = 0; gi < groups.size();) {
+    const uint32_t t = groups[gi].t;
+    size_t ge = gi;
+    while (ge < groups.size() && groups[ge].t == t) ++ge;
+    const uint32_t ng = (uint32_t)(ge - gi);
+    // one group whose label is an ordinary one: found from rspan alone; several (or a
+    // label that collides with the kSpan* markers): binary search over gtab
+    const bool single = ng == 1 && groups[gi].label < kSpanMixed;
+    if (!single) {
+      rspan[t] = make_uint4((uint32_t)gtab.size(), ng, kSpanMixed, 0u);
+      max_groups = std::max(max_groups, ng);
+    }
+    for (size_t g = gi; g < ge; ++g) {
+      const Group& G = groups[g];
+      const uint32_t nb = (G.n + kp - 1) / kp;
+      if (single) rspan[t] = make_uint4((uint32_t)blk, nb, G.label, 0u);
+      else gtab.push_back(make_uint4(G.label, (uint32_t)blk, nb, 0u));
+      for (uint32_t r = 0; r < G.n; ++r) {
+        const uint32_t a = in[G.first + r];
+        const uint64_t slot = blk * kp + r;
+        const uint32_t m = r % kp;
+        rrec[slot] = RevRec{src[a], ((uint32_t)jpos[a] << 13) | (m << 9), pa[a].weight};
+        rolab[slot] = pa[a].olabel;
+      }
+      blk += nb;
+    }
+    gi = ge;
+  }
+  uint32_t gsearch = 1;
+  while ((1u << (gsearch - 1)) < max_groups + 1) ++gsearch;
+
+  auto up = [&](int i, const void* src_p, size_t bytes) -> bool {
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(&d->rev_bufs[i], bytes) != hipSuccess) return false;
+    return hipMemcpy(d->rev_bufs[i], src_p, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+  if (gtab.empty()) gtab.push_back(zero4);
+  if (!up(0, rspan.data(), rspan.size() * sizeof(uint4)) ||
+      !up(1, gtab.data(), gtab.size() * sizeof(uint4)) ||
+      !up(2, rrec.data(), rrec.size() * sizeof(RevRec)) ||
+      !up(3, rolab.data(), rolab.size() * sizeof(uint32_t))) {
+    free_reverse_mirror(d);
+    return false;
+  }
+  d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
+                   (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch};
+  d->pull_ok = true;
+  return true;
+}
+
+int pull_waves_per_cu(const DeviceFst& rhs) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pull_kernel_for(rhs.rev.kp), 64, 0) !=
+      hipSuccess)
+    occ = 1;
+  return std::max(occ, 1);
+}
+
+hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
+                             unsigned int* next_item, const EagerLaunch& lp,
+                             const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
+  switch (rhs.rev.kp) {
+    case 4:
+      eager_pull_kernel<kPullRows, 4, kPullWaves>
+          <<<grid, 64, 0, stream>>>(rhs.view, rhs.rev, in, n_best, next_item, lp, out);
+      break;
+    case 5:
+      eager_pull_kernel<kPullRows, 5, kPullWaves>
+          <<<grid, 64, 0, stream>>>(rhs.view, rhs.rev, in, n_best, next_item, lp, out);
+      break;
+    default:
+      eager_pull_kernel<kPullRows, 8, kPullWaves>
+          <<<grid, 64, 0, stream>>>(rhs.view, rhs.rev, in, n_best, next_item, lp, out);
+      break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fstamd

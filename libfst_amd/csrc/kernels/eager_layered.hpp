@@ -768,7 +768,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
 }
 
 // Appends every string whose status is `code` to a device list (retry tier input).
-__global__ void collect_status_kernel(const int32_t* status, uint32_t num, int32_t code,
+[[maybe_unused]] static __global__ void collect_status_kernel(const int32_t* status, uint32_t num, int32_t code,
                                       uint32_t* list, uint32_t* count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < num && status[i] == code) list[atomicAdd(count, 1u)] = i;

@@ -1,0 +1,424 @@
+// eager_pull.hpp -- eager compose + shortestPath on layered lattices, one wavefront per
+// string, PULL formulation (gfx950 / CDNA4).  Tier P of the eager engine: it runs first
+// when the rhs has a reverse mirror (DeviceFst::rev) and hands the strings it cannot hold
+// to the push tiers (A0 eager_window.hpp, then A, B, C) through a device-side list.
+//
+// Same results as the push tiers (compose.zig:64-195 + shortest-path.zig:64-136, proof
+// in eager_layered.hpp / DESIGN.md §4.1): with no epsilon move every lattice arc goes
+// from layer k to layer k+1, and
+//   * the tuples of layer k+1 are numbered by their first candidate in the order
+//     (source id, position of the arc in the source's arcsByIlabel run) -- compose.zig's
+//     FIFO discovery order;
+//   * d(t) = min over candidates of d(s) + w (weights >= +0: Dijkstra's distance);
+//   * back(t) = the tight candidate with the smallest (source id, arc position) -- the
+//     tie rule of shortest-path.zig:74-84 applied by every relaxation;
+//   * best final = lexmin (d + final, id) over the last layer (shortest-path.zig:88-104).
+//
+// What differs is who does the work.  The push tiers give each lane SOURCE tuples and
+// merge candidates per target with LDS atomics (first index, min distance, then a second
+// pass for the tight back-pointer).  Here each lane owns TARGET states of the layer's
+// window [tmin', tmin' + wn) and pulls their in-arcs from the reverse mirror: one 16-B
+// record per in-arc (source, arc position j, weight) and one LDS read of the source's
+// cell (distance, rank).  The merge is then private to the lane:
+//   pk    = rank(s) << 16 | j << 13 | m << 9 | source slot   (order = candidate order)
+//   first = min pk                      -> the target exists iff first is a real candidate
+//   d     = min (d(s) + w)
+//   back  = min pk over the in-arcs with d(s) + w == d
+// No atomics, no per-target table, no second pass over LDS.  Ids (ranks) of layer k+1
+// come from a bitmap over the first keys (rank << 3 | j < 8 W): one LDS OR per target,
+// a popcount prefix over <= 40 words (DPP scan), one read per target.
+//
+// A slot with no tuple holds {+inf, kPullAbsent}: its candidates have distance +inf and
+// a key above every real one, so they never win -- the merge needs no validity selects.
+// Slots outside the current layer's window (and the null block's padding records, whose
+// source is kNoState) are clamped to slot W, which never holds a tuple.
+//
+// The back record of a tuple is {reverse record of its back arc, slab position of its
+// source}: the batched backtrace walks one dependent 8-B load per arc.
+#pragma once
+
+#include "device_common.hpp"
+#include "eager_layered.hpp"  // EagerLaunch, write_status
+#include "eager_wave.hpp"     // wave_lds_sync, wave_pick_best
+#include "eager_window.hpp"   // ChaseJob, kChaseBatch
+
+namespace fstamd {
+
+constexpr uint32_t kPullAbsent = 0xFFFF0000u;  // rank word of a slot that holds no tuple
+
+struct PullCell {
+  double d;         // distance of the slot's tuple (+inf: no tuple)
+  uint32_t rank16;  // rank << 16 (kPullAbsent: no tuple)
+  uint32_t pad;
+};
+
+template <int W>
+struct PullLds {
+  static constexpr int kWords = W * 8 / 64;  // first keys rank << 3 | j < 8 W
+  PullCell cell[W + 1];                      // slot W never holds a tuple
+  unsigned long long bits[kWords];
+  uint4 pre[kWords];                         // {prefix popcount, 0, word lo, word hi}
+  unsigned long long best;
+  uint32_t bestp;
+  ChaseJob job[kChaseBatch];
+};
+
+// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8, row_bcast 15/31);
+// every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+// One in-arc record against the current layer's cells: its candidate key and distance.
+__device__ __forceinline__ void pull_candidate(const PullCell* cell, const RevRec& r,
+                                               uint32_t tmin, uint32_t W, uint32_t& pk,
+                                               double& nd) {
+  const uint32_t idx = min(r.src - tmin, W);  // outside the window (or padding): slot W
+  const PullCell c = cell[idx];
+  pk = c.rank16 | r.y | idx;
+  nd = c.d + r.weight;  // times(d, times(One, w)) for w >= +0 (compose.zig:104,
+                        // shortest-path.zig:72); +inf stays +inf
+}
+
+template <int EW, int KP, int WAVES_PER_EU>
+__global__ void __launch_bounds__(64, WAVES_PER_EU)
+eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
+                  unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
+  constexpr int W = 64 * EW;
+  constexpr int kWords = PullLds<W>::kWords;
+  static_assert(KP <= 16, "m is 4 bits of the key");
+  static_assert(W < 512, "slots and ranks are 9 bits of the key");
+  __shared__ PullLds<W> S;
+  const uint32_t lane = threadIdx.x;
+  const double kInf = __builtin_huge_val();
+  uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
+  uint32_t njobs = 0;  // uniform: pending backtraces (slab j belongs to job j)
+
+  // lane r < njobs walks job r's path (shortest-path.zig:109-136): one 8-B back record
+  // per arc, {reverse record of the arc, slab position of the source}
+  auto chase_batch = [&]() {
+    wave_lds_sync();
+    uint32_t maxL = 0;
+    ChaseJob jb{};
+    if (lane < njobs) {
+      jb = S.job[lane];
+      maxL = jb.L;
+    }
+    maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
+    const uint2* sl = slabs + (size_t)lane * lp.back_cap;
+    uint32_t id = jb.id;
+    for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
+      if (lane < njobs && t < jb.L) {
+        const uint32_t k = jb.L - 1 - t;
+        const uint2 b = sl[FB(id, lp.back_cap, 60)];
+        out.out_il[jb.o + k] = in.labels[jb.off + k];
+        out.out_ol[jb.o + k] = rv.rolab[b.x];
+        out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+        id = b.y;
+      }
+    }
+    if (lane < njobs) {
+      out.status[jb.si] = kPathOk;
+      out.path_len[jb.si] = jb.L;
+      out.path_off[jb.si] = jb.o;
+      out.final_w[jb.si] = jb.fw;  // compose.zig:73: times(One, fw2) == fw2
+      if (out.work) {
+        out.work[2 * jb.si] = jb.tuples;
+        out.work[2 * jb.si + 1] = jb.relax;
+      }
+    }
+    njobs = 0;
+    wave_lds_sync();
+  };
+  const uint32_t num_items = __builtin_amdgcn_readfirstlane(
+      lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
+  const bool want_work = out.work != nullptr;
+
+#pragma unroll 1
+  for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
+    S.cell[i].d = kInf;
+    S.cell[i].rank16 = kPullAbsent;
+    S.cell[i].pad = 0;
+  }
+  if (lane < (uint32_t)kWords) S.bits[lane] = 0;
+  wave_lds_sync();
+  uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
+
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(next_item, 1u);
+    item = __builtin_amdgcn_readfirstlane(item);
+    if (item >= num_items) break;
+    const uint32_t si = __builtin_amdgcn_readfirstlane(lp.items ? lp.items[item] : item);
+    uint2* const back = slabs + (size_t)njobs * lp.back_cap;
+    const uint64_t off0 = in.offsets[si];
+    const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
+                         __builtin_amdgcn_readfirstlane((uint32_t)off0);
+    const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)(in.offsets[si + 1] - off));
+
+    if (rhs.start == kNoState || n_best != 1) {  // compose.zig:33-35, shortest-path.zig:21-24
+      if (lane == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+    // the watchdog is per string (a string that exceeds it reports INTERNAL)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+    // layer 0: the start tuple alone, slot 0 of a window at the start state
+#pragma unroll 1
+    for (uint32_t i = lane; i < wlast; i += 64) {
+      S.cell[i].d = kInf;
+      S.cell[i].rank16 = kPullAbsent;
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+      S.cell[0].d = w_one();
+      S.cell[0].rank16 = 0;
+    }
+    wave_lds_sync();
+    uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
+    uint32_t cmin = rhs.start, cmax = rhs.start;  // bounds of the current layer's states
+    uint32_t tuples = 1, relax = 0;
+    int32_t fail = kPathOk;
+    unsigned long long mykey = kMaxU64;  // this lane's best final candidate
+    uint32_t myp = kEmptyKey;
+    double myfw = 0.0;
+
+    uint32_t labs = 0;
+    for (uint32_t k = 0; k < L; ++k) {
+      if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+        fail = kPathInternal;
+        break;
+      }
+      if ((k & 63u) == 0) labs = k + lane < L ? in.labels[off + k + lane] : 0u;
+      const uint32_t lab = __builtin_amdgcn_readlane(labs, k & 63u);
+      if (lab == kEpsilon) {  // lhs epsilon output: not a layered lattice
+        fail = kPathUnsupported;
+        break;
+      }
+      // ---- window of the next layer: every target of a state in [cmin, cmax] lies in
+      // [cmin - jump_back, cmax + jump_fwd] (RhsView) ----
+      const uint32_t tn = cmin >= rhs.jump_back ? cmin - rhs.jump_back : 0u;
+      const uint64_t hi = min((uint64_t)cmax + rhs.jump_fwd, (uint64_t)rhs.num_states - 1);
+      const uint32_t nbase = base + wk;
+      if (hi - tn >= (uint64_t)W || (uint64_t)nbase + (hi - tn + 1) > lp.back_cap) {
+        fail = kPathOverflow;  // the push tiers take the string
+        break;
+      }
+      const uint32_t wn = (uint32_t)(hi - tn) + 1;
+      const uint32_t rows_n = (wn + 63) / 64;
+
+      // ---- (P1) pull: every target slot of the window merges its in-arcs ----
+      uint32_t fst[EW], bk[EW], bra[EW];
+      double bd[EW];
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        fst[e] = kEmptyKey;
+        bk[e] = kEmptyKey;
+        bra[e] = 0;
+        bd[e] = kInf;
+        if ((uint32_t)e >= rows_n) continue;  // uniform
+        const uint32_t i = (uint32_t)e * 64 + lane;
+        const bool inw = i < wn;
+        const uint32_t t = tn + i;
+        const uint4 rs = rv.rspan[inw ? t : 0u];
+        // (labels >= kSpanMixed always go through gtab: they collide with the markers)
+        const bool hit = rs.z == lab && lab < kSpanMixed;
+        uint32_t blk = hit ? rs.x : 0u;
+        uint32_t nb = hit ? rs.y : 0u;
+        if (__ballot(inw && rs.z == kSpanMixed)) {  // several in-labels: find the group
+          if (inw && rs.z == kSpanMixed) {
+            uint32_t a = rs.x, b = rs.x + rs.y;
+            for (uint32_t it = 0; it < rv.gsearch; ++it) {
+              if (a < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (rv.gtab[mid].x < lab) a = mid + 1;
+                else b = mid;
+              }
+            }
+            if (a < rs.x + rs.y) {
+              const uint4 g = rv.gtab[a];
+              if (g.x == lab) {
+                blk = g.y;
+                nb = g.z;
+              }
+            }
+          }
+        }
+        if (!inw) nb = 0;
+        const RevRec* R = rv.rrec + (size_t)(nb ? blk : 0u) * KP;
+        RevRec rr[KP];
+#pragma unroll
+        for (int m = 0; m < KP; ++m) rr[m] = R[m];
+        uint32_t pk[KP];
+        double nd[KP];
+        uint32_t f = kEmptyKey;
+        double b = kInf;
+#pragma unroll
+        for (int m = 0; m < KP; ++m) {
+          pull_candidate(S.cell, rr[m], tmin, (uint32_t)W, pk[m], nd[m]);
+          f = min(f, pk[m]);
+          b = fmin(b, nd[m]);
+        }
+        uint32_t c = kEmptyKey;
+#pragma unroll
+        for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
+        if (want_work) {
+#pragma unroll
+          for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(pk[m] < kPullAbsent));
+        }
+        uint32_t ra = (nb ? blk : 0u) * KP + ((c >> 9) & 15u);
+        // groups of more than KP in-arcs: the further blocks, rare (a hub state)
+        if (__ballot(nb > 1)) {
+          for (uint32_t x = 1;; ++x) {
+            const bool act = nb > x;
+            if (!__ballot(act)) break;
+            const RevRec* R2 = rv.rrec + (size_t)(act ? blk + x : 0u) * KP;
+#pragma unroll
+            for (int m = 0; m < KP; ++m) {
+              uint32_t p2;
+              double n2;
+              pull_candidate(S.cell, R2[m], tmin, (uint32_t)W, p2, n2);
+              f = min(f, p2);
+              if (n2 < b || (n2 == b && p2 < c)) {
+                b = n2;
+                c = p2;
+                ra = (act ? blk + x : 0u) * KP + m;
+              }
+              if (want_work) relax += (uint32_t)__popcll(__ballot(p2 < kPullAbsent));
+            }
+          }
+        }
+        fst[e] = f;
+        bd[e] = b;
+        bk[e] = c;
+        bra[e] = ra;
+        if (f < kPullAbsent) {  // a tuple: mark its first key (rank << 3 | j)
+          const uint32_t key = f >> 13;
+          atomicOr(&S.bits[key >> 6], 1ull << (key & 63u));
+        }
+      }
+      wave_lds_sync();
+
+      // ---- (P2) ranks: popcount prefix over the first-key bitmap ----
+      const uint32_t nw = (n_cur * 8 + 63) / 64;  // keys < 8 * n_cur
+      unsigned long long word = 0;
+      if (lane < nw) word = S.bits[lane];
+      const uint32_t pc = (uint32_t)__popcll(word);
+      const uint32_t inc = wave_incl_scan_dpp(pc);
+      const uint32_t n_next = __builtin_amdgcn_readlane(inc, 63);
+      if (lane < nw) {
+        S.pre[lane] = make_uint4(inc - pc, 0u, (uint32_t)word, (uint32_t)(word >> 32));
+        S.bits[lane] = 0;
+      }
+      wave_lds_sync();
+      if (n_next == 0) {  // no candidate: the lattice dies here, no final is reachable
+        n_cur = 0;
+        break;
+      }
+
+      // ---- (P3) the next layer's cells (rewriting every row the current one used), back
+      // records, and on the last layer the final candidates ----
+      const bool last = k + 1 == L;
+      const uint32_t rows_w = max(rows_n, (wk + 63) / 64);
+      uint32_t lo_slot = kEmptyKey, hi_slot = 0;  // uniform: present slots of the next layer
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        if ((uint32_t)e >= rows_w) continue;  // uniform
+        const uint32_t i = (uint32_t)e * 64 + lane;
+        const bool pres = (uint32_t)e < rows_n && fst[e] < kPullAbsent;
+        uint32_t rank = 0;
+        if ((uint32_t)e < rows_n) {
+          const uint32_t key = pres ? fst[e] >> 13 : 0u;
+          const uint4 p = S.pre[key >> 6];
+          const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
+          rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
+        }
+        PullCell nc;
+        nc.d = pres ? bd[e] : kInf;
+        nc.rank16 = pres ? rank << 16 : kPullAbsent;
+        nc.pad = 0;
+        S.cell[i] = nc;
+        const unsigned long long pm = __ballot(pres);
+        if (pm) {
+          lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
+          hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
+        }
+        if (pres) {
+          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + (bk[e] & 511u));
+          if (last) {  // final candidates, lexmin (total, rank) within the lane
+            const uint32_t t = tn + i;
+            const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
+            if (!w_is_zero(bd[e]) && !w_is_zero(fw2)) {
+              const unsigned long long kk = okey(bd[e] + fw2);  // times(d, times(One, fw2))
+              const uint32_t pp = (rank << 9) | i;
+              if (kk < mykey || (kk == mykey && pp < myp)) {
+                mykey = kk;
+                myp = pp;
+                myfw = fw2;
+              }
+            }
+          }
+        }
+      }
+      tmin = tn;
+      base = nbase;
+      wk = wn;
+      n_cur = n_next;
+      tuples += n_next;
+      cmin = tn + lo_slot;
+      cmax = tn + hi_slot;
+      wave_lds_sync();
+    }
+    wlast = wk;
+
+    if (fail != kPathOk) {
+      if (lane == 0) write_status(out, si, fail, tuples, relax);
+      continue;
+    }
+    if (L == 0 && lane == 0) {  // the start tuple is the whole lattice
+      const double fw2 = rhs.final_w[rhs.start];
+      if (!w_is_zero(fw2)) {
+        mykey = okey(w_one() + fw2);
+        myp = 0;
+        myfw = fw2;
+      }
+    }
+    uint32_t bp;
+    double fw2;
+    if (n_cur == 0 || !wave_pick_best(S.best, S.bestp, lane, mykey, myp, myfw, bp, fw2)) {
+      if (lane == 0) write_status(out, si, kPathEmpty, tuples, relax);
+      continue;
+    }
+    unsigned long long o = 0;
+    if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
+    o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((uint32_t)o);
+    if (o + L > out.arc_cap) {
+      if (lane == 0) write_status(out, si, kPathOutputFull, tuples, relax);
+      continue;
+    }
+    if (lane == 0) {
+      ChaseJob& j = S.job[njobs];
+      j.si = si;
+      j.L = L;
+      j.id = base + (bp & 511u);  // shortest-path.zig:109-136 starts at the best final
+      j.tuples = tuples;
+      j.relax = relax;
+      j.o = o;
+      j.off = off;
+      j.fw = fw2;
+    }
+    if (++njobs == (uint32_t)kChaseBatch) chase_batch();
+  }
+  if (njobs) chase_batch();
+}
+
+}  // namespace fstamd

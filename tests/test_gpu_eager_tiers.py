@@ -1,10 +1,10 @@
 """GPU parity of every tier of the eager layered chain (device_engine.hip run_chain).
 
-The chain is A0 (direct-mapped window, eager_window.hpp) -> A (hashed wave,
-eager_wave.hpp) -> B (256-thread LDS tables) -> C (HBM tables) -> general BFS; each tier
-takes the strings the previous one reports as OVERFLOW.  FSTAMD_EAGER_TIER1=wave starts
-the chain at A and =wg at B, so each tier is checked on its own as well as behind the
-others, against the oracle's compose + shortestPath (compose.zig:29-198,
+The chain is P (pull over the reverse mirror, eager_pull.hpp) -> A0 (direct-mapped
+window, eager_window.hpp) -> A (hashed wave, eager_wave.hpp) -> B (256-thread LDS tables)
+-> C (HBM tables) -> general BFS; each tier takes the strings the previous one reports as
+OVERFLOW.  FSTAMD_EAGER_TIER1=window starts the chain at A0, =wave at A and =wg at B, so
+each tier is checked on its own as well as behind the others, against the oracle's compose + shortestPath (compose.zig:29-198,
 shortest-path.zig:18-139), bit-exact.
 """
 import math
@@ -19,10 +19,10 @@ from test_gpu_parity import check, csr, load_blob, random_rhs
 pytestmark = pytest.mark.gpu
 
 EAGER = F.FST_SEM_EAGER
-STARTS = ["", "wave", "wg"]
+STARTS = ["", "window", "wave", "wg"]
 
 
-@pytest.fixture(params=STARTS, ids=["A0", "A", "B"])
+@pytest.fixture(params=STARTS, ids=["P", "A0", "A", "B"])
 def tier(request, monkeypatch):
     if request.param:
         monkeypatch.setenv("FSTAMD_EAGER_TIER1", request.param)
