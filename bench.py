@@ -31,11 +31,11 @@ from libfst_amd import fst as FF  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Measured HBM traffic of the metric kernel: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-# over this same command (scripts/profile_r01.sh), reduced by scripts/pmc_summary.py.
+# over this same command (scripts/profile_bench.sh), reduced by scripts/pmc_summary.py.
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
-EAGER_KERNEL = "eager_window_kernel"   # tier A0, takes every metric string
+EAGER_KERNEL = "eager_pull_kernel"     # tier P, takes every metric string
 LAZY_KERNEL = "lazy_layered_kernel"
 
 
@@ -102,19 +102,54 @@ class DeviceBatch:
         self.w = torch.empty(self.cap, dtype=torch.float64, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
         self.work = torch.empty(2 * B, dtype=torch.int32, device=dev)
+        # timed steps produce the results only; the per-string work counters (tuples,
+        # relaxations: instrumentation for the roofline's B_alg) come from one extra run
         self.desc = FF.FstDeviceBatch(
+            self.status.data_ptr(), self.plen.data_ptr(), self.poff.data_ptr(),
+            self.fin.data_ptr(), self.il.data_ptr(), self.ol.data_ptr(), self.w.data_ptr(),
+            self.cap, self.cursor.data_ptr(), 0)
+        self.desc_work = FF.FstDeviceBatch(
             self.status.data_ptr(), self.plen.data_ptr(), self.poff.data_ptr(),
             self.fin.data_ptr(), self.il.data_ptr(), self.ol.data_ptr(), self.w.data_ptr(),
             self.cap, self.cursor.data_ptr(), self.work.data_ptr())
 
-    def run(self, rhs, sem, dev_index, stream):
+    def run(self, rhs, sem, dev_index, stream, work=False):
         opts = FF.FstBatchOptions(dev_index, sem, 0)
         rc = F.lib().fst_device_compose_shortest_path(
             rhs.h, dev_ptr(self.labels), dev_ptr(self.offsets), self.num, self.max_len, 1,
-            C.byref(opts), C.byref(self.desc), C.c_void_p(stream))
+            C.byref(opts), C.byref(self.desc_work if work else self.desc), C.c_void_p(stream))
         if rc != FF.FST_OK:
             raise RuntimeError(f"fst_device_compose_shortest_path failed: {rc}")
         return F.last_launch_stats()
+
+
+def check_sample(batch, blob_bytes, sem, n=256):
+    """Bit-compares the first n strings of the last run with the oracle (compose.zig +
+    shortest-path.zig, or compose-shortest-path.zig): status, path labels, arc weights and
+    final weight, f64 bit patterns.  The oracle is the checker here, never the thing timed."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi as O  # checker / CPU baseline only
+
+    n = min(n, batch.num)
+    offs = batch.offsets[: n + 1].cpu().numpy().astype(np.uint64)
+    labels = batch.labels[: int(offs[-1])].cpu().numpy().astype(np.uint32)
+    ref = O.batch_run(blob_bytes, labels, offs, 1 if sem == F.FST_SEM_EAGER else 0, 1)
+    status = batch.status[:n].cpu().numpy()
+    exp = np.where(ref.empty == 1, F.FST_PATH_EMPTY, F.FST_PATH_OK)
+    assert np.all(ref.status == O.OR_OK) and np.array_equal(status, exp), "status mismatch"
+    plen = batch.plen[:n].cpu().numpy().astype(np.int64)
+    poff = batch.poff[:n].cpu().numpy().astype(np.int64)
+    fin = batch.fin[:n].cpu().numpy()
+    il, ol, w = batch.il.cpu().numpy(), batch.ol.cpu().numpy(), batch.w.cpu().numpy()
+    for i in np.nonzero(exp == F.FST_PATH_OK)[0]:
+        a, b = int(ref.offsets[i]), int(ref.offsets[i + 1])
+        assert plen[i] == b - a, ("path length", i)
+        g = slice(int(poff[i]), int(poff[i]) + b - a)
+        assert np.array_equal(il[g].astype(np.uint32), ref.ilabels[a:b]), ("ilabels", i)
+        assert np.array_equal(ol[g].astype(np.uint32), ref.olabels[a:b]), ("olabels", i)
+        assert np.array_equal(w[g].view(np.uint64), ref.weights[a:b].view(np.uint64)), ("w", i)
+        assert fin[i:i + 1].view(np.uint64)[0] == ref.finals[i:i + 1].view(np.uint64)[0], i
+    return int(n)
 
 
 def b_alg_bytes(work, lengths, plen):
@@ -202,14 +237,19 @@ def main():
     batch = DeviceBatch(lengths, lambda t: torch.ones(t, dtype=torch.int32), dev)
     el, kms, st = timed(batch, rhs, sem, local, args.steps, args.warmup, world)
 
-    # correctness spot check of the last step (every metric string has one answer)
+    # correctness of the last timed step: every metric string has one answer, and a fixed
+    # sample is bit-compared with the oracle
     status = batch.status.cpu().numpy()
     plen = batch.plen.cpu().numpy().astype(np.int64)
-    work = batch.work.cpu().numpy().astype(np.int64)
     assert np.all(status == F.FST_PATH_OK), np.unique(status, return_counts=True)
     assert np.all(plen == L)
-    ol = batch.ol[: min(L * 8, batch.cap)].cpu().numpy()
-    assert np.all(ol[: L] == 1)
+    blob_check = blob_host if blob_host is not None else D.blob_bytes(
+        F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, args.transducer_len, args.branches))
+    checked = check_sample(batch, blob_check, sem)
+    # one untimed run with the per-string work counters (B_alg of the roofline)
+    batch.run(rhs, sem, local, torch.cuda.current_stream().cuda_stream, work=True)
+    torch.cuda.synchronize()
+    work = batch.work.cpu().numpy().astype(np.int64)
 
     total_strings = args.batch * args.steps * world
     value = total_strings / el
@@ -230,7 +270,8 @@ def main():
         vel, vk, _ = timed(vb, rhs, sem, local, args.steps, args.warmup, world)
         extra["varied"] = {"value": args.batch * args.steps * world / vel,
                            "kernel_ms": float(np.mean(vk)),
-                           "lengths": "uniform 1..%d, ~10%% strings with a dead label" % L}
+                           "lengths": "uniform 1..%d, ~10%% strings with a dead label" % L,
+                           "checked_vs_oracle": check_sample(vb, blob_check, sem)}
         del vb
     if args.lazy_batch and sem == F.FST_SEM_EAGER:
         lb = DeviceBatch(np.full(args.lazy_batch, L, np.int64),
@@ -240,6 +281,7 @@ def main():
         assert np.all(ls == F.FST_PATH_OK)
         extra["lazy"] = {"value": args.lazy_batch * world / lel, "kernel_ms": float(np.mean(lk)),
                          "batch": args.lazy_batch,
+                         "checked_vs_oracle": check_sample(lb, blob_check, F.FST_SEM_LAZY),
                          "note": "fst_compose_frozen_shortest_path semantics (lazy_layered_kernel rounds engine)"}
 
     if rank == 0:
@@ -281,6 +323,7 @@ def main():
                                  "rhs is L2/LDS-resident, so this can exceed the HBM peak; "
                                  "hbm_traffic_* is the PMC-measured DRAM traffic"},
             "cpu_baseline": cpu,
+            "checked_vs_oracle": checked,
         }
         line.update(extra)
         print(json.dumps(line), flush=True)

@@ -1,6 +1,7 @@
 // eager_pull.hip -- the pull tier's reverse arc mirror (host build + upload) and launches.
 // Kernel and proof: kernels/eager_pull.hpp.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -11,17 +12,32 @@
 namespace fstamd {
 
 namespace {
-constexpr int kPullWaves = 4;
+// Waves per SIMD the compiler targets: 5 fit spill-free with blocks of <= 5 records (the
+// metric: 5 waves 20.3 M strings/s, 4 waves 18.5 M, 6 waves 19.8 M with spills);
+// 8-record blocks need 4.  FSTAMD_PULL_WAVES=4|5|6 overrides (occupancy experiments).
+int pull_waves_knob(uint32_t kp) {
+  const char* w = std::getenv("FSTAMD_PULL_WAVES");
+  if (w && (w[0] == '4' || w[0] == '5' || w[0] == '6') && w[1] == 0) return w[0] - '0';
+  return kp <= 5 ? 5 : 4;
+}
 
-template <int KP>
+template <int KP, int WV>
 const void* pull_kernel_ptr() {
-  return (const void*)eager_pull_kernel<kPullRows, KP, kPullWaves>;
+  return (const void*)eager_pull_kernel<kPullRows, KP, WV>;
+}
+template <int WV>
+const void* pull_kernel_kp(uint32_t kp) {
+  switch (kp) {
+    case 4: return pull_kernel_ptr<4, WV>();
+    case 5: return pull_kernel_ptr<5, WV>();
+    default: return pull_kernel_ptr<8, WV>();
+  }
 }
 const void* pull_kernel_for(uint32_t kp) {
-  switch (kp) {
-    case 4: return pull_kernel_ptr<4>();
-    case 5: return pull_kernel_ptr<5>();
-    default: return pull_kernel_ptr<8>();
+  switch (pull_waves_knob(kp)) {
+    case 5: return pull_kernel_kp<5>(kp);
+    case 6: return pull_kernel_kp<6>(kp);
+    default: return pull_kernel_kp<4>(kp);
   }
 }
 }  // namespace
@@ -42,7 +58,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   // weights (>= +0, no NaN)
   if (d->has_eps || !d->nonneg || d->nan) return true;
   const uint32_t ns = f.num_states(), na = f.header().num_arcs;
-  if (ns == 0 || ns >= kSpanMixed) return true;
+  if (ns == 0 || ns >= (1u << 27)) return true;  // records hold 16 * state
   const StateEntry* se = f.states();
   const PackedArc* pa = f.arcs();
 
@@ -101,7 +117,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   for (const Group& g : groups) nblocks += (g.n + kp - 1) / kp;
   if (nblocks * kp * sizeof(RevRec) > (4ull << 30) || nblocks * kp >= 0xFFFFFFFFull) return true;
 
-  std::vector<RevRec> rrec(nblocks * kp, RevRec{kNoState, 0u, 0.0});
+  std::vector<RevRec> rrec(nblocks * kp, RevRec{0xFFFFFFF0u, 0u, 0.0});  // padding
   std::vector<uint32_t> rolab(nblocks * kp, 0u);
   std::vector<uint4> rspan(ns, make_uint4(0u, 0u, kSpanNone, 0u));
   std::vector<uint4> gtab;
@@ -128,7 +144,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
         const uint32_t a = in[G.first + r];
         const uint64_t slot = blk * kp + r;
         const uint32_t m = r % kp;
-        rrec[slot] = RevRec{src[a], ((uint32_t)jpos[a] << 13) | (m << 9), pa[a].weight};
+        rrec[slot] = RevRec{src[a] << 4, ((uint32_t)jpos[a] << 17) | (m << 13), pa[a].weight};
         rolab[slot] = pa[a].olabel;
       }
       blk += nb;
@@ -169,21 +185,9 @@ int pull_waves_per_cu(const DeviceFst& rhs) {
 hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
                              unsigned int* next_item, const EagerLaunch& lp,
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
-  switch (rhs.rev.kp) {
-    case 4:
-      eager_pull_kernel<kPullRows, 4, kPullWaves>
-          <<<grid, 64, 0, stream>>>(rhs.view, rhs.rev, in, n_best, next_item, lp, out);
-      break;
-    case 5:
-      eager_pull_kernel<kPullRows, 5, kPullWaves>
-          <<<grid, 64, 0, stream>>>(rhs.view, rhs.rev, in, n_best, next_item, lp, out);
-      break;
-    default:
-      eager_pull_kernel<kPullRows, 8, kPullWaves>
-          <<<grid, 64, 0, stream>>>(rhs.view, rhs.rev, in, n_best, next_item, lp, out);
-      break;
-  }
-  return hipGetLastError();
+  void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
+                  (void*)&next_item, (void*)&lp, (void*)&out};
+  return hipLaunchKernel(pull_kernel_for(rhs.rev.kp), dim3(grid), dim3(64), args, 0, stream);
 }
 
 }  // namespace fstamd

@@ -20,7 +20,7 @@
 // window [tmin', tmin' + wn) and pulls their in-arcs from the reverse mirror: one 16-B
 // record per in-arc (source, arc position j, weight) and one LDS read of the source's
 // cell (distance, rank).  The merge is then private to the lane:
-//   pk    = rank(s) << 16 | j << 13 | m << 9 | source slot   (order = candidate order)
+//   pk    = rank(s) << 20 | j << 17 | m << 13 | 16 * source slot  (order = candidate order)
 //   first = min pk                      -> the target exists iff first is a real candidate
 //   d     = min (d(s) + w)
 //   back  = min pk over the in-arcs with d(s) + w == d
@@ -30,8 +30,9 @@
 //
 // A slot with no tuple holds {+inf, kPullAbsent}: its candidates have distance +inf and
 // a key above every real one, so they never win -- the merge needs no validity selects.
-// Slots outside the current layer's window (and the null block's padding records, whose
-// source is kNoState) are clamped to slot W, which never holds a tuple.
+// Reverse records hold 16 * source state, so the source's cell offset is one subtraction:
+// slots outside the current layer's window (and the null block's padding records) are
+// clamped to slot W, which never holds a tuple.
 //
 // The back record of a tuple is {reverse record of its back arc, slab position of its
 // source}: the batched backtrace walks one dependent 8-B load per arc.
@@ -46,9 +47,9 @@ namespace fstamd {
 
 constexpr uint32_t kPullAbsent = 0xFFFF0000u;  // rank word of a slot that holds no tuple
 
-struct PullCell {
+struct alignas(16) PullCell {
   double d;         // distance of the slot's tuple (+inf: no tuple)
-  uint32_t rank16;  // rank << 16 (kPullAbsent: no tuple)
+  uint32_t rank20;  // rank << 20 (kPullAbsent: no tuple)
   uint32_t pad;
 };
 
@@ -77,13 +78,49 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
 
 // One in-arc record against the current layer's cells: its candidate key and distance.
 __device__ __forceinline__ void pull_candidate(const PullCell* cell, const RevRec& r,
-                                               uint32_t tmin, uint32_t W, uint32_t& pk,
+                                               uint32_t tmin16, uint32_t W16, uint32_t& pk,
                                                double& nd) {
-  const uint32_t idx = min(r.src - tmin, W);  // outside the window (or padding): slot W
-  const PullCell c = cell[idx];
-  pk = c.rank16 | r.y | idx;
-  nd = c.d + r.weight;  // times(d, times(One, w)) for w >= +0 (compose.zig:104,
-                        // shortest-path.zig:72); +inf stays +inf
+  // byte offset of the source's cell; outside the window (or padding): slot W
+  const uint32_t off = min(r.src - tmin16, W16);
+  const uint4 c = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(cell) + off);
+  // (folding the pad c.w into the OR makes the compiler read the cell with one
+  // ds_read2_b64 instead of b64 + b32, but costs a register and spills: 19.1 vs 20.1 M
+  // strings/s)
+  pk = c.z | r.y | off;
+  // times(d, times(One, w)) for w >= +0 (compose.zig:104, shortest-path.zig:72); +inf
+  // stays +inf
+  nd = __longlong_as_double((long long)(((unsigned long long)c.y << 32) | c.x)) + r.weight;
+}
+
+// The in-arc group of target t for input label `lab`: its first block and block count
+// (nb = 0: no in-arc with that label, or t outside the window).
+__device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, bool inw, uint32_t t,
+                                           uint32_t& blk, uint32_t& nb) {
+  const uint4 rs = rv.rspan[inw ? t : 0u];
+  // (labels >= kSpanMixed always go through gtab: they collide with the markers)
+  const bool hit = rs.z == lab && lab < kSpanMixed;
+  blk = hit ? rs.x : 0u;
+  nb = hit ? rs.y : 0u;
+  if (__ballot(inw && rs.z == kSpanMixed)) {  // several in-labels: binary search of gtab
+    if (inw && rs.z == kSpanMixed) {
+      uint32_t a = rs.x, b = rs.x + rs.y;
+      for (uint32_t it = 0; it < rv.gsearch; ++it) {
+        if (a < b) {
+          const uint32_t mid = (a + b) >> 1;
+          if (rv.gtab[mid].x < lab) a = mid + 1;
+          else b = mid;
+        }
+      }
+      if (a < rs.x + rs.y) {
+        const uint4 g = rv.gtab[a];
+        if (g.x == lab) {
+          blk = g.y;
+          nb = g.z;
+        }
+      }
+    }
+  }
+  if (!inw) nb = 0;
 }
 
 template <int EW, int KP, int WAVES_PER_EU>
@@ -93,7 +130,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   constexpr int W = 64 * EW;
   constexpr int kWords = PullLds<W>::kWords;
   static_assert(KP <= 16, "m is 4 bits of the key");
-  static_assert(W < 512, "slots and ranks are 9 bits of the key");
+  static_assert(W < 512, "16 * slot is 13 bits of the key, ranks 9 bits");
   __shared__ PullLds<W> S;
   const uint32_t lane = threadIdx.x;
   const double kInf = __builtin_huge_val();
@@ -143,7 +180,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
     S.cell[i].d = kInf;
-    S.cell[i].rank16 = kPullAbsent;
+    S.cell[i].rank20 = kPullAbsent;
     S.cell[i].pad = 0;
   }
   if (lane < (uint32_t)kWords) S.bits[lane] = 0;
@@ -175,12 +212,12 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll 1
     for (uint32_t i = lane; i < wlast; i += 64) {
       S.cell[i].d = kInf;
-      S.cell[i].rank16 = kPullAbsent;
+      S.cell[i].rank20 = kPullAbsent;
     }
     wave_lds_sync();
     if (lane == 0) {
       S.cell[0].d = w_one();
-      S.cell[0].rank16 = 0;
+      S.cell[0].rank20 = 0;
     }
     wave_lds_sync();
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
@@ -225,34 +262,10 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         bra[e] = 0;
         bd[e] = kInf;
         if ((uint32_t)e >= rows_n) continue;  // uniform
+        // (looking up every row's group before the row loop measured no faster)
         const uint32_t i = (uint32_t)e * 64 + lane;
-        const bool inw = i < wn;
-        const uint32_t t = tn + i;
-        const uint4 rs = rv.rspan[inw ? t : 0u];
-        // (labels >= kSpanMixed always go through gtab: they collide with the markers)
-        const bool hit = rs.z == lab && lab < kSpanMixed;
-        uint32_t blk = hit ? rs.x : 0u;
-        uint32_t nb = hit ? rs.y : 0u;
-        if (__ballot(inw && rs.z == kSpanMixed)) {  // several in-labels: find the group
-          if (inw && rs.z == kSpanMixed) {
-            uint32_t a = rs.x, b = rs.x + rs.y;
-            for (uint32_t it = 0; it < rv.gsearch; ++it) {
-              if (a < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (rv.gtab[mid].x < lab) a = mid + 1;
-                else b = mid;
-              }
-            }
-            if (a < rs.x + rs.y) {
-              const uint4 g = rv.gtab[a];
-              if (g.x == lab) {
-                blk = g.y;
-                nb = g.z;
-              }
-            }
-          }
-        }
-        if (!inw) nb = 0;
+        uint32_t blk, nb;
+        pull_group(rv, lab, i < wn, tn + i, blk, nb);
         const RevRec* R = rv.rrec + (size_t)(nb ? blk : 0u) * KP;
         RevRec rr[KP];
 #pragma unroll
@@ -263,7 +276,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         double b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
-          pull_candidate(S.cell, rr[m], tmin, (uint32_t)W, pk[m], nd[m]);
+          pull_candidate(S.cell, rr[m], tmin << 4, 16u * W, pk[m], nd[m]);
           f = min(f, pk[m]);
           b = fmin(b, nd[m]);
         }
@@ -274,7 +287,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(pk[m] < kPullAbsent));
         }
-        uint32_t ra = (nb ? blk : 0u) * KP + ((c >> 9) & 15u);
+        uint32_t ra = (nb ? blk : 0u) * KP + ((c >> 13) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
           for (uint32_t x = 1;; ++x) {
@@ -285,7 +298,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             for (int m = 0; m < KP; ++m) {
               uint32_t p2;
               double n2;
-              pull_candidate(S.cell, R2[m], tmin, (uint32_t)W, p2, n2);
+              pull_candidate(S.cell, R2[m], tmin << 4, 16u * W, p2, n2);
               f = min(f, p2);
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
@@ -301,7 +314,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         bk[e] = c;
         bra[e] = ra;
         if (f < kPullAbsent) {  // a tuple: mark its first key (rank << 3 | j)
-          const uint32_t key = f >> 13;
+          const uint32_t key = f >> 17;
           atomicOr(&S.bits[key >> 6], 1ull << (key & 63u));
         }
       }
@@ -336,14 +349,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const bool pres = (uint32_t)e < rows_n && fst[e] < kPullAbsent;
         uint32_t rank = 0;
         if ((uint32_t)e < rows_n) {
-          const uint32_t key = pres ? fst[e] >> 13 : 0u;
+          const uint32_t key = pres ? fst[e] >> 17 : 0u;
           const uint4 p = S.pre[key >> 6];
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
         PullCell nc;
         nc.d = pres ? bd[e] : kInf;
-        nc.rank16 = pres ? rank << 16 : kPullAbsent;
+        nc.rank20 = pres ? rank << 20 : kPullAbsent;
         nc.pad = 0;
         S.cell[i] = nc;
         const unsigned long long pm = __ballot(pres);
@@ -352,7 +365,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + (bk[e] & 511u));
+          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + ((bk[e] & 0x1FFFu) >> 4));
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];

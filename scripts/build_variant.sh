@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B builds of the pull tier: compiles eager_pull.hip with extra defines and links it with
+# the release objects into libfst_amd/variants/<name>.so (select with LIBFST_AMD_LIB=...).
+# usage: scripts/build_variant.sh <name> "<-DFLAG ...>"
+set -e
+cd "$(dirname "$0")/../libfst_amd/csrc"
+make -s -j8
+name=$1; defs=$2
+mkdir -p ../variants build_var
+HIPCC=/opt/rocm/bin/hipcc
+$HIPCC -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=off $defs --offload-arch=gfx950 \
+  -c eager_pull.hip -o build_var/$name.o
+$HIPCC -shared -fPIC --offload-arch=gfx950 -o ../variants/$name.so \
+  build/host_fst.cpp.o build/c_api.cpp.o build/device_engine.hip.o build_var/$name.o
+echo "built libfst_amd/variants/$name.so ($defs)"

@@ -2,7 +2,7 @@
 # rocprofv3 passes for the bench workload (run on the GPU box via gpurun):
 #   1) kernel trace + stats (average kernel durations, compared with bench.py's HIP events)
 #   2) FETCH_SIZE pass, 3) WRITE_SIZE pass (separate: they do not fit one TCC pass).
-# usage: scripts/profile_r01.sh <outdir-under-gpurun_out>
+# usage: scripts/profile_bench.sh <outdir-under-gpurun_out>
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 out=${1:-gpurun_out/prof}
