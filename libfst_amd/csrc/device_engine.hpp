@@ -61,13 +61,14 @@ struct RevRec {
 };
 static_assert(sizeof(RevRec) == 16, "RevRec is one 16-byte load");
 struct RevView {
-  const uint4* rspan;     // [num_states] one group: {block, nblocks, ilabel, 0};
-                          // several: {first gtab entry, groups, kSpanMixed, 0}; none: kSpanNone
-  const uint4* gtab;      // groups of multi-label states {ilabel, block, nblocks, 0}, by ilabel
+  const uint4* rspan;     // [num_states + kPullW] one group: {first record, nblocks, ilabel,
+                          // 0}; several: {first gtab entry, groups, kSpanMixed, 0}; none (and
+                          // the padding past the last state): {0, 0, kSpanNone, 0}
+  const uint4* gtab;      // groups of multi-label states {ilabel, first record, nblocks, 0}
   const RevRec* rrec;     // [nblocks * kp]
   const uint32_t* rolab;  // [nblocks * kp] olabel of each record (backtrace only)
   uint32_t kp;            // records per block
-  uint32_t gsearch;       // binary-search steps over the longest gtab run
+  uint32_t gsearch;       // binary-search steps over the longest gtab run (0: no gtab)
 };
 
 struct DeviceFst {

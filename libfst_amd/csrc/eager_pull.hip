@@ -119,9 +119,10 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
 
   std::vector<RevRec> rrec(nblocks * kp, RevRec{0xFFFFFFF0u, 0u, 0.0});  // padding
   std::vector<uint32_t> rolab(nblocks * kp, 0u);
-  std::vector<uint4> rspan(ns, make_uint4(0u, 0u, kSpanNone, 0u));
+  // padded by kPullW entries: a window row may run past the last state
+  std::vector<uint4> rspan((size_t)ns + kPullW, make_uint4(0u, 0u, kSpanNone, 0u));
   std::vector<uint4> gtab;
-  uint32_t max_groups = 1;
+  uint32_t max_groups = 0;
   uint64_t blk = 1;
   for (size_t gi = 0; gi < groups.size();) {
     const uint32_t t = groups[gi].t;
@@ -138,8 +139,9 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     for (size_t g = gi; g < ge; ++g) {
       const Group& G = groups[g];
       const uint32_t nb = (G.n + kp - 1) / kp;
-      if (single) rspan[t] = make_uint4((uint32_t)blk, nb, G.label, 0u);
-      else gtab.push_back(make_uint4(G.label, (uint32_t)blk, nb, 0u));
+      const uint32_t rec0 = (uint32_t)(blk * kp);  // index of the group's first record
+      if (single) rspan[t] = make_uint4(rec0, nb, G.label, 0u);
+      else gtab.push_back(make_uint4(G.label, rec0, nb, 0u));
       for (uint32_t r = 0; r < G.n; ++r) {
         const uint32_t a = in[G.first + r];
         const uint64_t slot = blk * kp + r;
@@ -151,8 +153,9 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     }
     gi = ge;
   }
-  uint32_t gsearch = 1;
-  while ((1u << (gsearch - 1)) < max_groups + 1) ++gsearch;
+  uint32_t gsearch = 0;  // 0: no state has several in-labels (the kernel skips the search)
+  if (!gtab.empty())
+    while ((1u << gsearch) < max_groups + 1) ++gsearch;
 
   auto up = [&](int i, const void* src_p, size_t bytes) -> bool {
     if (bytes == 0) bytes = 16;

@@ -79,7 +79,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
 // One in-arc record against the current layer's cells: its candidate key and distance.
 __device__ __forceinline__ void pull_candidate(const PullCell* cell, const RevRec& r,
                                                uint32_t tmin16, uint32_t W16, uint32_t& pk,
-                                               double& nd) {
+                                               double& nd, uint32_t& rank_word) {
   // byte offset of the source's cell; outside the window (or padding): slot W
   const uint32_t off = min(r.src - tmin16, W16);
   const uint4 c = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(cell) + off);
@@ -87,22 +87,25 @@ __device__ __forceinline__ void pull_candidate(const PullCell* cell, const RevRe
   // ds_read2_b64 instead of b64 + b32, but costs a register and spills: 19.1 vs 20.1 M
   // strings/s)
   pk = c.z | r.y | off;
+  rank_word = c.z;
   // times(d, times(One, w)) for w >= +0 (compose.zig:104, shortest-path.zig:72); +inf
   // stays +inf
   nd = __longlong_as_double((long long)(((unsigned long long)c.y << 32) | c.x)) + r.weight;
 }
 
-// The in-arc group of target t for input label `lab`: its first block and block count
-// (nb = 0: no in-arc with that label, or t outside the window).
-__device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, bool inw, uint32_t t,
-                                           uint32_t& blk, uint32_t& nb) {
-  const uint4 rs = rv.rspan[inw ? t : 0u];
+// The in-arc group of target t for input label `lab`: the index of its first record and
+// its block count (nb = 0: no in-arc with that label).  rspan is padded past the last
+// state, so t may run past the window (such targets have no in-arc from the layer).
+__device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, uint32_t t,
+                                           uint32_t& rec0, uint32_t& nb) {
+  const uint4 rs = rv.rspan[t];
   // (labels >= kSpanMixed always go through gtab: they collide with the markers)
   const bool hit = rs.z == lab && lab < kSpanMixed;
-  blk = hit ? rs.x : 0u;
+  rec0 = hit ? rs.x : 0u;
   nb = hit ? rs.y : 0u;
-  if (__ballot(inw && rs.z == kSpanMixed)) {  // several in-labels: binary search of gtab
-    if (inw && rs.z == kSpanMixed) {
+  // several in-labels: binary search of gtab (gsearch == 0: the rhs has no such state)
+  if (rv.gsearch && __ballot(rs.z == kSpanMixed)) {
+    if (rs.z == kSpanMixed) {
       uint32_t a = rs.x, b = rs.x + rs.y;
       for (uint32_t it = 0; it < rv.gsearch; ++it) {
         if (a < b) {
@@ -114,13 +117,12 @@ __device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, bool
       if (a < rs.x + rs.y) {
         const uint4 g = rv.gtab[a];
         if (g.x == lab) {
-          blk = g.y;
+          rec0 = g.y;
           nb = g.z;
         }
       }
     }
   }
-  if (!inw) nb = 0;
 }
 
 template <int EW, int KP, int WAVES_PER_EU>
@@ -264,19 +266,19 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if ((uint32_t)e >= rows_n) continue;  // uniform
         // (looking up every row's group before the row loop measured no faster)
         const uint32_t i = (uint32_t)e * 64 + lane;
-        uint32_t blk, nb;
-        pull_group(rv, lab, i < wn, tn + i, blk, nb);
-        const RevRec* R = rv.rrec + (size_t)(nb ? blk : 0u) * KP;
+        uint32_t rec0, nb;
+        pull_group(rv, lab, tn + i, rec0, nb);
+        const RevRec* R = rv.rrec + rec0;
         RevRec rr[KP];
 #pragma unroll
         for (int m = 0; m < KP; ++m) rr[m] = R[m];
-        uint32_t pk[KP];
+        uint32_t pk[KP], rw[KP];
         double nd[KP];
         uint32_t f = kEmptyKey;
         double b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
-          pull_candidate(S.cell, rr[m], tmin << 4, 16u * W, pk[m], nd[m]);
+          pull_candidate(S.cell, rr[m], tmin << 4, 16u * W, pk[m], nd[m], rw[m]);
           f = min(f, pk[m]);
           b = fmin(b, nd[m]);
         }
@@ -285,27 +287,27 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
         if (want_work) {
 #pragma unroll
-          for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(pk[m] < kPullAbsent));
+          for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
         }
-        uint32_t ra = (nb ? blk : 0u) * KP + ((c >> 13) & 15u);
+        uint32_t ra = rec0 + ((c >> 13) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
           for (uint32_t x = 1;; ++x) {
             const bool act = nb > x;
             if (!__ballot(act)) break;
-            const RevRec* R2 = rv.rrec + (size_t)(act ? blk + x : 0u) * KP;
+            const uint32_t rx = act ? rec0 + x * KP : 0u;
 #pragma unroll
             for (int m = 0; m < KP; ++m) {
-              uint32_t p2;
+              uint32_t p2, w2;
               double n2;
-              pull_candidate(S.cell, R2[m], tmin << 4, 16u * W, p2, n2);
+              pull_candidate(S.cell, rv.rrec[rx + m], tmin << 4, 16u * W, p2, n2, w2);
               f = min(f, p2);
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
                 c = p2;
-                ra = (act ? blk + x : 0u) * KP + m;
+                ra = rx + m;
               }
-              if (want_work) relax += (uint32_t)__popcll(__ballot(p2 < kPullAbsent));
+              if (want_work) relax += (uint32_t)__popcll(__ballot(w2 < kPullAbsent));
             }
           }
         }
