@@ -50,10 +50,10 @@ struct RhsView {
 
 // Reverse arc mirror for the pull tier (kernels/eager_pull.hpp): the in-arcs of every rhs
 // state t, grouped by ilabel, each group in padded blocks of `kp` records.  Record m of a
-// block: 16 * the source state (its LDS cell offset before the window shift), y = (j << 17)
+// block: 8 * the source state (its LDS cell offset before the window shift), y = (j << 17)
 // | (m << 13) with j = the arc's position in its source's run of equal ilabels (the
 // candidate order of compose.zig:93-121), and the weight.  Padding records have src =
-// 0xFFFFFFF0.  Block 0 is all padding (the null block).
+// 0xFFFFFFF8.  Block 0 is all padding (the null block).
 struct RevRec {
   uint32_t src;
   uint32_t y;

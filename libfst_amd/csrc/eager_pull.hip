@@ -58,7 +58,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   // weights (>= +0, no NaN)
   if (d->has_eps || !d->nonneg || d->nan) return true;
   const uint32_t ns = f.num_states(), na = f.header().num_arcs;
-  if (ns == 0 || ns >= (1u << 27)) return true;  // records hold 16 * state
+  if (ns == 0 || ns >= (1u << 28)) return true;  // records hold 8 * state
   const StateEntry* se = f.states();
   const PackedArc* pa = f.arcs();
 
@@ -117,7 +117,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   for (const Group& g : groups) nblocks += (g.n + kp - 1) / kp;
   if (nblocks * kp * sizeof(RevRec) > (4ull << 30) || nblocks * kp >= 0xFFFFFFFFull) return true;
 
-  std::vector<RevRec> rrec(nblocks * kp, RevRec{0xFFFFFFF0u, 0u, 0.0});  // padding
+  std::vector<RevRec> rrec(nblocks * kp, RevRec{0xFFFFFFF8u, 0u, 0.0});  // padding
   std::vector<uint32_t> rolab(nblocks * kp, 0u);
   // padded by kPullW entries: a window row may run past the last state
   std::vector<uint4> rspan((size_t)ns + kPullW, make_uint4(0u, 0u, kSpanNone, 0u));
@@ -146,7 +146,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
         const uint32_t a = in[G.first + r];
         const uint64_t slot = blk * kp + r;
         const uint32_t m = r % kp;
-        rrec[slot] = RevRec{src[a] << 4, ((uint32_t)jpos[a] << 17) | (m << 13), pa[a].weight};
+        rrec[slot] = RevRec{src[a] << 3, ((uint32_t)jpos[a] << 17) | (m << 13), pa[a].weight};
         rolab[slot] = pa[a].olabel;
       }
       blk += nb;

@@ -20,7 +20,7 @@
 // window [tmin', tmin' + wn) and pulls their in-arcs from the reverse mirror: one 16-B
 // record per in-arc (source, arc position j, weight) and one LDS read of the source's
 // cell (distance, rank).  The merge is then private to the lane:
-//   pk    = rank(s) << 20 | j << 17 | m << 13 | 16 * source slot  (order = candidate order)
+//   pk    = rank(s) << 20 | j << 17 | m << 13 | 8 * source slot  (order = candidate order)
 //   first = min pk                      -> the target exists iff first is a real candidate
 //   d     = min (d(s) + w)
 //   back  = min pk over the in-arcs with d(s) + w == d
@@ -30,7 +30,7 @@
 //
 // A slot with no tuple holds {+inf, kPullAbsent}: its candidates have distance +inf and
 // a key above every real one, so they never win -- the merge needs no validity selects.
-// Reverse records hold 16 * source state, so the source's cell offset is one subtraction:
+// Reverse records hold 8 * source state, so the source's cell offset is one subtraction:
 // slots outside the current layer's window (and the null block's padding records) are
 // clamped to slot W, which never holds a tuple.
 //
@@ -47,16 +47,15 @@ namespace fstamd {
 
 constexpr uint32_t kPullAbsent = 0xFFFF0000u;  // rank word of a slot that holds no tuple
 
-struct alignas(16) PullCell {
-  double d;         // distance of the slot's tuple (+inf: no tuple)
-  uint32_t rank20;  // rank << 20 (kPullAbsent: no tuple)
-  uint32_t pad;
-};
 
 template <int W>
 struct PullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys rank << 3 | j < 8 W
-  PullCell cell[W + 1];                      // slot W never holds a tuple
+  // the current layer's cells, slot W never holds a tuple.  Two arrays of 8-B entries
+  // (one byte offset addresses both): 16-B cells cost ~12 K LDS bank-conflict cycles per
+  // metric string
+  double d[W + 1];                 // distance of the slot's tuple (+inf: no tuple)
+  unsigned long long rk[W + 1];    // rank << 20 (kPullAbsent: no tuple) in the low word
   unsigned long long bits[kWords];
   uint4 pre[kWords];                         // {prefix popcount, 0, word lo, word hi}
   unsigned long long best;
@@ -77,20 +76,22 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
 }
 
 // One in-arc record against the current layer's cells: its candidate key and distance.
-__device__ __forceinline__ void pull_candidate(const PullCell* cell, const RevRec& r,
-                                               uint32_t tmin16, uint32_t W16, uint32_t& pk,
-                                               double& nd, uint32_t& rank_word) {
+template <int W>
+__device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec& r,
+                                               uint32_t tmin8, uint32_t& pk, double& nd,
+                                               uint32_t& rank_word) {
   // byte offset of the source's cell; outside the window (or padding): slot W
-  const uint32_t off = min(r.src - tmin16, W16);
-  const uint4 c = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(cell) + off);
+  const uint32_t off = min(r.src - tmin8, 8u * W);
+  const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + off);
+  const uint32_t rw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S.rk) + off);
   // (folding the pad c.w into the OR makes the compiler read the cell with one
   // ds_read2_b64 instead of b64 + b32, but costs a register and spills: 19.1 vs 20.1 M
   // strings/s)
-  pk = c.z | r.y | off;
-  rank_word = c.z;
+  pk = rw | r.y | off;
+  rank_word = rw;
   // times(d, times(One, w)) for w >= +0 (compose.zig:104, shortest-path.zig:72); +inf
   // stays +inf
-  nd = __longlong_as_double((long long)(((unsigned long long)c.y << 32) | c.x)) + r.weight;
+  nd = d + r.weight;
 }
 
 // The in-arc group of target t for input label `lab`: the index of its first record and
@@ -132,7 +133,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   constexpr int W = 64 * EW;
   constexpr int kWords = PullLds<W>::kWords;
   static_assert(KP <= 16, "m is 4 bits of the key");
-  static_assert(W < 512, "16 * slot is 13 bits of the key, ranks 9 bits");
+  static_assert(W < 512, "8 * slot is 12 bits of the key, ranks 9 bits");
   __shared__ PullLds<W> S;
   const uint32_t lane = threadIdx.x;
   const double kInf = __builtin_huge_val();
@@ -181,9 +182,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-    S.cell[i].d = kInf;
-    S.cell[i].rank20 = kPullAbsent;
-    S.cell[i].pad = 0;
+    S.d[i] = kInf;
+    S.rk[i] = kPullAbsent;
   }
   if (lane < (uint32_t)kWords) S.bits[lane] = 0;
   wave_lds_sync();
@@ -213,13 +213,13 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     // layer 0: the start tuple alone, slot 0 of a window at the start state
 #pragma unroll 1
     for (uint32_t i = lane; i < wlast; i += 64) {
-      S.cell[i].d = kInf;
-      S.cell[i].rank20 = kPullAbsent;
+      S.d[i] = kInf;
+      S.rk[i] = kPullAbsent;
     }
     wave_lds_sync();
     if (lane == 0) {
-      S.cell[0].d = w_one();
-      S.cell[0].rank20 = 0;
+      S.d[0] = w_one();
+      S.rk[0] = 0;
     }
     wave_lds_sync();
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
@@ -278,7 +278,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         double b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
-          pull_candidate(S.cell, rr[m], tmin << 4, 16u * W, pk[m], nd[m], rw[m]);
+          pull_candidate<W>(S, rr[m], tmin << 3, pk[m], nd[m], rw[m]);
           f = min(f, pk[m]);
           b = fmin(b, nd[m]);
         }
@@ -300,7 +300,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             for (int m = 0; m < KP; ++m) {
               uint32_t p2, w2;
               double n2;
-              pull_candidate(S.cell, rv.rrec[rx + m], tmin << 4, 16u * W, p2, n2, w2);
+              pull_candidate<W>(S, rv.rrec[rx + m], tmin << 3, p2, n2, w2);
               f = min(f, p2);
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
@@ -356,18 +356,15 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
-        PullCell nc;
-        nc.d = pres ? bd[e] : kInf;
-        nc.rank20 = pres ? rank << 20 : kPullAbsent;
-        nc.pad = 0;
-        S.cell[i] = nc;
+        S.d[i] = pres ? bd[e] : kInf;
+        S.rk[i] = pres ? rank << 20 : kPullAbsent;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + ((bk[e] & 0x1FFFu) >> 4));
+          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + ((bk[e] & 0x1FFFu) >> 3));
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
