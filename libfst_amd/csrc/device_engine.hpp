@@ -69,6 +69,8 @@ struct RevView {
   const uint32_t* rolab;  // [nblocks * kp] olabel of each record (backtrace only)
   uint32_t kp;            // records per block
   uint32_t gsearch;       // binary-search steps over the longest gtab run (0: no gtab)
+  uint32_t direct;        // 1: block 0 of state t at record t * kp (every state has at most
+                          // one in-label group); rspan.x = the record of its block 1
 };
 
 struct DeviceFst {

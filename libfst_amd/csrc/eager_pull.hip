@@ -14,30 +14,19 @@ namespace fstamd {
 namespace {
 // Waves per SIMD the compiler targets: 5 fit spill-free with blocks of <= 5 records (the
 // metric: 5 waves 20.3 M strings/s, 4 waves 18.5 M, 6 waves 19.8 M with spills);
-// 8-record blocks need 4.  FSTAMD_PULL_WAVES=4|5|6 overrides (occupancy experiments).
-int pull_waves_knob(uint32_t kp) {
-  const char* w = std::getenv("FSTAMD_PULL_WAVES");
-  if (w && (w[0] == '4' || w[0] == '5' || w[0] == '6') && w[1] == 0) return w[0] - '0';
-  return kp <= 5 ? 5 : 4;
-}
+// 8-record blocks need 4.
 
 template <int KP, int WV>
-const void* pull_kernel_ptr() {
-  return (const void*)eager_pull_kernel<kPullRows, KP, WV>;
+const void* pull_kernel_ptr(bool direct) {
+  return direct ? (const void*)eager_pull_kernel<kPullRows, KP, true, WV>
+                : (const void*)eager_pull_kernel<kPullRows, KP, false, WV>;
 }
-template <int WV>
-const void* pull_kernel_kp(uint32_t kp) {
-  switch (kp) {
-    case 4: return pull_kernel_ptr<4, WV>();
-    case 5: return pull_kernel_ptr<5, WV>();
-    default: return pull_kernel_ptr<8, WV>();
-  }
-}
-const void* pull_kernel_for(uint32_t kp) {
-  switch (pull_waves_knob(kp)) {
-    case 5: return pull_kernel_kp<5>(kp);
-    case 6: return pull_kernel_kp<6>(kp);
-    default: return pull_kernel_kp<4>(kp);
+const void* pull_kernel_for(const RevView& rv) {
+  const bool dir = rv.direct != 0;
+  switch (rv.kp) {
+    case 4: return pull_kernel_ptr<4, 5>(dir);
+    case 5: return pull_kernel_ptr<5, 5>(dir);
+    default: return pull_kernel_ptr<8, 4>(dir);
   }
 }
 }  // namespace
@@ -113,8 +102,16 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       kp = cand;
     }
   }
-  uint64_t nblocks = 1;  // block 0: the null block
-  for (const Group& g : groups) nblocks += (g.n + kp - 1) / kp;
+  // Direct layout: when every state has at most one in-label group (and no label collides
+  // with the kSpan* markers), the first block of state t sits at record t * kp, so the
+  // kernel loads it together with rspan[t] instead of after it (one L2 round trip per
+  // target row instead of two).  Further blocks follow the direct region.
+  bool direct = !std::getenv("FSTAMD_PULL_INDIRECT");
+  for (size_t g = 0; g < groups.size() && direct; ++g)
+    if ((g > 0 && groups[g].t == groups[g - 1].t) || groups[g].label >= kSpanMixed) direct = false;
+  const uint64_t ndirect = direct ? (uint64_t)ns + kPullW : 0;  // rows may run past the last state
+  uint64_t nblocks = direct ? ndirect : 1;  // indirect: block 0 is the null block
+  for (const Group& g : groups) nblocks += (g.n + kp - 1) / kp - (direct ? 1 : 0);
   if (nblocks * kp * sizeof(RevRec) > (4ull << 30) || nblocks * kp >= 0xFFFFFFFFull) return true;
 
   std::vector<RevRec> rrec(nblocks * kp, RevRec{0xFFFFFFF8u, 0u, 0.0});  // padding
@@ -123,7 +120,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   std::vector<uint4> rspan((size_t)ns + kPullW, make_uint4(0u, 0u, kSpanNone, 0u));
   std::vector<uint4> gtab;
   uint32_t max_groups = 0;
-  uint64_t blk = 1;
+  uint64_t blk = direct ? ndirect : 1;  // next free block past the fixed ones
   for (size_t gi = 0; gi < groups.size();) {
     const uint32_t t = groups[gi].t;
     size_t ge = gi;
@@ -139,17 +136,19 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     for (size_t g = gi; g < ge; ++g) {
       const Group& G = groups[g];
       const uint32_t nb = (G.n + kp - 1) / kp;
-      const uint32_t rec0 = (uint32_t)(blk * kp);  // index of the group's first record
+      // direct: block 0 at t * kp, blocks 1.. from `blk` on (rspan.x = their first record)
+      const uint32_t rec0 = (uint32_t)(blk * kp);
       if (single) rspan[t] = make_uint4(rec0, nb, G.label, 0u);
       else gtab.push_back(make_uint4(G.label, rec0, nb, 0u));
       for (uint32_t r = 0; r < G.n; ++r) {
         const uint32_t a = in[G.first + r];
-        const uint64_t slot = blk * kp + r;
+        const uint64_t slot = direct ? (r < kp ? (uint64_t)t * kp + r : blk * kp + (r - kp))
+                                     : blk * kp + r;
         const uint32_t m = r % kp;
         rrec[slot] = RevRec{src[a] << 3, ((uint32_t)jpos[a] << 17) | (m << 13), pa[a].weight};
         rolab[slot] = pa[a].olabel;
       }
-      blk += nb;
+      blk += nb - (direct ? 1 : 0);
     }
     gi = ge;
   }
@@ -172,14 +171,15 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     return false;
   }
   d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
-                   (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch};
+                   (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
+                   direct ? 1u : 0u};
   d->pull_ok = true;
   return true;
 }
 
 int pull_waves_per_cu(const DeviceFst& rhs) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pull_kernel_for(rhs.rev.kp), 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pull_kernel_for(rhs.rev), 64, 0) !=
       hipSuccess)
     occ = 1;
   return std::max(occ, 1);
@@ -190,7 +190,7 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
   void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
                   (void*)&next_item, (void*)&lp, (void*)&out};
-  return hipLaunchKernel(pull_kernel_for(rhs.rev.kp), dim3(grid), dim3(64), args, 0, stream);
+  return hipLaunchKernel(pull_kernel_for(rhs.rev), dim3(grid), dim3(64), args, 0, stream);
 }
 
 }  // namespace fstamd

@@ -126,7 +126,10 @@ __device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, uint
   }
 }
 
-template <int EW, int KP, int WAVES_PER_EU>
+// DIRECT (RevView::direct): block 0 of target t is records [t * KP, t * KP + KP), loaded
+// together with rspan[t] (which then only confirms the label); otherwise the group is
+// looked up first (pull_group) and its records loaded after.
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
 eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                   unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
@@ -266,8 +269,18 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if ((uint32_t)e >= rows_n) continue;  // uniform
         // (looking up every row's group before the row loop measured no faster)
         const uint32_t i = (uint32_t)e * 64 + lane;
-        uint32_t rec0, nb;
-        pull_group(rv, lab, tn + i, rec0, nb);
+        const uint32_t t = tn + i;
+        uint32_t rec0, nb, xrec = 0;
+        bool hit = true;
+        if constexpr (DIRECT) {
+          const uint4 rs = rv.rspan[t];
+          hit = rs.z == lab && lab < kSpanMixed;  // block 0 holds the arcs of another label
+          rec0 = t * KP;
+          nb = hit ? rs.y : 0u;
+          xrec = rs.x;
+        } else {
+          pull_group(rv, lab, t, rec0, nb);
+        }
         const RevRec* R = rv.rrec + rec0;
         RevRec rr[KP];
 #pragma unroll
@@ -285,9 +298,17 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t c = kEmptyKey;
 #pragma unroll
         for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
+        if constexpr (DIRECT) {
+          if (!hit) {
+            f = kEmptyKey;
+            b = kInf;
+            c = kEmptyKey;
+          }
+        }
         if (want_work) {
 #pragma unroll
-          for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
+          for (int m = 0; m < KP; ++m)
+            relax += (uint32_t)__popcll(__ballot(hit && rw[m] < kPullAbsent));
         }
         uint32_t ra = rec0 + ((c >> 13) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
@@ -295,7 +316,10 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           for (uint32_t x = 1;; ++x) {
             const bool act = nb > x;
             if (!__ballot(act)) break;
-            const uint32_t rx = act ? rec0 + x * KP : 0u;
+            // inactive lanes read a padding block (indirect: block 0; direct: the block of
+            // the first padding state past the last one)
+            const uint32_t rx = act ? (DIRECT ? xrec + (x - 1) * KP : rec0 + x * KP)
+                                    : (DIRECT ? rhs.num_states * KP : 0u);
 #pragma unroll
             for (int m = 0; m < KP; ++m) {
               uint32_t p2, w2;

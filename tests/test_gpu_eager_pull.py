@@ -7,7 +7,8 @@ OK is bit-exact against the oracle's compose + shortestPath (compose.zig:29-198,
 shortest-path.zig:18-139).  The shapes target the reverse mirror's corners: groups of in-
 arcs longer than one block (hub states), several in-labels per state (gtab search),
 same-label runs of 8 (j = 7), labels that collide with the span markers, full 320-state
-layers (ranks up to 319, all 40 bitmap words), +inf arc and final weights.
+layers (ranks up to 319, all 40 bitmap words), +inf arc and final weights -- each in the
+direct and the indirect record layout.
 """
 import math
 
@@ -23,10 +24,16 @@ pytestmark = pytest.mark.gpu
 EAGER = F.FST_SEM_EAGER
 
 
-@pytest.fixture
-def only_p(monkeypatch):
+@pytest.fixture(params=["direct", "indirect"])
+def only_p(request, monkeypatch):
+    # direct: block 0 of every state at a fixed record index (single-label rhs, the
+    # default there); indirect: group lookup first (FSTAMD_PULL_INDIRECT forces it)
     monkeypatch.setenv("FSTAMD_EAGER_ONLY_FIRST", "1")
     monkeypatch.delenv("FSTAMD_EAGER_TIER1", raising=False)
+    if request.param == "indirect":
+        monkeypatch.setenv("FSTAMD_PULL_INDIRECT", "1")
+    else:
+        monkeypatch.delenv("FSTAMD_PULL_INDIRECT", raising=False)
 
 
 def run_p(blob, seqs, expect_all=True):
