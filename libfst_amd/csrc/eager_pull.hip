@@ -21,11 +21,14 @@ const void* pull_kernel_ptr(bool direct) {
   return direct ? (const void*)eager_pull_kernel<kPullRows, KP, true, WV>
                 : (const void*)eager_pull_kernel<kPullRows, KP, false, WV>;
 }
+#ifndef FSTAMD_PULL_WAVES_SMALL  // A/B builds: waves per SIMD for blocks of <= 5 records
+#define FSTAMD_PULL_WAVES_SMALL 5
+#endif
 const void* pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
   switch (rv.kp) {
-    case 4: return pull_kernel_ptr<4, 5>(dir);
-    case 5: return pull_kernel_ptr<5, 5>(dir);
+    case 4: return pull_kernel_ptr<4, FSTAMD_PULL_WAVES_SMALL>(dir);
+    case 5: return pull_kernel_ptr<5, FSTAMD_PULL_WAVES_SMALL>(dir);
     default: return pull_kernel_ptr<8, 4>(dir);
   }
 }
