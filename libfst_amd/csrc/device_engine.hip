@@ -466,6 +466,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
           hipSuccess)
         occ = 1;
       grid_w = (uint32_t)std::min<uint64_t>((uint64_t)std::max(occ, 1) * num_cus_, in.num_strings);
+      // behind tier P, A0 only takes P's overflows: 2 waves per CU keep its slabs small
+      if (use_p) grid_w = std::min<uint32_t>(grid_w, 2u * (uint32_t)num_cus_);
       while (grid_w > 1 && (uint64_t)grid_w * kChaseBatch * back_cap_w * 8 > (24ull << 30))
         grid_w /= 2;
       grid_w = std::max<uint32_t>(grid_w, 1);
