@@ -50,7 +50,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   // weights (>= +0, no NaN)
   if (d->has_eps || !d->nonneg || d->nan) return true;
   const uint32_t ns = f.num_states(), na = f.header().num_arcs;
-  if (ns == 0 || ns >= (1u << 28)) return true;  // records hold 8 * state
+  if (ns == 0 || ns >= (1u << 27)) return true;  // records hold 8 * state < 2^30
   const StateEntry* se = f.states();
   const PackedArc* pa = f.arcs();
 

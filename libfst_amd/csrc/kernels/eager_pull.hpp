@@ -271,10 +271,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint32_t i = (uint32_t)e * 64 + lane;
         const uint32_t t = tn + i;
         uint32_t rec0, nb, xrec = 0;
-        bool hit = true;
+        uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
           const uint4 rs = rv.rspan[t];
-          hit = rs.z == lab && lab < kSpanMixed;  // block 0 holds the arcs of another label
+          // block 0 holds the arcs of another label: shifting the window origin by 2^31
+          // sends every source of the row past slot W (8 * state < 2^30), so the row
+          // merges to "no tuple" with no per-result selects
+          const bool hit = rs.z == lab && lab < kSpanMixed;
+          tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;
           rec0 = t * KP;
           nb = hit ? rs.y : 0u;
           xrec = rs.x;
@@ -291,24 +295,16 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         double b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
-          pull_candidate<W>(S, rr[m], tmin << 3, pk[m], nd[m], rw[m]);
+          pull_candidate<W>(S, rr[m], tmin8, pk[m], nd[m], rw[m]);
           f = min(f, pk[m]);
           b = fmin(b, nd[m]);
         }
         uint32_t c = kEmptyKey;
 #pragma unroll
         for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
-        if constexpr (DIRECT) {
-          if (!hit) {
-            f = kEmptyKey;
-            b = kInf;
-            c = kEmptyKey;
-          }
-        }
         if (want_work) {
 #pragma unroll
-          for (int m = 0; m < KP; ++m)
-            relax += (uint32_t)__popcll(__ballot(hit && rw[m] < kPullAbsent));
+          for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
         }
         uint32_t ra = rec0 + ((c >> 13) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
@@ -324,7 +320,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             for (int m = 0; m < KP; ++m) {
               uint32_t p2, w2;
               double n2;
-              pull_candidate<W>(S, rv.rrec[rx + m], tmin << 3, p2, n2, w2);
+              pull_candidate<W>(S, rv.rrec[rx + m], tmin8, p2, n2, w2);
               f = min(f, p2);
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
