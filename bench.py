@@ -33,6 +33,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Measured HBM traffic of the metric kernel: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 # over this same command (scripts/profile_bench.sh), reduced by scripts/pmc_summary.py.
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+# SQ instruction mix of the metric kernel (scripts/sq_counters.sh + sq_summary.py --json):
+# the kernel's real bound is VALU issue, not bytes
+ISSUE_FILE = os.path.join(REPO, "profiles", "sq_issue.json")
+L2_PEAK_GBS = 34500.0  # MI355X aggregate L2 (MI355X_MICROARCH.md "L2 (per XCD)")
 
 
 EAGER_KERNEL = "eager_pull_kernel"     # tier P, takes every metric string
@@ -51,6 +55,25 @@ def measured_traffic(args, sem):
     if t.get("kernel") != EAGER_KERNEL:
         return None, None
     return t["traffic_per_string"] * args.batch, t.get("source", TRAFFIC_FILE)
+
+
+def issue_profile(sem):
+    """VALU issue figures of the eager metric kernel from the committed SQ summary."""
+    if sem != F.FST_SEM_EAGER:
+        return None
+    try:
+        t = json.load(open(ISSUE_FILE))
+    except (OSError, ValueError):
+        return None
+    if t.get("kernel") != EAGER_KERNEL:
+        return None
+    ps, wc = t["per_string"], t["of_wave_cycles"]
+    return {"bound": "valu-issue",
+            "valu_insts_per_string": ps.get("SQ_INSTS_VALU"),
+            "salu_insts_per_string": ps.get("SQ_INSTS_SALU"),
+            "lds_insts_per_string": ps.get("SQ_INSTS_LDS"),
+            "valu_active_per_wave": wc.get("SQ_ACTIVE_INST_VALU"),
+            "source": t.get("source", ISSUE_FILE)}
 
 
 def parse():
@@ -318,10 +341,16 @@ def main():
                          "hbm_traffic_gbs": (traffic / (avg_k * 1e-3) / 1e9) if traffic else None,
                          "hbm_traffic_frac": (traffic / (avg_k * 1e-3) / 1e9 / HBM_PEAK_GBS)
                          if traffic else None,
+                         "l2_peak": L2_PEAK_GBS,
+                         "l2_frac": achieved / L2_PEAK_GBS,
+                         "issue": issue_profile(sem),
                          "note": "achieved = SURVEY 8(d) logical bytes (24 B per arc relaxed, 16 B "
-                                 "per tuple expanded, labels, path) / kernel time; the 0.56 MB "
-                                 "rhs is L2/LDS-resident, so this can exceed the HBM peak; "
-                                 "hbm_traffic_* is the PMC-measured DRAM traffic"},
+                                 "per tuple expanded, labels, path) / kernel time. Those reads hit "
+                                 "the 0.6 MB L2-resident rhs mirror (and LDS), never HBM, so frac "
+                                 "(vs the 8 TB/s HBM peak) exceeds 1; l2_frac prices them against "
+                                 "the 34.5 TB/s L2. hbm_traffic_* is the PMC-measured DRAM traffic "
+                                 "(back records, labels, paths). The kernel is bound by VALU issue "
+                                 "(issue: SQ counters)"},
             "cpu_baseline": cpu,
             "checked_vs_oracle": checked,
         }
