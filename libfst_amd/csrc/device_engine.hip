@@ -199,7 +199,8 @@ constexpr int kEwinWaves = 3;
 static_assert((uint32_t)kEwinW == kPullW, "tiers P and A0 share the back slab geometry");
 
 // Item counters and list counts, one 256-B block shared by the engines (word ranges):
-// run_chain [0..6] and [14..15] (pull tier), lazy replay retry tiers [6..13], run_bfs_chain [8..11] (never in the
+// run_chain [0..6] and [14..15] (pull tier), run_lazy_pull [34..35], lazy replay retry
+// tiers [6..13], run_bfs_chain [8..11] (never in the
 // same call as the replay tiers), run_lazy_layered [32], run_lazy_dense [33].
 constexpr size_t kCounterBytes = 256;
 
@@ -245,6 +246,8 @@ enum Scratch : size_t {
   kBfsHeap,
   kPullBack,
   kItems4,
+  kLpBack,
+  kItems5,
   kNumScratch
 };
 
@@ -653,11 +656,27 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     const bool layered = !rhs.has_eps && rhs.view.max_span <= kLlSpanMax &&
                          (uint64_t)(in.max_len + 1) * rhs.view.num_states <= kLlDenseMax &&
                          !(ll && std::strcmp(ll, "0") == 0);
-    if (layered) {
-      if (stats) stats->engine = 4;
-      HIP_TRY(run_lazy_layered(rhs, in, n, out, stream));
+    // Layer-local pull first (kernels/lazy_pull.hpp) when the rhs has a reverse mirror
+    // that suits it; the strings it hands on go to the rounds engines.
+    const bool use_lp = !rhs.has_eps && rhs.lazy_pull_ok && !force_rounds;
+    uint32_t* lp_list = nullptr;
+    uint32_t* lp_count = nullptr;
+    if (use_lp) {
+      if (stats) stats->engine = 7;
+      HIP_TRY(run_lazy_pull(rhs, in, n, out, stream, &lp_list, &lp_count));
+      if (std::getenv("FSTAMD_LAZY_ONLY_FIRST")) {  // test hook: what the pull took alone
+        if (stats) {
+          HIP_TRY(hipEventRecord(ev1_, stream));
+          HIP_TRY(finish_stats(ev0_, ev1_, stats));
+        }
+        return hipSuccess;
+      }
     }
-    HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !layered, true));
+    if (layered) {
+      if (stats && !use_lp) stats->engine = 4;
+      HIP_TRY(run_lazy_layered(rhs, in, n, out, stream, lp_list, lp_count));
+    }
+    HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !layered && !use_lp, true));
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
@@ -797,9 +816,36 @@ __global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_
 
 // One-wave dense lazy engine for layered lattices.  Its per-wave dense arrays are left
 // clean by every string, so they are initialised only when (re)allocated.
+hipError_t DeviceEngine::run_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                       const BatchOutDev& out, hipStream_t stream,
+                                       uint32_t** list, uint32_t** count_dev) {
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [34..35] are ours
+  if (!ctr) return hipErrorOutOfMemory;
+  // kChaseBatch back slabs per wave, kPullW slots per layer (as tier P)
+  const uint32_t back_cap =
+      (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * kPullW, 1u << 22);
+  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)lazy_pull_waves_per_cu(rhs) * num_cus_,
+                                               in.num_strings);
+  while (grid > 1 && (uint64_t)grid * kChaseBatch * back_cap * 8 > (24ull << 30)) grid /= 2;
+  grid = std::max<uint32_t>(grid, 1);
+  uint2* back = (uint2*)scratch(kLpBack, (size_t)grid * kChaseBatch * back_cap * 8);
+  uint32_t* lst = (uint32_t*)scratch(kItems5, (size_t)in.num_strings * 4);
+  if (!back || !lst) return hipErrorOutOfMemory;
+  HIP_TRY(hipMemsetAsync(ctr + 34, 0, 8, stream));
+  EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back, back_cap, watchdog_ticks()};
+  HIP_TRY(launch_lazy_pull(rhs, in, n, ctr + 34, lp, out, grid, stream));
+  collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
+      out.status, in.num_strings, kPathOverflow, lst, ctr + 35);
+  HIP_TRY(hipGetLastError());
+  *list = lst;
+  *count_dev = ctr + 35;
+  return hipSuccess;
+}
+
 hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput& in,
                                           uint32_t n, const BatchOutDev& out,
-                                          hipStream_t stream) {
+                                          hipStream_t stream, const uint32_t* items,
+                                          const uint32_t* num_items_dev) {
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [32] is ours
   if (!ctr) return hipErrorOutOfMemory;
   LlWs ws{};
@@ -807,12 +853,17 @@ hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput
   ws.dn = (uint64_t)(in.max_len + 1) * rhs.view.num_states;
   ws.ncap = (uint32_t)ws.dn;
   ws.wd_ticks = watchdog_ticks();
+  ws.items = items;
+  ws.num_items_dev = num_items_dev;
   ws.acap = (uint32_t)std::min<uint64_t>(ws.dn, 1u << 15);
   const uint64_t per_wave = ws.dn * (8 + 8 + 4 + 4 + 4 + 4) + ((uint64_t)ws.lcap + 2) * 4 +
                             (uint64_t)ws.acap * 32;
   const uint64_t budget = 48ull << 30;  // of the 288 GB: all 16 waves per CU at the metric
+  // behind the lazy pull (items != null) it takes only the pull's fallbacks: 2 waves per
+  // CU keep its dense workspaces small
   uint32_t grid = (uint32_t)std::min<uint64_t>(
-      {(uint64_t)num_cus_ * 16, (uint64_t)in.num_strings, std::max<uint64_t>(1, budget / per_wave)});
+      {(uint64_t)num_cus_ * (items ? 2 : 16), (uint64_t)in.num_strings,
+       std::max<uint64_t>(1, budget / per_wave)});
   grid = std::max<uint32_t>(grid, 1);
   const size_t g = grid;
   ws.dk = (unsigned long long*)scratch(kLlDk, g * ws.dn * 8);

@@ -91,6 +91,10 @@ struct DeviceFst {
   // pull tier (kernels/eager_pull.hpp): reverse mirror, built when the rhs qualifies
   // (no input epsilon, weights >= +0, every same-ilabel run of a state <= 8 arcs)
   bool pull_ok = false;
+  // lazy pull tier (kernels/lazy_pull.hpp) too: for arcs of one source into one target
+  // within a same-ilabel run, candidate order = olabel order (relax's (id, il, ol) rule
+  // then reduces to (id, candidate))
+  bool lazy_pull_ok = false;
   RevView rev{};
   void* rev_bufs[4] = {nullptr, nullptr, nullptr, nullptr};
 
@@ -163,6 +167,11 @@ int pull_waves_per_cu(const DeviceFst& rhs);
 hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
                              unsigned int* next_item, const EagerLaunch& lp,
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream);
+// Lazy pull tier (eager_pull.hip, kernels/lazy_pull.hpp): resident waves per CU, launch.
+int lazy_pull_waves_per_cu(const DeviceFst& rhs);
+hipError_t launch_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
+                            unsigned int* next_item, const EagerLaunch& lp,
+                            const BatchOutDev& out, uint32_t grid, hipStream_t stream);
 
 // Per-device engine state: persistent workspaces (grown on demand) and a lock,
 // since the C ABI may be called from several threads.
@@ -208,7 +217,14 @@ class DeviceEngine {
   // composeShortestPath on layered lattices (kernels/lazy_layered.hpp); strings it does
   // not take end UNSUPPORTED / OVERFLOW for run_bfs_chain.
   hipError_t run_lazy_layered(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
-                              const BatchOutDev& out, hipStream_t stream);
+                              const BatchOutDev& out, hipStream_t stream,
+                              const uint32_t* items = nullptr,
+                              const uint32_t* num_items_dev = nullptr);
+  // composeShortestPath on layered lattices by the layer-local pull (kernels/lazy_pull.hpp);
+  // the strings it hands on (OVERFLOW) are listed in *list, their count at *count_dev.
+  hipError_t run_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                           const BatchOutDev& out, hipStream_t stream, uint32_t** list,
+                           uint32_t** count_dev);
   // composeShortestPath as a dense-indexed exact replay (kernels/lazy_dense.hpp), for rhs
   // with input epsilons; strings it does not take end UNSUPPORTED / OVERFLOW for
   // run_bfs_chain.  *ran = false: it took none (the lattice exceeds its dense index).

@@ -8,6 +8,7 @@
 #include "device_engine.hpp"
 #include "host_fst.hpp"
 #include "kernels/eager_pull.hpp"
+#include "kernels/lazy_pull.hpp"
 
 namespace fstamd {
 
@@ -32,6 +33,20 @@ const void* pull_kernel_for(const RevView& rv) {
     default: return pull_kernel_ptr<8, 4>(dir);
   }
 }
+constexpr int kLazyPullWaves = 3;
+template <int KP>
+const void* lazy_pull_ptr(bool direct) {
+  return direct ? (const void*)lazy_pull_kernel<kPullRows, KP, true, kLazyPullWaves>
+                : (const void*)lazy_pull_kernel<kPullRows, KP, false, kLazyPullWaves>;
+}
+const void* lazy_pull_kernel_for(const RevView& rv) {
+  const bool dir = rv.direct != 0;
+  switch (rv.kp) {
+    case 4: return lazy_pull_ptr<4>(dir);
+    case 5: return lazy_pull_ptr<5>(dir);
+    default: return lazy_pull_ptr<8>(dir);
+  }
+}
 }  // namespace
 
 void free_reverse_mirror(DeviceFst* d) {
@@ -45,6 +60,7 @@ void free_reverse_mirror(DeviceFst* d) {
 
 bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   d->pull_ok = false;
+  d->lazy_pull_ok = false;
   if (std::getenv("FSTAMD_NO_PULL")) return true;
   // the pull tier's contract: layered lattices (no input epsilon) and the push tiers'
   // weights (>= +0, no NaN)
@@ -69,6 +85,16 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       ++indeg[pa[a].nextstate];
     }
   }
+  // lazy pull: within a same-ilabel run, arcs into one target must come in olabel order
+  // (fromMutable sorts by (ilabel, olabel, weight, nextstate); a fromBytes blob may not)
+  bool ol_ordered = true;
+  for (uint32_t s = 0; s < ns && ol_ordered; ++s)
+    for (uint32_t a = se[s].arc_offset; a < se[s].arc_offset + se[s].num_arcs && ol_ordered; ++a)
+      for (uint32_t b = a - jpos[a]; b < a; ++b)
+        if (pa[b].nextstate == pa[a].nextstate && pa[b].olabel > pa[a].olabel) {
+          ol_ordered = false;
+          break;
+        }
   // in-arcs by target (counting sort), then by (ilabel, source, j) within a target
   std::vector<uint32_t> ioff(ns + 1, 0);
   for (uint32_t t = 0; t < ns; ++t) ioff[t + 1] = ioff[t] + indeg[t];
@@ -177,6 +203,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
                    direct ? 1u : 0u};
   d->pull_ok = true;
+  d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;
 }
 
@@ -194,6 +221,22 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
   void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
                   (void*)&next_item, (void*)&lp, (void*)&out};
   return hipLaunchKernel(pull_kernel_for(rhs.rev), dim3(grid), dim3(64), args, 0, stream);
+}
+
+int lazy_pull_waves_per_cu(const DeviceFst& rhs) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lazy_pull_kernel_for(rhs.rev), 64, 0) !=
+      hipSuccess)
+    occ = 1;
+  return std::max(occ, 1);
+}
+
+hipError_t launch_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
+                            unsigned int* next_item, const EagerLaunch& lp,
+                            const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
+  void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
+                  (void*)&next_item, (void*)&lp, (void*)&out};
+  return hipLaunchKernel(lazy_pull_kernel_for(rhs.rev), dim3(grid), dim3(64), args, 0, stream);
 }
 
 }  // namespace fstamd

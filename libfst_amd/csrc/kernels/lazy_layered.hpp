@@ -41,6 +41,8 @@ struct LlWs {
   unsigned long long wd_ticks;
   unsigned long long* prof;  // [grid * 8] (FSTAMD_BFS_PROF): ticks of layers, rounds,
                              // backs/best/output, reset; items; rounds
+  const uint32_t* items;     // null: item i is string i; else the strings to take
+  const uint32_t* num_items_dev;  // entries of items (device count)
 };
 
 constexpr uint32_t kLlPend = 0x80000000u;
@@ -162,12 +164,14 @@ lazy_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
   const uint32_t NS = rhs.num_states;
   unsigned long long* prof = ws.prof ? ws.prof + w * 8 : nullptr;
 
+  const uint32_t num_items =
+      __builtin_amdgcn_readfirstlane(ws.items ? *ws.num_items_dev : in.num_strings);
   for (uint32_t guard = 0;; ++guard) {
     uint32_t item = 0;
     if (lane == 0) item = atomicAdd(next_item, 1u);
     item = __builtin_amdgcn_readfirstlane(item);
-    if (item >= in.num_strings) break;
-    const uint32_t si = item;
+    if (item >= num_items) break;
+    const uint32_t si = __builtin_amdgcn_readfirstlane(ws.items ? ws.items[item] : item);
     const uint64_t off = in.offsets[si];
     const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)(in.offsets[si + 1] - off));
     const uint32_t* labels = in.labels + off;

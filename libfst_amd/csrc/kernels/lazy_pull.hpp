@@ -1,0 +1,521 @@
+// lazy_pull.hpp -- composeShortestPath (FST_SEM_LAZY) on layered lattices, one wavefront
+// per string, PULL formulation over the reverse mirror of tier P (gfx950 / CDNA4).
+//
+// Domain: chain inputs without label 0 against an rhs without input epsilons, finite
+// weights >= 0 (every lattice arc goes from layer k to layer k+1).  The reference
+// (src/ops/compose-shortest-path.zig:26-401) pops min (dist, id) with ids given at first
+// touch (getOrCreate, :70-89); the answer depends on the ids through the tie rules of
+// relax (:107-141) and of the best final (:165-179).  tests/lazy_pull_model.py states the
+// argument and is checked against the oracle's sequential replay:
+//
+//   C  if every tuple x but the start has a tight in-neighbour u that pops before it --
+//      d(u) < d(x), or d(u) == d(x) and id(u) < id(x) -- the pop order is exactly the
+//      sort by (dist, id).
+//
+// Under C every piece of the answer is layer-local, so a layer costs a pull merge like
+// tier P's plus one sort:
+//   * p_k  = pop rank within layer k = rank of (d, r_k)           -- stable LSD split sort
+//   * r_k+1 (id order within layer k+1) = order of (p_k(u*), j*), u* = the first toucher
+//     (the in-neighbour popped first), j* its candidate position    -- first-key bitmap
+//   * back(x) = lexmin (r_k(u), j) over tight in-arcs (relax's (id, il, ol) order with il
+//     fixed by the layer; the reverse mirror is built only when, for arcs of one source
+//     into one target, candidate order = ol order)
+//   * best = lexmin (total, r_L)
+// C needs id(u) < id(x) across adjacent layers: id(u) < id(x) iff u's first toucher popped
+// before x's, recursively down the chains of first touchers.  Each cell keeps tb = d(u*)
+// (-1 for the start) and run = the length of the initial run of equal distances in its
+// chain; a tight u certifies x when tb(u) < tb(x), or tb equal and run(u) < run(x).  A
+// string with an uncertified tuple ends OVERFLOW and the rounds engine (lazy_layered.hpp)
+// takes it.
+#pragma once
+
+#include "eager_pull.hpp"  // RevView helpers, pull_group, wave_incl_scan_dpp, ChaseJob
+
+namespace fstamd {
+
+constexpr uint32_t kLpAbsent = 0xFFF00000u;  // rank words of a slot that holds no tuple
+constexpr uint32_t kLpRunMask = 0xFFFu;      // run (<= 4095 layers) below the pop rank
+constexpr uint32_t kLpMaxLen = 4095;
+
+template <int W>
+struct LazyPullLds {
+  static constexpr int kWords = W * 8 / 64;  // first keys p << 3 | j < 8 W
+  // the current layer's cells (slot W never holds a tuple), 8-B arrays addressed by one
+  // byte offset
+  double d[W + 1];                 // distance (+inf: no tuple)
+  unsigned long long rp[W + 1];    // lo: id rank << 20; hi: pop rank << 20 | run
+  double tb[W + 1];                // distance of the first toucher (-1: the start)
+  unsigned long long bits[kWords];
+  uint4 pre[kWords];
+  uint16_t ord[2][W];              // sort: slots in id order, then in pop order
+  unsigned long long best;
+  uint32_t bestp;
+  ChaseJob job[kChaseBatch];
+};
+
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU>
+__global__ void __launch_bounds__(64, WAVES_PER_EU)
+lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
+                 unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
+  constexpr int W = 64 * EW;
+  constexpr int kWords = LazyPullLds<W>::kWords;
+  static_assert(KP <= 16 && W < 512, "key layout as in eager_pull.hpp");
+  __shared__ LazyPullLds<W> S;
+  const uint32_t lane = threadIdx.x;
+  const double kInf = __builtin_huge_val();
+  const unsigned long long kAbsent2 = ((unsigned long long)kLpAbsent << 32) | kLpAbsent;
+  uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
+  uint32_t njobs = 0;
+
+  // the batched backtrace of tier P (shortest-path.zig:109-136 / compose-shortest-
+  // path.zig:368-380: the path has exactly L arcs, one per layer)
+  auto chase_batch = [&]() {
+    wave_lds_sync();
+    uint32_t maxL = 0;
+    ChaseJob jb{};
+    if (lane < njobs) {
+      jb = S.job[lane];
+      maxL = jb.L;
+    }
+    maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
+    const uint2* sl = slabs + (size_t)lane * lp.back_cap;
+    uint32_t id = jb.id;
+    for (uint32_t t = 0; t < maxL; ++t) {
+      if (lane < njobs && t < jb.L) {
+        const uint32_t k = jb.L - 1 - t;
+        const uint2 b = sl[FB(id, lp.back_cap, 70)];
+        out.out_il[jb.o + k] = in.labels[jb.off + k];
+        out.out_ol[jb.o + k] = rv.rolab[b.x];
+        out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+        id = b.y;
+      }
+    }
+    if (lane < njobs) {
+      out.status[jb.si] = kPathOk;
+      out.path_len[jb.si] = jb.L;
+      out.path_off[jb.si] = jb.o;
+      out.final_w[jb.si] = jb.fw;
+      if (out.work) {
+        out.work[2 * jb.si] = jb.tuples;
+        out.work[2 * jb.si + 1] = jb.relax;
+      }
+    }
+    njobs = 0;
+    wave_lds_sync();
+  };
+  const uint32_t num_items = __builtin_amdgcn_readfirstlane(
+      lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
+  const bool want_work = out.work != nullptr;
+
+#pragma unroll 1
+  for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
+    S.d[i] = kInf;
+    S.rp[i] = kAbsent2;
+    S.tb[i] = kInf;
+  }
+  if (lane < (uint32_t)kWords) S.bits[lane] = 0;
+  wave_lds_sync();
+  uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
+
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(next_item, 1u);
+    item = __builtin_amdgcn_readfirstlane(item);
+    if (item >= num_items) break;
+    const uint32_t si = __builtin_amdgcn_readfirstlane(lp.items ? lp.items[item] : item);
+    uint2* const back = slabs + (size_t)njobs * lp.back_cap;
+    const uint64_t off0 = in.offsets[si];
+    const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
+                         __builtin_amdgcn_readfirstlane((uint32_t)off0);
+    const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)(in.offsets[si + 1] - off));
+
+    if (rhs.start == kNoState || n_best != 1) {  // compose-shortest-path.zig:30-33
+      if (lane == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+
+    // layer 0: the start tuple (id 0, pop rank 0, tb -1 < every distance)
+#pragma unroll 1
+    for (uint32_t i = lane; i < wlast; i += 64) {
+      S.d[i] = kInf;
+      S.rp[i] = kAbsent2;
+      S.tb[i] = kInf;
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+      S.d[0] = w_one();
+      S.rp[0] = 0;
+      S.tb[0] = -1.0;
+    }
+    wave_lds_sync();
+    uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
+    uint32_t cmin = rhs.start, cmax = rhs.start;
+    uint32_t tuples = 1, relax = 0;
+    int32_t fail = L > kLpMaxLen ? kPathOverflow : kPathOk;
+    unsigned long long mykey = kMaxU64;
+    uint32_t myp = kEmptyKey;
+    double myfw = 0.0;
+
+    uint32_t labs = 0;
+    for (uint32_t k = 0; k < L && fail == kPathOk; ++k) {
+      if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
+        fail = kPathInternal;
+        break;
+      }
+      if ((k & 63u) == 0) labs = k + lane < L ? in.labels[off + k + lane] : 0u;
+      const uint32_t lab = __builtin_amdgcn_readlane(labs, k & 63u);
+      if (lab == kEpsilon) {
+        fail = kPathUnsupported;
+        break;
+      }
+      const uint32_t tn = cmin >= rhs.jump_back ? cmin - rhs.jump_back : 0u;
+      const uint64_t hi = min((uint64_t)cmax + rhs.jump_fwd, (uint64_t)rhs.num_states - 1);
+      const uint32_t nbase = base + wk;
+      if (hi - tn >= (uint64_t)W || (uint64_t)nbase + (hi - tn + 1) > lp.back_cap) {
+        fail = kPathOverflow;
+        break;
+      }
+      const uint32_t wn = (uint32_t)(hi - tn) + 1;
+      const uint32_t rows_n = (wn + 63) / 64;
+      const bool check_c = k + 1 < L;  // the last layer's pop order is never used
+
+      // ---- (P1) pull merge per target: first toucher, distance, back-pointer, C ----
+      uint32_t fst[EW], bk[EW], bra[EW], runx[EW];
+      double bd[EW], tbx[EW];
+      bool uncert = false;
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        fst[e] = kEmptyKey;
+        bk[e] = kEmptyKey;
+        bra[e] = 0;
+        bd[e] = kInf;
+        tbx[e] = kInf;
+        runx[e] = 0;
+        if ((uint32_t)e >= rows_n) continue;  // uniform
+        const uint32_t i = (uint32_t)e * 64 + lane;
+        const uint32_t t = tn + i;
+        uint32_t rec0, nb, xrec = 0;
+        uint32_t tmin8 = tmin << 3;
+        if constexpr (DIRECT) {
+          const uint4 rs = rv.rspan[t];
+          const bool hit = rs.z == lab && lab < kSpanMixed;
+          tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;  // no in-arc of this label (tier P)
+          rec0 = t * KP;
+          nb = hit ? rs.y : 0u;
+          xrec = rs.x;
+        } else {
+          pull_group(rv, lab, t, rec0, nb);
+        }
+        // first record of block x >= 1 of a group longer than one block (a hub state);
+        // lanes without one read a padding block
+        auto block_rec = [&](uint32_t x) -> uint32_t {
+          if (nb > x) return DIRECT ? xrec + (x - 1) * KP : rec0 + x * KP;
+          return DIRECT ? rhs.num_states * KP : 0u;
+        };
+        const bool hubs = __ballot(nb > 1) != 0;  // uniform
+        const RevRec* R = rv.rrec + rec0;
+        RevRec rr[KP];
+#pragma unroll
+        for (int m = 0; m < KP; ++m) rr[m] = R[m];
+        uint32_t bpk[KP];
+        double nd[KP];
+        uint32_t ff = kEmptyKey, wpos = 0;
+        double b = kInf;
+#pragma unroll
+        for (int m = 0; m < KP; ++m) {
+          const uint32_t o = min(rr[m].src - tmin8, 8u * W);
+          const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + o);
+          const unsigned long long rpw =
+              *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
+          nd[m] = d + rr[m].weight;  // times(d, w) for finite w >= 0 (:108)
+          bpk[m] = (uint32_t)rpw | rr[m].y | o;
+          ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | rr[m].y | o);
+          b = fmin(b, nd[m]);
+          wpos |= (rr[m].weight > 0.0 ? 1u : 0u) << m;
+          if (want_work) relax += (uint32_t)__popcll(__ballot((uint32_t)rpw < kLpAbsent));
+        }
+        uint32_t c = kEmptyKey;
+#pragma unroll
+        for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? bpk[m] : kEmptyKey);
+        uint32_t ra = rec0 + ((c >> 13) & 15u);
+        if (hubs) {  // the further blocks: first toucher, distance, back-pointer
+          for (uint32_t x = 1;; ++x) {
+            if (!__ballot(nb > x)) break;
+            const uint32_t rxx = block_rec(x);
+#pragma unroll
+            for (int m = 0; m < KP; ++m) {
+              const RevRec r2 = rv.rrec[rxx + m];
+              const uint32_t o = min(r2.src - tmin8, 8u * W);
+              const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + o);
+              const unsigned long long rpw =
+                  *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
+              const double n2 = d + r2.weight;
+              const uint32_t p2 = (uint32_t)rpw | r2.y | o;
+              ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | r2.y | o);
+              if (n2 < b || (n2 == b && p2 < c)) {
+                b = n2;
+                c = p2;
+                ra = rxx + m;
+              }
+              if (want_work) relax += (uint32_t)__popcll(__ballot((uint32_t)rpw < kLpAbsent));
+            }
+          }
+        }
+        uint32_t tpos = 0;  // a tight in-arc of positive weight (block 0; hubs: below)
+#pragma unroll
+        for (int m = 0; m < KP; ++m) tpos |= (nd[m] == b && ((wpos >> m) & 1u)) ? 1u : 0u;
+        const bool pres = ff < kLpAbsent;
+        // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
+        const uint32_t ou = pres ? (ff & 0x1FFFu) : 8u * W;
+        const double du = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + ou);
+        const double tbu = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + ou);
+        const uint32_t ruu =
+            (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ou) >> 32) &
+            kLpRunMask;
+        const double tx = du;
+        const uint32_t rx = 1u + (tbu == tx ? ruu : 0u);
+        // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
+        // source certified by (tb, run)
+        if (check_c && __ballot(pres && (!tpos || nb > 1))) {
+          bool cert = !pres || tpos;
+#pragma unroll
+          for (int m = 0; m < KP; ++m) {
+            const uint32_t o = bpk[m] & 0x1FFFu;
+            const double tbm = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + o);
+            const uint32_t rm =
+                (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
+                kLpRunMask;
+            cert |= nd[m] == b && (tbm < tx || (tbm == tx && rm < rx));
+          }
+          if (hubs) {  // the further blocks' tight in-arcs
+            for (uint32_t x = 1;; ++x) {
+              if (!__ballot(nb > x)) break;
+              const uint32_t rxx = block_rec(x);
+#pragma unroll
+              for (int m = 0; m < KP; ++m) {
+                const RevRec r2 = rv.rrec[rxx + m];
+                const uint32_t o = min(r2.src - tmin8, 8u * W);
+                const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + o);
+                const double tbm = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + o);
+                const uint32_t rm =
+                    (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
+                    kLpRunMask;
+                cert |= d + r2.weight == b &&
+                        (r2.weight > 0.0 || tbm < tx || (tbm == tx && rm < rx));
+              }
+            }
+          }
+          uncert |= !cert;
+        }
+        fst[e] = ff;
+        bd[e] = b;
+        bk[e] = c;
+        bra[e] = ra;
+        tbx[e] = tx;
+        runx[e] = rx;
+        if (pres) {
+          const uint32_t key = ff >> 17;  // pop rank << 3 | j
+          atomicOr(&S.bits[key >> 6], 1ull << (key & 63u));
+        }
+      }
+      wave_lds_sync();
+
+      // ---- (P2) id ranks of the next layer: popcount prefix over the first keys ----
+      const uint32_t nw = (n_cur * 8 + 63) / 64;
+      unsigned long long word = 0;
+      if (lane < nw) word = S.bits[lane];
+      const uint32_t pc = (uint32_t)__popcll(word);
+      const uint32_t inc = wave_incl_scan_dpp(pc);
+      const uint32_t n_next = __builtin_amdgcn_readlane(inc, 63);
+      if (lane < nw) {
+        S.pre[lane] = make_uint4(inc - pc, 0u, (uint32_t)word, (uint32_t)(word >> 32));
+        S.bits[lane] = 0;
+      }
+      wave_lds_sync();
+      // an uncertified tuple: the rounds engine takes the string
+      if (__ballot(uncert)) {
+        fail = kPathOverflow;
+        break;
+      }
+      if (n_next == 0) {
+        n_cur = 0;
+        break;
+      }
+
+      // ---- (P3) the next layer's cells (pop ranks after the sort), back records ----
+      const bool last = k + 1 == L;
+      const uint32_t rows_w = max(rows_n, (wk + 63) / 64);
+      uint32_t lo_slot = kEmptyKey, hi_slot = 0;
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        if ((uint32_t)e >= rows_w) continue;
+        const uint32_t i = (uint32_t)e * 64 + lane;
+        const bool pres = (uint32_t)e < rows_n && fst[e] < kLpAbsent;
+        uint32_t rank = 0;
+        if ((uint32_t)e < rows_n) {
+          const uint32_t key = pres ? fst[e] >> 17 : 0u;
+          const uint4 p = S.pre[key >> 6];
+          const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
+          rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
+        }
+        S.d[i] = pres ? bd[e] : kInf;
+        S.tb[i] = pres ? tbx[e] : kInf;
+        // pop rank: identity until the sort below fills it in
+        S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
+        if (pres) S.ord[0][rank] = (uint16_t)i;
+        const unsigned long long pm = __ballot(pres);
+        if (pm) {
+          lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
+          hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
+        }
+        if (pres) {
+          back[FB(nbase + i, lp.back_cap, 71)] = make_uint2(bra[e], base + ((bk[e] & 0x1FFFu) >> 3));
+          if (last) {  // best final: lexmin (total, id) (compose-shortest-path.zig:165-179)
+            const uint32_t t = tn + i;
+            const double fw2 = rhs.final_w[FB(t, rhs.num_states, 72)];
+            if (!w_is_zero(fw2)) {
+              const unsigned long long kk = okey(bd[e] + fw2);
+              const uint32_t pp = (rank << 9) | i;
+              if (kk < mykey || (kk == mykey && pp < myp)) {
+                mykey = kk;
+                myp = pp;
+                myfw = fw2;
+              }
+            }
+          }
+        }
+      }
+      wave_lds_sync();
+
+      // ---- (P4) pop ranks: stable sort of the id order by distance (LSD, one bit per
+      // pass, only the bits that differ) ----
+      if (!last && n_next > 1) {
+        const uint32_t rows_s = (n_next + 63) / 64;
+        const unsigned long long k0 =
+            (unsigned long long)__double_as_longlong(S.d[S.ord[0][0]]);
+        unsigned long long diff = 0;
+        for (uint32_t q = lane; q < n_next; q += 64)
+          diff |= (unsigned long long)__double_as_longlong(S.d[S.ord[0][q]]) ^ k0;
+        unsigned long long vary = ((unsigned long long)__builtin_amdgcn_readfirstlane(
+                                       wave_or_u32((uint32_t)(diff >> 32))) << 32) |
+                                  __builtin_amdgcn_readfirstlane(wave_or_u32((uint32_t)diff));
+        uint32_t cur = 0;
+        while (vary) {
+          const uint32_t bit = (uint32_t)__builtin_ctzll(vary);
+          vary &= vary - 1;
+          uint32_t slot[EW], v[EW];
+          unsigned long long z[EW];
+          uint32_t Z = 0;
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {
+            slot[e] = 0;
+            v[e] = 0;
+            z[e] = 0;
+            if ((uint32_t)e >= rows_s) continue;
+            const uint32_t q = (uint32_t)e * 64 + lane;
+            const bool valid = q < n_next;
+            slot[e] = valid ? S.ord[cur][q] : 0u;
+            const unsigned long long key = (unsigned long long)__double_as_longlong(S.d[slot[e]]);
+            v[e] = (uint32_t)(key >> bit) & 1u;
+            z[e] = __ballot(valid && !v[e]);
+            Z += (uint32_t)__popcll(z[e]);
+          }
+          uint32_t zb = 0, ob = 0;
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {
+            if ((uint32_t)e >= rows_s) continue;
+            const uint32_t q = (uint32_t)e * 64 + lane;
+            const bool valid = q < n_next;
+            const unsigned long long o = __ballot(valid && v[e]);
+            const uint32_t below0 = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(z[e] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)z[e], 0u));
+            const uint32_t below1 = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(o >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)o, 0u));
+            const uint32_t dst = v[e] ? Z + ob + below1 : zb + below0;
+            if (valid) S.ord[cur ^ 1u][dst] = (uint16_t)slot[e];
+            zb += (uint32_t)__popcll(z[e]);
+            ob += (uint32_t)__popcll(o);
+          }
+          cur ^= 1u;
+          wave_lds_sync();
+        }
+        for (uint32_t q = lane; q < n_next; q += 64) {  // pop rank q -> the cell's high word
+          const uint32_t sl = S.ord[cur][q];
+          const unsigned long long rpw = S.rp[sl];
+          S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
+        }
+        wave_lds_sync();
+      }
+      tmin = tn;
+      base = nbase;
+      wk = wn;
+      n_cur = n_next;
+      tuples += n_next;
+      cmin = tn + lo_slot;
+      cmax = tn + hi_slot;
+    }
+    wlast = wk;
+
+    if (fail != kPathOk) {
+      // leave every cell empty for the next string (a failed string may stop mid-layer)
+      wave_lds_sync();
+#pragma unroll 1
+      for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
+        S.d[i] = kInf;
+        S.rp[i] = kAbsent2;
+        S.tb[i] = kInf;
+      }
+      if (lane < (uint32_t)kWords) S.bits[lane] = 0;
+      wave_lds_sync();
+      wlast = 0;
+      if (lane == 0) write_status(out, si, fail, tuples, relax);
+      continue;
+    }
+    if (L == 0 && lane == 0) {
+      const double fw2 = rhs.final_w[rhs.start];
+      if (!w_is_zero(fw2)) {
+        mykey = okey(w_one() + fw2);
+        myp = 0;
+        myfw = fw2;
+      }
+    }
+    uint32_t bp;
+    double fw2;
+    if (n_cur == 0 || !wave_pick_best(S.best, S.bestp, lane, mykey, myp, myfw, bp, fw2)) {
+      if (lane == 0) write_status(out, si, kPathEmpty, tuples, relax);
+      continue;
+    }
+    unsigned long long o = 0;
+    if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
+    o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((uint32_t)o);
+    if (o + L > out.arc_cap) {
+      if (lane == 0) write_status(out, si, kPathOutputFull, tuples, relax);
+      continue;
+    }
+    if (lane == 0) {
+      ChaseJob& j = S.job[njobs];
+      j.si = si;
+      j.L = L;
+      j.id = base + (bp & 511u);
+      j.tuples = tuples;
+      j.relax = relax;
+      j.o = o;
+      j.off = off;
+      j.fw = fw2;
+    }
+    if (++njobs == (uint32_t)kChaseBatch) chase_batch();
+  }
+  if (njobs) chase_batch();
+}
+
+}  // namespace fstamd
