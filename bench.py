@@ -40,7 +40,7 @@ L2_PEAK_GBS = 34500.0  # MI355X aggregate L2 (MI355X_MICROARCH.md "L2 (per XCD)"
 
 
 EAGER_KERNEL = "eager_pull_kernel"     # tier P, takes every metric string
-LAZY_KERNEL = "lazy_layered_kernel"
+LAZY_KERNEL = "lazy_pull_kernel"
 
 
 def measured_traffic(args, sem):
@@ -305,7 +305,7 @@ def main():
         extra["lazy"] = {"value": args.lazy_batch * world / lel, "kernel_ms": float(np.mean(lk)),
                          "batch": args.lazy_batch,
                          "checked_vs_oracle": check_sample(lb, blob_check, F.FST_SEM_LAZY),
-                         "note": "fst_compose_frozen_shortest_path semantics (lazy_layered_kernel rounds engine)"}
+                         "note": "fst_compose_frozen_shortest_path semantics (lazy_pull_kernel, exact vs the oracle)"}
 
     if rank == 0:
         traffic, traffic_src = measured_traffic(args, sem)

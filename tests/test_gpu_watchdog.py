@@ -53,7 +53,7 @@ def _check_cycled(rhs_blob, uniq, reps, got, sem):
         assert np.all(bits(got.finals[idx]) == bits(ref.finals[j:j + 1])[0])
 
 
-@pytest.mark.parametrize("sem,reps", [(EAGER, 150000), (LAZY, 12000)])
+@pytest.mark.parametrize("sem,reps", [(EAGER, 150000), (LAZY, 60000)])
 def test_watchdog_is_per_string(sem, reps, monkeypatch):
     blob = O.freeze(O.gen("ambiguous", 4096, 12))
     rhs = F.Fst.from_bytes(blob)
@@ -65,9 +65,9 @@ def test_watchdog_is_per_string(sem, reps, monkeypatch):
         F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
     full_ms = F.last_launch_stats().kernel_ms
     wd_ms = int(full_ms / 3)
-    # each string must be far inside the limit (eager ~0.3 ms, lazy ~6 ms per string);
+    # each string must be far inside the limit (~0.3 ms per string in either pull tier);
     # otherwise this box is too fast for the batch and the test proves nothing
-    floor = 3 if sem == EAGER else 30
+    floor = 3
     assert wd_ms >= floor, f"launch {full_ms:.1f} ms too short to exercise the watchdog"
     monkeypatch.setenv("FSTAMD_WATCHDOG_MS", str(wd_ms))
     got = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
