@@ -47,7 +47,7 @@ struct LazyPullLds {
   double tb[W + 1];                // distance of the first toucher (-1: the start)
   unsigned long long bits[kWords];
   uint4 pre[kWords];
-  uint16_t ord[2][W];              // sort: slots in id order, then in pop order
+  uint32_t ord[2][W];              // sort: (key << 9 |) slot in id order, then pop order
   unsigned long long best;
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
@@ -371,7 +371,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         S.tb[i] = pres ? tbx[e] : kInf;
         // pop rank: identity until the sort below fills it in
         S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
-        if (pres) S.ord[0][rank] = (uint16_t)i;
+        if (pres) S.ord[0][rank] = i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -397,35 +397,73 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       wave_lds_sync();
 
       // ---- (P4) pop ranks: stable sort of the id order by distance (LSD, one bit per
-      // pass, only the bits that differ) ----
+      // pass, only the bits that differ).  Integer distances (integer weights, the
+      // metric's) are sorted as d - dmin packed above the slot: a handful of bits instead
+      // of the f64 pattern's exponent and mantissa bits ----
+#ifdef FSTAMD_LP_NOSORT  // timing experiment only: wrong pop ranks
+      if (false) {
+#else
       if (!last && n_next > 1) {
+#endif
         const uint32_t rows_s = (n_next + 63) / 64;
-        const unsigned long long k0 =
-            (unsigned long long)__double_as_longlong(S.d[S.ord[0][0]]);
-        unsigned long long diff = 0;
-        for (uint32_t q = lane; q < n_next; q += 64)
-          diff |= (unsigned long long)__double_as_longlong(S.d[S.ord[0][q]]) ^ k0;
-        unsigned long long vary = ((unsigned long long)__builtin_amdgcn_readfirstlane(
-                                       wave_or_u32((uint32_t)(diff >> 32))) << 32) |
-                                  __builtin_amdgcn_readfirstlane(wave_or_u32((uint32_t)diff));
+        double mn = kInf, mx = -kInf;
+        bool isint = true;
+        for (uint32_t q = lane; q < n_next; q += 64) {
+          const double d = S.d[S.ord[0][q]];
+          mn = fmin(mn, d);
+          mx = fmax(mx, d);
+          isint &= d == __builtin_trunc(d);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mn = fmin(mn, __shfl_xor(mn, o, 64));
+          mx = fmax(mx, __shfl_xor(mx, o, 64));
+        }
+        const bool ik = __ballot(!isint) == 0 && mx - mn < 8388608.0;  // keys < 2^23
+        unsigned long long vary;
+        if (ik) {
+          uint32_t acc = 0;
+          for (uint32_t q = lane; q < n_next; q += 64) {
+            const uint32_t sl = S.ord[0][q];
+            const uint32_t key = (uint32_t)(S.d[sl] - mn);  // exact: integers, < 2^23
+            S.ord[0][q] = (key << 9) | sl;
+            acc |= key;
+          }
+          vary = (unsigned long long)__builtin_amdgcn_readfirstlane(wave_or_u32(acc)) << 9;
+        } else {
+          const unsigned long long k0 =
+              (unsigned long long)__double_as_longlong(S.d[S.ord[0][0]]);
+          unsigned long long diff = 0;
+          for (uint32_t q = lane; q < n_next; q += 64)
+            diff |= (unsigned long long)__double_as_longlong(S.d[S.ord[0][q]]) ^ k0;
+          vary = ((unsigned long long)__builtin_amdgcn_readfirstlane(
+                      wave_or_u32((uint32_t)(diff >> 32))) << 32) |
+                 __builtin_amdgcn_readfirstlane(wave_or_u32((uint32_t)diff));
+        }
+        wave_lds_sync();
         uint32_t cur = 0;
         while (vary) {
           const uint32_t bit = (uint32_t)__builtin_ctzll(vary);
           vary &= vary - 1;
-          uint32_t slot[EW], v[EW];
+          uint32_t el[EW], v[EW];
           unsigned long long z[EW];
           uint32_t Z = 0;
 #pragma unroll
           for (int e = 0; e < EW; ++e) {
-            slot[e] = 0;
+            el[e] = 0;
             v[e] = 0;
             z[e] = 0;
             if ((uint32_t)e >= rows_s) continue;
             const uint32_t q = (uint32_t)e * 64 + lane;
             const bool valid = q < n_next;
-            slot[e] = valid ? S.ord[cur][q] : 0u;
-            const unsigned long long key = (unsigned long long)__double_as_longlong(S.d[slot[e]]);
-            v[e] = (uint32_t)(key >> bit) & 1u;
+            el[e] = valid ? S.ord[cur][q] : 0u;
+            if (ik) {
+              v[e] = (el[e] >> bit) & 1u;
+            } else {
+              const unsigned long long key =
+                  (unsigned long long)__double_as_longlong(S.d[el[e] & 511u]);
+              v[e] = (uint32_t)(key >> bit) & 1u;
+            }
             z[e] = __ballot(valid && !v[e]);
             Z += (uint32_t)__popcll(z[e]);
           }
@@ -441,7 +479,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t below1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(o >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)o, 0u));
             const uint32_t dst = v[e] ? Z + ob + below1 : zb + below0;
-            if (valid) S.ord[cur ^ 1u][dst] = (uint16_t)slot[e];
+            if (valid) S.ord[cur ^ 1u][dst] = el[e];
             zb += (uint32_t)__popcll(z[e]);
             ob += (uint32_t)__popcll(o);
           }
@@ -449,7 +487,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           wave_lds_sync();
         }
         for (uint32_t q = lane; q < n_next; q += 64) {  // pop rank q -> the cell's high word
-          const uint32_t sl = S.ord[cur][q];
+          const uint32_t sl = S.ord[cur][q] & 511u;
           const unsigned long long rpw = S.rp[sl];
           S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
         }
