@@ -36,6 +36,7 @@ namespace fstamd {
 constexpr uint32_t kLpAbsent = 0xFFF00000u;  // rank words of a slot that holds no tuple
 constexpr uint32_t kLpRunMask = 0xFFFu;      // run (<= 4095 layers) below the pop rank
 constexpr uint32_t kLpMaxLen = 4095;
+constexpr int kLpBins = 256;  // counting sort of the pop order: integer keys d - dmin < 256
 
 template <int W>
 struct LazyPullLds {
@@ -45,9 +46,20 @@ struct LazyPullLds {
   double d[W + 1];                 // distance (+inf: no tuple)
   unsigned long long rp[W + 1];    // lo: id rank << 20; hi: pop rank << 20 | run
   double tb[W + 1];                // distance of the first toucher (-1: the start)
-  unsigned long long bits[kWords];
-  uint4 pre[kWords];
-  uint32_t ord[2][W];              // sort: (key << 9 |) slot in id order, then pop order
+  uint32_t ord0[W];                // (key << 9 |) slot in id order
+  // P1-P3 and the split sort use {bits, pre, ord1}; the counting sort overlays {mask,
+  // hist} on them (bits lies under mask, which the counting sort leaves all zero)
+  union {
+    struct {
+      unsigned long long bits[kWords];
+      uint4 pre[kWords];
+      uint32_t ord1[W];            // split sort: the other buffer
+    };
+    struct {
+      unsigned long long mask[kLpBins];  // lanes of the current 64-chunk holding key b
+      uint32_t hist[kLpBins];            // running count of key b, then its prefix
+    };
+  };
   unsigned long long best;
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
@@ -371,7 +383,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         S.tb[i] = pres ? tbx[e] : kInf;
         // pop rank: identity until the sort below fills it in
         S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
-        if (pres) S.ord[0][rank] = i;
+        if (pres) S.ord0[rank] = i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -396,10 +408,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       }
       wave_lds_sync();
 
-      // ---- (P4) pop ranks: stable sort of the id order by distance (LSD, one bit per
-      // pass, only the bits that differ).  Integer distances (integer weights, the
-      // metric's) are sorted as d - dmin packed above the slot: a handful of bits instead
-      // of the f64 pattern's exponent and mantissa bits ----
+      // ---- (P4) pop ranks: stable sort of the id order by distance.  Integer distances
+      // (integer weights, the metric's) are keyed as d - dmin; keys < 256 take a counting
+      // sort, the rest a stable LSD split sort (one bit per pass, only the bits that
+      // differ; f64 bit patterns when the distances are not integers) ----
 #ifdef FSTAMD_LP_NOSORT  // timing experiment only: wrong pop ranks
       if (false) {
 #else
@@ -409,7 +421,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         double mn = kInf, mx = -kInf;
         bool isint = true;
         for (uint32_t q = lane; q < n_next; q += 64) {
-          const double d = S.d[S.ord[0][q]];
+          const double d = S.d[S.ord0[q]];
           mn = fmin(mn, d);
           mx = fmax(mx, d);
           isint &= d == __builtin_trunc(d);
@@ -420,25 +432,84 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           mx = fmax(mx, __shfl_xor(mx, o, 64));
         }
         const bool ik = __ballot(!isint) == 0 && mx - mn < 8388608.0;  // keys < 2^23
-        unsigned long long vary;
+#ifdef FSTAMD_LP_SPLIT_ONLY  // A/B: the split sort for every layer
+        const bool counting = false;
+#else
+        const bool counting = ik && mx - mn < (double)kLpBins;
+#endif
+        unsigned long long vary = 0;
         if (ik) {
           uint32_t acc = 0;
           for (uint32_t q = lane; q < n_next; q += 64) {
-            const uint32_t sl = S.ord[0][q];
+            const uint32_t sl = S.ord0[q];
             const uint32_t key = (uint32_t)(S.d[sl] - mn);  // exact: integers, < 2^23
-            S.ord[0][q] = (key << 9) | sl;
+            S.ord0[q] = (key << 9) | sl;
             acc |= key;
           }
           vary = (unsigned long long)__builtin_amdgcn_readfirstlane(wave_or_u32(acc)) << 9;
         } else {
           const unsigned long long k0 =
-              (unsigned long long)__double_as_longlong(S.d[S.ord[0][0]]);
+              (unsigned long long)__double_as_longlong(S.d[S.ord0[0]]);
           unsigned long long diff = 0;
           for (uint32_t q = lane; q < n_next; q += 64)
-            diff |= (unsigned long long)__double_as_longlong(S.d[S.ord[0][q]]) ^ k0;
+            diff |= (unsigned long long)__double_as_longlong(S.d[S.ord0[q]]) ^ k0;
           vary = ((unsigned long long)__builtin_amdgcn_readfirstlane(
                       wave_or_u32((uint32_t)(diff >> 32))) << 32) |
                  __builtin_amdgcn_readfirstlane(wave_or_u32((uint32_t)diff));
+        }
+        if (counting) {
+          // stable counting sort, 64 ids at a time in id order: the lanes holding key b
+          // meet in mask[b] (LDS OR), a lane's rank among them = the equal keys before
+          // it in the chunk; hist[b] carries the count from earlier chunks.  One wave's
+          // LDS operations complete in order, so the fences below separate the steps.
+#pragma unroll
+          for (int b = 0; b < kLpBins / 64; ++b) {
+            S.mask[b * 64 + lane] = 0;
+            S.hist[b * 64 + lane] = 0;
+          }
+          wave_lds_sync();
+          uint32_t ck[EW], cw[EW];
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {
+            ck[e] = 0;
+            cw[e] = 0;
+            if ((uint32_t)e >= rows_s) continue;  // uniform
+            const uint32_t q = (uint32_t)e * 64 + lane;
+            const bool valid = q < n_next;
+            ck[e] = valid ? S.ord0[q] : 0u;
+            const uint32_t key = ck[e] >> 9;
+            if (valid) atomicOr(&S.mask[key], 1ull << lane);
+            wave_lds_sync();
+            const unsigned long long peers = valid ? S.mask[key] : 0ull;
+            const uint32_t hb = valid ? S.hist[key] : 0u;
+            wave_lds_sync();
+            const unsigned long long lt = peers & ((1ull << lane) - 1ull);
+            cw[e] = hb + (uint32_t)__popcll(lt);
+            if (valid && lt == 0) {  // the key's first lane in this chunk
+              S.hist[key] = hb + (uint32_t)__popcll(peers);
+              S.mask[key] = 0;
+            }
+            wave_lds_sync();
+          }
+          // exclusive prefix of the counts: lane l holds keys 4l .. 4l+3
+          const uint4 h = reinterpret_cast<const uint4*>(S.hist)[lane];
+          const uint32_t s4 = h.x + h.y + h.z + h.w;
+          const uint32_t ex = wave_incl_scan_dpp(s4) - s4;
+          reinterpret_cast<uint4*>(S.hist)[lane] =
+              make_uint4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
+          wave_lds_sync();
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {  // pop rank -> the cell's high word
+            if ((uint32_t)e >= rows_s) continue;
+            if ((uint32_t)e * 64 + lane < n_next) {
+              const uint32_t q = S.hist[ck[e] >> 9] + cw[e];
+              const uint32_t sl = ck[e] & 511u;
+              const unsigned long long rpw = S.rp[sl];
+              S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
+            }
+          }
+          wave_lds_sync();
+          vary = 0;  // the split sort below has nothing to do
         }
         wave_lds_sync();
         uint32_t cur = 0;
@@ -456,7 +527,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             if ((uint32_t)e >= rows_s) continue;
             const uint32_t q = (uint32_t)e * 64 + lane;
             const bool valid = q < n_next;
-            el[e] = valid ? S.ord[cur][q] : 0u;
+            el[e] = valid ? (cur ? S.ord1 : S.ord0)[q] : 0u;
             if (ik) {
               v[e] = (el[e] >> bit) & 1u;
             } else {
@@ -479,15 +550,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t below1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(o >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)o, 0u));
             const uint32_t dst = v[e] ? Z + ob + below1 : zb + below0;
-            if (valid) S.ord[cur ^ 1u][dst] = el[e];
+            if (valid) (cur ? S.ord0 : S.ord1)[dst] = el[e];
             zb += (uint32_t)__popcll(z[e]);
             ob += (uint32_t)__popcll(o);
           }
           cur ^= 1u;
           wave_lds_sync();
         }
-        for (uint32_t q = lane; q < n_next; q += 64) {  // pop rank q -> the cell's high word
-          const uint32_t sl = S.ord[cur][q] & 511u;
+        for (uint32_t q = lane; q < n_next && !counting; q += 64) {  // pop rank q -> cell
+          const uint32_t sl = (cur ? S.ord1 : S.ord0)[q] & 511u;
           const unsigned long long rpw = S.rp[sl];
           S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
         }

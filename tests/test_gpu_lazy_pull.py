@@ -125,3 +125,50 @@ def test_fromBytes_blob_out_of_olabel_order_skips_the_tier(monkeypatch):
     monkeypatch.delenv("FSTAMD_LAZY_ONLY_FIRST")
     check(blob, labels, offsets, LAZY)
     assert np.all(got.status == F.FST_PATH_OK)
+
+
+def scaled_ambiguous(T, scale, stay=True):
+    # the reference bench's ambiguous chain (bench/optimize-bench.zig:250-277) with its
+    # weights b scaled: the pop-order keys d - dmin of a layer span ~3 k * scale
+    f = O.Fst()
+    for _ in range(T + 1):
+        f.add_state(0.0)
+    f.start = 0
+    for i in range(T + 1):
+        if stay:
+            f.add_arc(i, 1, 1, 0.0, i)
+        for b in range(4):
+            f.add_arc(i, 1, (i + b) % 255 + 1, float(b * scale), min(i + b + 1, T))
+    return f
+
+
+@pytest.mark.parametrize("scale", [1, 7, 40, 1000])
+def test_pop_order_sorts_counting_and_split(only_lp, scale):
+    # layers of up to 257 tuples (5 chunks of 64 ids): scale 1 keeps every layer's keys
+    # below 256 (the counting sort), 7 crosses 256 from layer ~13 on, 40 and 1000 use the
+    # split sort almost everywhere; every string must match the oracle
+    blob = O.freeze(scaled_ambiguous(300, scale))
+    seqs = [[1] * L for L in (1, 2, 9, 17, 40, 64, 70)] + [[1] * 64] * 8
+    got, took = run_lp(blob, seqs, expect_all=False)
+    assert took.mean() > 0.5, took.mean()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_wide_layers(only_lp, seed):
+    # ~100-300 states, two labels: layers of well over 64 tuples with many equal integer
+    # distances (chunks whose lanes share keys), some weights large enough to push the
+    # key range past 256
+    rng = np.random.default_rng(9900 + seed)
+    ns = int(rng.integers(100, 300))
+    f = O.Fst()
+    for _ in range(ns):
+        f.add_state(float(rng.integers(0, 3)) if rng.random() < 0.7 else math.inf)
+    f.start = 0
+    for s in range(ns):
+        for _ in range(int(rng.integers(1, 5))):
+            w = float(rng.integers(0, 3)) if rng.random() < 0.9 else float(rng.integers(50, 400))
+            f.add_arc(s, int(rng.integers(1, 3)), int(rng.integers(1, 9)), w,
+                      int(rng.integers(ns)))
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(1, 3, int(rng.integers(0, 30)))] for _ in range(96)]
+    run_lp(blob, seqs, expect_all=False)
