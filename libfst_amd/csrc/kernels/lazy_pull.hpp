@@ -31,6 +31,10 @@
 
 #include "eager_pull.hpp"  // RevView helpers, pull_group, wave_incl_scan_dpp, ChaseJob
 
+extern "C" __device__ double __ockl_wfred_min_f64(double);
+extern "C" __device__ double __ockl_wfred_max_f64(double);
+extern "C" __device__ unsigned long long __ockl_wfred_or_u64(unsigned long long);
+
 namespace fstamd {
 
 constexpr uint32_t kLpAbsent = 0xFFF00000u;  // rank words of a slot that holds no tuple
@@ -64,12 +68,6 @@ struct LazyPullLds {
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
 };
-
-__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-  return v;
-}
 
 template <int EW, int KP, bool DIRECT, int WAVES_PER_EU>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
@@ -363,8 +361,28 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         break;
       }
 
-      // ---- (P3) the next layer's cells (pop ranks after the sort), back records ----
+      // ---- (P3) the next layer's cells (pop ranks after the sort), back records, and
+      // P4's sort keys from the distances still in registers ----
       const bool last = k + 1 == L;
+      const bool sort = !last && n_next > 1;  // the last layer's pop order is never used
+      double mn = kInf, mx = -kInf;
+      bool nonint = false;
+#pragma unroll
+      for (int e = 0; e < EW; ++e) {
+        if ((uint32_t)e >= rows_n || fst[e] >= kLpAbsent) continue;
+        mn = fmin(mn, bd[e]);
+        mx = fmax(mx, bd[e]);
+        nonint |= bd[e] != __builtin_trunc(bd[e]);
+      }
+      bool ik = false;  // integer distances with d - dmin < 2^23: keys d - dmin
+      if (sort) {
+        mn = __ockl_wfred_min_f64(mn);
+        mx = __ockl_wfred_max_f64(mx);
+        ik = __ballot(nonint) == 0 && mx - mn < 8388608.0;
+      }
+      const unsigned long long mnb = (unsigned long long)__double_as_longlong(mn);
+      uint32_t kacc = 0;            // OR of the integer keys
+      unsigned long long diff = 0;  // OR of the f64 patterns' differences from dmin's
       const uint32_t rows_w = max(rows_n, (wk + 63) / 64);
       uint32_t lo_slot = kEmptyKey, hi_slot = 0;
 #pragma unroll
@@ -383,7 +401,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         S.tb[i] = pres ? tbx[e] : kInf;
         // pop rank: identity until the sort below fills it in
         S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
-        if (pres) S.ord0[rank] = i;
+        if (pres && sort) {
+          const uint32_t key = ik ? (uint32_t)(bd[e] - mn) : 0u;  // exact: integers < 2^23
+          S.ord0[rank] = (key << 9) | i;
+          kacc |= key;
+          diff |= ik ? 0ull : (unsigned long long)__double_as_longlong(bd[e]) ^ mnb;
+        }
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -415,47 +438,21 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #ifdef FSTAMD_LP_NOSORT  // timing experiment only: wrong pop ranks
       if (false) {
 #else
-      if (!last && n_next > 1) {
+      if (sort) {
 #endif
         const uint32_t rows_s = (n_next + 63) / 64;
-        double mn = kInf, mx = -kInf;
-        bool isint = true;
-        for (uint32_t q = lane; q < n_next; q += 64) {
-          const double d = S.d[S.ord0[q]];
-          mn = fmin(mn, d);
-          mx = fmax(mx, d);
-          isint &= d == __builtin_trunc(d);
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          mn = fmin(mn, __shfl_xor(mn, o, 64));
-          mx = fmax(mx, __shfl_xor(mx, o, 64));
-        }
-        const bool ik = __ballot(!isint) == 0 && mx - mn < 8388608.0;  // keys < 2^23
 #ifdef FSTAMD_LP_SPLIT_ONLY  // A/B: the split sort for every layer
         const bool counting = false;
 #else
         const bool counting = ik && mx - mn < (double)kLpBins;
 #endif
-        unsigned long long vary = 0;
+        unsigned long long vary;
         if (ik) {
-          uint32_t acc = 0;
-          for (uint32_t q = lane; q < n_next; q += 64) {
-            const uint32_t sl = S.ord0[q];
-            const uint32_t key = (uint32_t)(S.d[sl] - mn);  // exact: integers, < 2^23
-            S.ord0[q] = (key << 9) | sl;
-            acc |= key;
-          }
-          vary = (unsigned long long)__builtin_amdgcn_readfirstlane(wave_or_u32(acc)) << 9;
+          vary = (unsigned long long)__builtin_amdgcn_readfirstlane(__ockl_wfred_or_u32(kacc)) << 9;
         } else {
-          const unsigned long long k0 =
-              (unsigned long long)__double_as_longlong(S.d[S.ord0[0]]);
-          unsigned long long diff = 0;
-          for (uint32_t q = lane; q < n_next; q += 64)
-            diff |= (unsigned long long)__double_as_longlong(S.d[S.ord0[q]]) ^ k0;
-          vary = ((unsigned long long)__builtin_amdgcn_readfirstlane(
-                      wave_or_u32((uint32_t)(diff >> 32))) << 32) |
-                 __builtin_amdgcn_readfirstlane(wave_or_u32((uint32_t)diff));
+          const unsigned long long dv = __ockl_wfred_or_u64(diff);
+          vary = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(dv >> 32)) << 32) |
+                 __builtin_amdgcn_readfirstlane((uint32_t)dv);
         }
         if (counting) {
           // stable counting sort, 64 ids at a time in id order: the lanes holding key b
