@@ -636,6 +636,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     bool ran = false;
     HIP_TRY(run_lazy_dense(rhs, in, n, out, stream, &ran));
+    if (stats && !ran) stats->engine = 3;  // too large for the dense engine: rounds only
     if (!std::getenv("FSTAMD_DENSE_NOFALLBACK"))  // debug: leave UNSUPPORTED strings
       HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !ran, true));
     if (stats) {
@@ -911,6 +912,9 @@ hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput
 // (compacted when full; a string that still overflows goes to the rounds engine).  The
 // dense arrays are left clean by every string, so they are initialised only when
 // (re)allocated.  *ran = false when the lattice is too large for the engine at all.
+// LDS of a gfx950 workgroup is 160 KB; the kernel's static LdLds takes ~4.6 KB of it.
+constexpr size_t kLdMaxDynLds = 150 * 1024;
+
 hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                         const BatchOutDev& out, hipStream_t stream, bool* ran) {
   *ran = false;
@@ -922,7 +926,23 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     uint64_t dn;
     size_t lds;
   };
-  const uint64_t budget = 128ull << 30;  // of the 288 GB: latency-bound, so many waves
+  // Latency-bound: the waves in flight set the rate, and at large rhs (config 3, T =
+  // 65,536: ~0.9 GB per wave) memory caps them.  The budget is what HBM has free (the
+  // dense arrays already held count as free for them) less a 24 GB reserve, 90 % of it;
+  // 128 GB when the runtime cannot say.  Arrays above 128 GB are released after the call
+  // so that later calls of other engines find their memory.  FSTAMD_DENSE_BUDGET_GB sets it.
+  uint64_t budget = 128ull << 30;
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
+      uint64_t avail = fr;
+      for (size_t b : {kLdRec, kLdBarc, kLdIds, kLdLeaf, kLdFut}) avail += sizes_[b];
+      const uint64_t reserve = 24ull << 30;
+      budget = avail > 2 * reserve ? (avail - reserve) / 10 * 9 : avail / 2;
+    }
+    if (const char* be = std::getenv("FSTAMD_DENSE_BUDGET_GB"))
+      budget = (uint64_t)std::max(1, std::atoi(be)) << 30;
+  }
   const uint32_t max_waves = (uint32_t)num_cus_ * 16;
   const char* ge = std::getenv("FSTAMD_DENSE_GRID");  // debug: fewer waves
   auto make_plan = [&](uint32_t max_len, uint32_t count, Plan& p) -> bool {
@@ -931,8 +951,12 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     if (p.dn > kLdDenseMax) return false;
     p.nleaf = (uint32_t)((p.dn + 63) / 64);
     p.nsum = (p.nleaf + 63) / 64;
+    // dynamic LDS: the summary bitmap and the labels (config 3 at T = 65,536, L = 251:
+    // 65 KB; the waves in flight there are capped by HBM long before LDS)
     p.lds = (size_t)p.nsum * 8 + (size_t)p.lcap * 4;
-    if (p.lds > 48 * 1024) return false;
+    if (const char* le = std::getenv("FSTAMD_DENSE_LDS_MIN"))  // tests: a > 64 KB launch
+      p.lds = std::max<size_t>(p.lds, (size_t)std::max(0, std::atoi(le)));
+    if (p.lds > kLdMaxDynLds) return false;
     p.fcap = (uint32_t)std::max<uint64_t>(4096, p.dn / 4);
     const uint64_t per_wave = p.dn * (16 + 4 + 4) + (uint64_t)p.nleaf * 8 + (uint64_t)p.fcap * 16;
     p.grid = (uint32_t)std::min<uint64_t>(
@@ -1037,12 +1061,17 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     ws.nsum = p.nsum;
     ws.fcap = p.fcap;
     ws.wd_ticks = watchdog_ticks();
+    // + 10 us per dense tuple (s_memrealtime: 100 MHz), unless a test set the watchdog
+    ws.wd_tuple_ticks = std::getenv("FSTAMD_WATCHDOG_MS") ? 0ull : 1000ull;
     ws.items = d_order ? d_order + p.first : nullptr;
     ws.num_items = p.count;
     HIP_TRY(hipMemsetAsync(ctr + 33, 0, 4, stream));
 #ifdef FSTAMD_DEBUG_WAIT
     HIP_TRY(debug_trace_arm());
 #endif
+    if (p.lds > 64 * 1024)  // beyond the default dynamic-LDS limit of a launch
+      HIP_TRY(hipFuncSetAttribute((const void*)lazy_dense_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
     lazy_dense_kernel<<<p.grid, 64, p.lds, stream>>>(rhs.view, in, n, ctr + 33, ws, out);
     HIP_TRY(hipGetLastError());
 #ifdef FSTAMD_DEBUG_WAIT
@@ -1063,6 +1092,18 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
                  "[lazy-dense prof] grid %u items %llu | per item: pops %.0f advances %.1f "
                  "future entries scanned %.0f\n",
                  grid, sum[3], sum[0] / it, sum[1] / it, sum[2] / it);
+  }
+  uint64_t held = 0;
+  for (size_t b : {kLdRec, kLdBarc, kLdIds, kLdLeaf, kLdFut}) held += sizes_[b];
+  if (held > (128ull << 30)) {  // beyond the old fixed budget: give it back after the call
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (size_t b : {kLdRec, kLdBarc, kLdIds, kLdLeaf, kLdFut}) {
+      (void)hipFree(bufs_[b]);
+      bufs_[b] = nullptr;
+      sizes_[b] = 0;
+    }
+    ld_clean_ = nullptr;
+    ld_leaf_ = nullptr;
   }
   return hipSuccess;
 }

@@ -9,7 +9,11 @@
 // rounds engines degenerate to one pop per round.  What makes a pop cheap here:
 //   * tuple (k, s2, f) -- input position, rhs state, filter (0, or 1 after an rhs
 //     epsilon; a chain without label 0 never reaches 2) -- lives at the dense index
-//     (k * NS + s2) * 2 + f: no hash, no probing.  rec[x] = {dist, id | settled, back
+//     (s2 * (L + 1) + k) * 2 + f: no hash, no probing.  State-major: on epsilon-dense
+//     lattices the pops sweep the rhs states with every input position open at once, so
+//     the live tuples of a wave stay in a few pages (position-major, they spread over
+//     L + 1 pages of 2 * NS * 16 B: at T = 65,536 with ~250 waves resident, TLB misses made
+//     a pop 6x slower).  rec[x] = {dist, id | settled, back
 //     source id}: one 16-B load answers getOrCreate and relax (:99-141) for a target;
 //   * the heap is split by distance.  With weights >= 0 the popped distances never
 //     decrease, and the reference pops min (dist, id) among open tuples (stale and
@@ -41,6 +45,10 @@
 #include "eager_wave.hpp"     // wave_lds_sync
 #include "lazy_wave.hpp"      // wave_fence, lanemask_lt
 
+extern "C" __device__ double __ockl_wfred_min_f64(double);
+extern "C" __device__ unsigned long long __ockl_wfred_or_u64(unsigned long long);
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
 namespace fstamd {
 
 struct LdWs {
@@ -49,9 +57,12 @@ struct LdWs {
   uint32_t* ids;              // [grid * dn] id -> dense index
   unsigned long long* leaf;   // [grid * nleaf] open-at-dcur bitmap over ids
   uint4* fut;                 // [grid * fcap] {dist lo, dist hi, dense index, 0}
-  unsigned long long dn;      // dense tuples per wave = (lcap + 1) * NS * 2
+  unsigned long long dn;      // dense tuples per wave = NS * (lcap + 1) * 2
   uint32_t nleaf, nsum, fcap, lcap;
   unsigned long long wd_ticks;
+  // the watchdog grows with the string's lattice: a pop takes ~2.5 us (4 us with every
+  // wave resident), and config 3 at T = 65,536 pops up to 33 M tuples per string
+  unsigned long long wd_tuple_ticks;
   unsigned long long* prof;   // [grid * 8] (FSTAMD_BFS_PROF): pops, advances, scanned, items
   const uint32_t* items;      // this launch's strings (a length bucket), or nullptr = all
   uint32_t num_items;         // entries of items (ignored when items is nullptr)
@@ -84,26 +95,19 @@ __device__ __forceinline__ uint4 ld_rec(double d, uint32_t id, uint32_t prev) {
   return make_uint4((uint32_t)b, (uint32_t)(b >> 32), id, prev);
 }
 
-__device__ __forceinline__ double wave_min_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double y = __shfl_xor(v, o, 64);
-    v = y < v ? y : v;
-  }
-  return v;
-}
+// Wave reductions over DPP (the ockl ones) and uniform-lane reads (v_readlane): no
+// ds_bpermute round trips on the pop's serial path.
+__device__ __forceinline__ double wave_min_f64(double v) { return __ockl_wfred_min_f64(v); }
 __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-  return v;
+  return __ockl_wfred_or_u64(v);
 }
-__device__ __forceinline__ uint32_t wave_min_u32d(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t y = __shfl_xor(v, o, 64);
-    v = y < v ? y : v;
-  }
-  return v;
+__device__ __forceinline__ uint32_t wave_min_u32d(uint32_t v) { return __ockl_wfred_min_u32(v); }
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) {  // l uniform
+  return __builtin_amdgcn_readlane(v, l);
+}
+__device__ __forceinline__ unsigned long long lane_read64(unsigned long long v, uint32_t l) {
+  return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+         __builtin_amdgcn_readlane((uint32_t)v, l);
 }
 // Leaf words are updated with L2 atomics (several lanes may set bits of one word in one
 // instruction), so they are read with agent-scope loads, which skip the vector L1.
@@ -157,12 +161,13 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
   unsigned long long* prof = V.prof;
   const unsigned long long t0 = V.t0;
   const uint32_t NS = rhs.num_states;
-  const uint32_t KS = 2 * NS;
+  const uint32_t LC = L + 1;  // the dense index's position stride (state-major)
   if (prof && lane == 0) prof[3] += 1;
-  const uint32_t nsum_s = (uint32_t)(((uint64_t)(L + 1) * KS + 4095) / 4096);
+  const uint32_t nsum_s = (uint32_t)(((uint64_t)LC * 2 * NS + 4095) / 4096);
+  const unsigned long long wd = ws.wd_ticks + (uint64_t)LC * 2 * NS * ws.wd_tuple_ticks;
 
   // ---- init tuple (fst1.start, fst2.start, 0), id 0, dist One (:146-153) ----
-  const uint32_t x0 = 2 * rhs.start;
+  const uint32_t x0 = 2 * rhs.start * LC;
   if (lane == 0) {
     R[x0] = ld_rec(w_one(), 0u, kLdNoPrev);
     ids[0] = x0;
@@ -204,7 +209,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
     // ---- the lowest open id at dcur ----
     bool have = uni(cache && cur_bits != 0ull ? 1u : 0u) != 0u;
     while (!have) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > wd) {
         fail = kPathInternal;
         site = 1;
         break;
@@ -216,7 +221,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
         const unsigned long long nz = __ballot(v != 0ull);
         if (nz) {
           const uint32_t l = (uint32_t)__ffsll((long long)nz) - 1;
-          const unsigned long long vv = uni64(__shfl(v, (int)l, 64));
+          const unsigned long long vv = lane_read64(v, l);
           scur = s0 + l;
           found = (s0 + l) * 64 + (uint32_t)__ffsll((long long)vv) - 1;
           break;
@@ -297,13 +302,13 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
     }
     ++pops;
     FT(item, si, pops, 3);
-    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {
+    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > wd) {
       fail = kPathInternal;
       site = 2;
       break;
     }
-    const uint32_t k = x / KS;
-    const uint32_t s = (x - k * KS) >> 1;
+    const uint32_t s = (x >> 1) / LC;
+    const uint32_t k = (x >> 1) - s * LC;
     if (k > L || s >= NS || pid >= nn) {  // invariant guard: never walk on garbage
       fail = kPathInternal;
       site = 3;
@@ -343,7 +348,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
       if (p1 || p3) {
         const uint32_t rank = p1 ? (uint32_t)__popcll(m1 & lanemask_lt())
                                  : n1 + (uint32_t)__popcll(m3 & lanemask_lt());
-        S.x[rank] = p1 ? (k + 1) * KS + 2 * r.next : k * KS + 2 * r.next + 1;
+        S.x[rank] = p1 ? 2 * (r.next * LC + k + 1) : 2 * (r.next * LC + k) + 1;
         S.a[rank] = aoff + lane;
         S.il[rank] = il;
         S.ol[rank] = r.olabel;
@@ -369,7 +374,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
           const bool p1 = c < n1;
           const uint32_t a = p1 ? lo1 + c : lo3 + (c - n1);
           const ArcRec r = rhs.rec[a];
-          S.x[lane] = p1 ? (k + 1) * KS + 2 * r.next : k * KS + 2 * r.next + 1;
+          S.x[lane] = p1 ? 2 * (r.next * LC + k + 1) : 2 * (r.next * LC + k) + 1;
           S.a[lane] = a;
           S.il[lane] = p1 ? label : kEpsilon;
           S.ol[lane] = r.olabel;
@@ -411,7 +416,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
         unsigned long long pend = __ballot(act);
         while (pend) {
           const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
-          const uint32_t xl = __shfl(tx, (int)l, 64);
+          const uint32_t xl = lane_read(tx, l);
           const unsigned long long m = __ballot(act && tx == xl);
           if (lane == l) gmask = m;
           pend &= ~m;

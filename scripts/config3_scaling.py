@@ -13,6 +13,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -33,9 +34,23 @@ def main():
     ap.add_argument("--ts", default="4096,16384,65536")
     ap.add_argument("--n", type=int, default=4)
     ap.add_argument("--cpu-max-t", type=int, default=16384)
+    ap.add_argument("--len", type=int, default=0, help="fixed string length (probes)")
+    ap.add_argument("--cpu-n", type=int, default=0,
+                    help="also time the CPU port on the first N strings (--cpu-threads)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
+    # a launch at T = 65,536 runs for minutes without returning: say so every 30 s (gpurun
+    # takes 3 silent minutes for a hang)
+    t_start = time.perf_counter()
+
+    def heartbeat():
+        while True:
+            time.sleep(30)
+            print(f"# still running, {time.perf_counter() - t_start:.0f} s", flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     rng = np.random.default_rng(0x5EED)
-    lens = rng.integers(11, 252, a.n)
+    lens = rng.integers(11, 252, a.n) if a.len == 0 else np.full(a.n, a.len)
     for T in [int(x) for x in a.ts.split(",")]:
         fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, 12)
         blob = D.blob_bytes(fz)
@@ -66,6 +81,14 @@ def main():
             line["cpu_kind"] = "port (oracle/fst_oracle.c -O3), 1 thread, first string"
             line["parity_first_string"] = bool(got_ok and ref.empty[0] == 0 and int(
                 b.plen[0].item()) == int(ref.offsets[1] - ref.offsets[0]))
+        if a.cpu_n > 0:
+            cl = [int(x) for x in lens[:a.cpu_n]]
+            labels = np.ones(sum(cl), np.uint32)
+            offs = np.concatenate([[0], np.cumsum(cl)]).astype(np.uint64)
+            secs, _ = O.batch_time(blob, labels, offs, 0, a.cpu_threads)
+            line["cpu_strings_per_s"] = len(cl) / secs
+            line["cpu_sample"] = (f"first {len(cl)} strings, {a.cpu_threads} threads, "
+                                  "oracle/fst_oracle.c -O3 (port), lazy")
         line["lengths"] = f"{len(lens)} strings, L uniform 11..251 (seed 0x5EED), first {list(map(int, lens[:4]))}"
         line["status"] = {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))}
         print(json.dumps(line), flush=True)

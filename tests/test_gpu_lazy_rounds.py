@@ -149,3 +149,15 @@ def test_dense_length_buckets(monkeypatch, buckets):
     seqs = [[int(x) for x in rng.integers(0 if i % 9 == 0 else 1, 4, int(rng.integers(0, 14)))]
             for i in range(64)]
     check(blob, *csr(seqs), LAZY)
+
+
+def test_dense_replay_beyond_64k_lds(monkeypatch):
+    # config 3 at full size (T = 65,536, L up to 251) needs ~65 KB of dynamic LDS for the
+    # dense replay's summary bitmap; such a launch goes past HIP's default 64 KB limit.
+    # FSTAMD_DENSE_LDS_MIN inflates a small launch to 100 KB: the engine must still run
+    # (engine 5, not the rounds fallback) and be exact
+    monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "dense")
+    monkeypatch.setenv("FSTAMD_DENSE_LDS_MIN", "100000")
+    blob = O.freeze(O.gen("eps_dense", 256, 12))
+    check(blob, *csr([[1] * L for L in (0, 3, 11, 24, 40)]), LAZY)
+    assert F.last_launch_stats().engine == 5
