@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -118,14 +119,69 @@ bool gpu_available() {
   return ok == 1;
 }
 
-// RAII device buffer
+// Device buffers of the batch calls come from a per-process pool of power-of-two blocks:
+// hipMalloc / hipFree of tens of MB per call (inputs, arena, CSR results) cost up to
+// ~20 ms of host time a call, and hipFree synchronises the device.  Every DevBuf user
+// synchronises before the buffer goes back, so a block is never reused while a kernel
+// still runs on it.  Blocks beyond kPoolMax bytes held are freed instead; fst_teardown
+// empties the pool.
+constexpr size_t kPoolMax = 16ull << 30;
+struct BufPool {
+  std::mutex mu;
+  std::multimap<std::pair<int, size_t>, void*> free;
+  size_t held = 0;
+};
+BufPool& buf_pool() {
+  static BufPool* p = new BufPool;  // never destroyed: DevBufs may outlive static teardown
+  return *p;
+}
+void pool_clear() {
+  BufPool& P = buf_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  for (auto& kv : P.free) {
+    (void)hipSetDevice(kv.first.first);
+    (void)hipFree(kv.second);
+  }
+  P.free.clear();
+  P.held = 0;
+}
+
+// RAII device buffer (pooled)
 struct DevBuf {
   void* p = nullptr;
+  size_t cls = 0;
+  int dev = 0;
   explicit DevBuf(size_t n) {
-    if (hipMalloc(&p, std::max<size_t>(n, 16)) != hipSuccess) p = nullptr;
+    cls = 4096;
+    while (cls < n) cls <<= 1;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    BufPool& P = buf_pool();
+    {
+      std::lock_guard<std::mutex> g(P.mu);
+      auto it = P.free.find({dev, cls});
+      if (it != P.free.end()) {
+        p = it->second;
+        P.free.erase(it);
+        P.held -= cls;
+        return;
+      }
+    }
+    if (hipMalloc(&p, cls) != hipSuccess) p = nullptr;
   }
   ~DevBuf() {
-    if (p) (void)hipFree(p);
+    if (!p) return;
+    BufPool& P = buf_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    if (P.held + cls <= kPoolMax) {
+      P.free.insert({{dev, cls}, p});
+      P.held += cls;
+    } else {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+      (void)hipSetDevice(cur);
+    }
   }
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -297,8 +353,31 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
                              std::unique_ptr<DevOut>* keep);
 
 // Chain batch on the GPU from host arrays; fills `h` in input order.
+// FSTAMD_HOST_PROF=1: wall time per host phase of the batch calls, printed to stderr at
+// the end of each call (where a host API call spends its time beside the kernels).
+struct HostProf {
+  bool on = std::getenv("FSTAMD_HOST_PROF") != nullptr;
+  double ms[8] = {};  // inputs H2D, output alloc, engine + sync, download, project, result
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(int i) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    ms[i] += std::chrono::duration<double, std::milli>(n - t).count();
+    t = n;
+  }
+  void print(const char* what) const {
+    if (!on) return;
+    std::fprintf(stderr,
+                 "[libfst_amd host] %s: inputs %.2f alloc %.2f engine %.2f download %.2f "
+                 "project %.2f result %.2f ms\n",
+                 what, ms[0], ms[1], ms[2], ms[3], ms[4], ms[5]);
+  }
+};
+thread_local HostProf* t_prof = nullptr;
+
 FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
-                              uint32_t num, uint32_t n, int semantics, int dev, HostPaths* h) {
+                              uint32_t num, uint32_t n, int semantics, int dev, HostPaths* h,
+                              std::unique_ptr<DevOut>* keep = nullptr) {
   if (dev < 0) dev = current_device();
   if (dev < 0) return FST_INVALID_ARG;
   if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
@@ -317,7 +396,52 @@ FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64
   if (hipMemcpy(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice) != hipSuccess)
     return FST_OOM;
   ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
-  return run_chain_batch_dev(*D, in, total, n, semantics, dev, h, nullptr);
+  if (t_prof) t_prof->lap(0);
+  return run_chain_batch_dev(*D, in, total, n, semantics, dev, h, keep);
+}
+
+// The batch result straight from the device outputs: compacted to CSR on the device
+// (DeviceEngine::compact_paths), then one copy per array into the caller's result.
+// `fail` (device, optional): a pipeline's first failing stage per string.
+FstError download_batch_result(int dev, const DevOut& o, uint32_t num, const int32_t* fail,
+                               FstBatchResult* out) {
+  unsigned long long used = 0;
+  if (hipMemcpy(&used, o.cursor.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
+  used = std::min<unsigned long long>(used, o.v.arc_cap);
+  DevBuf st(num * 4ull), off((num + 1ull) * 8), fin(num * 8ull), il(used * 4), ol(used * 4),
+      w(used * 8);
+  if (!st.p || !off.p || !fin.p || !il.p || !ol.p || !w.p) return FST_OOM;
+  uint64_t tot = 0;
+  {
+    DeviceEngine& E = DeviceEngine::get(dev);
+    std::lock_guard<std::mutex> lk(E.mutex());
+    if (E.compact_paths(o.v, num, fail, (int32_t*)st.p, (uint64_t*)off.p, (uint32_t*)il.p,
+                        (uint32_t*)ol.p, (double*)w.p, (double*)fin.p, &tot, nullptr) != hipSuccess)
+      return FST_OOM;
+  }
+  if (tot > used) return FST_OOM;  // cannot happen: OK paths are in the arena
+  if (t_prof) t_prof->lap(4);
+  out->num_strings = num;
+  out->total_arcs = tot;
+  out->status = (int32_t*)std::malloc(std::max<size_t>(num, 1) * 4);
+  out->path_offsets = (uint64_t*)std::malloc((num + 1ull) * 8);
+  out->final_weights = (double*)std::malloc(std::max<size_t>(num, 1) * 8);
+  out->ilabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
+  out->olabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
+  out->weights = (double*)std::malloc(std::max<uint64_t>(tot, 1) * 8);
+  if (!out->status || !out->path_offsets || !out->final_weights || !out->ilabels ||
+      !out->olabels || !out->weights)
+    return FST_OOM;
+  if ((num && (hipMemcpy(out->status, st.p, num * 4ull, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(out->final_weights, fin.p, num * 8ull, hipMemcpyDeviceToHost) !=
+                   hipSuccess)) ||
+      hipMemcpy(out->path_offsets, off.p, (num + 1ull) * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      (tot && (hipMemcpy(out->ilabels, il.p, tot * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(out->olabels, ol.p, tot * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+               hipMemcpy(out->weights, w.p, tot * 8, hipMemcpyDeviceToHost) != hipSuccess)))
+    return FST_OOM;
+  if (t_prof) t_prof->lap(3);
+  return FST_OK;
 }
 
 // One batch on device inputs; the path arena grows on OUTPUT_FULL.  With `keep` the
@@ -334,11 +458,14 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
   std::lock_guard<std::mutex> lk(E.mutex());
   constexpr int kAttempts = 6;
   for (int attempt = 0; attempt < kAttempts; ++attempt, arc_cap *= 4) {
+    if (t_prof) t_prof->lap(7);
     auto out = std::make_unique<DevOut>(num, arc_cap);
     if (!out->ok()) return FST_OOM;
+    if (t_prof) t_prof->lap(1);
     LaunchStats st;
     hipError_t err = E.run_chain(D, in, n, semantics, out->v, nullptr, &st);
     if (err == hipSuccess) err = hipDeviceSynchronize();
+    if (t_prof) t_prof->lap(2);
     if (err != hipSuccess) {
       std::fprintf(stderr, "[libfst_amd] batch engine failed: %s\n", hipGetErrorString(err));
       return FST_OOM;
@@ -353,6 +480,7 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
     } else if (!out->download(num, h)) {
       return FST_OOM;
     }
+    if (t_prof) t_prof->lap(3);
     for (uint32_t i = 0; i < num; ++i) full |= h->status[i] == kPathOutputFull;
     // The last attempt's result stands: strings still OUTPUT_FULL keep that status (the
     // caller sees FST_PATH_OUTPUT_FULL per string), and `keep` is always set on FST_OK.
@@ -362,35 +490,6 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
     }
   }
   return FST_OOM;  // unreachable: the last attempt returns above
-}
-
-// HostPaths (engine order) -> FstBatchResult (malloc'ed CSR, fst_batch_result_free).
-void fill_batch_result(const HostPaths& h, uint32_t num_strings, FstBatchResult* out) {
-  out->num_strings = num_strings;
-  out->status = (int32_t*)std::malloc(std::max<size_t>(num_strings, 1) * 4);
-  out->path_offsets = (uint64_t*)std::malloc((num_strings + 1ull) * 8);
-  out->final_weights = (double*)std::malloc(std::max<size_t>(num_strings, 1) * 8);
-  uint64_t tot = 0;
-  for (uint32_t i = 0; i < num_strings; ++i) {
-    out->path_offsets[i] = tot;
-    if (h.status[i] == kPathOk) tot += h.len[i];
-  }
-  out->path_offsets[num_strings] = tot;
-  out->total_arcs = tot;
-  out->ilabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
-  out->olabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
-  out->weights = (double*)std::malloc(std::max<uint64_t>(tot, 1) * 8);
-  for (uint32_t i = 0; i < num_strings; ++i) {
-    out->status[i] = h.status[i];
-    out->final_weights[i] = h.status[i] == kPathOk ? h.fin[i] : w_zero();
-    if (h.status[i] != kPathOk) continue;
-    const uint64_t o = out->path_offsets[i];
-    for (uint32_t k = 0; k < h.len[i]; ++k) {
-      out->ilabels[o + k] = h.il[h.off[i] + k];
-      out->olabels[o + k] = h.ol[h.off[i] + k];
-      out->weights[o + k] = h.w[h.off[i] + k];
-    }
-  }
 }
 
 }  // namespace
@@ -765,9 +864,12 @@ int32_t fst_print_output_string(FstMutableHandle handle, uint8_t* buf, uint32_t 
 }
 
 void fst_teardown(void) {
-  std::lock_guard<std::mutex> g(g_api_mu);
-  g_mut.clear();
-  g_fst.clear();
+  {
+    std::lock_guard<std::mutex> g(g_api_mu);
+    g_mut.clear();
+    g_fst.clear();
+  }
+  pool_clear();
 }
 
 // ---- Batched entries (fst_batch.h) ----------------------------------------------------
@@ -789,11 +891,27 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   if (!b) return FST_INVALID_ARG;
   if (!gpu_available()) return FST_INVALID_ARG;
   const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
-  const int dev = opts ? opts->device : -1;
+  int dev = opts ? opts->device : -1;
+  if (dev < 0) dev = current_device();
+  if (dev < 0 || hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  HostProf prof;
+  t_prof = &prof;
+  struct ProfScope {
+    ~ProfScope() { t_prof = nullptr; }
+  } prof_scope;
   HostPaths h;
-  FstError e = run_chain_batch_host(*b, labels, offsets, num_strings, n, semantics, dev, &h);
+  std::unique_ptr<DevOut> keep;
+  FstError e =
+      run_chain_batch_host(*b, labels, offsets, num_strings, n, semantics, dev, &h, &keep);
   if (e != FST_OK) return e;
-  fill_batch_result(h, num_strings, out);
+  if (!keep) return FST_OOM;
+  e = download_batch_result(dev, *keep, num_strings, nullptr, out);
+  if (e != FST_OK) {
+    fst_batch_result_free(out);
+    return e;
+  }
+  prof.lap(5);
+  prof.print("fst_compose_frozen_shortest_path_batch");
   return FST_OK;
 }
 
@@ -848,6 +966,11 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
   const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
   int dev = opts && opts->device >= 0 ? opts->device : current_device();
   if (dev < 0 || hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  HostProf prof;
+  t_prof = &prof;
+  struct ProfScope {
+    ~ProfScope() { t_prof = nullptr; }
+  } prof_scope;
   // stage-1 inputs
   const uint64_t total = num_strings ? offsets[num_strings] - offsets[0] : 0;
   uint32_t max_len = 0;
@@ -861,19 +984,21 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
     return FST_OOM;
   if (hipMemcpy(off->p, rebased.data(), (num_strings + 1ull) * 8, hipMemcpyHostToDevice) != hipSuccess)
     return FST_OOM;
-  std::vector<int32_t> fail(num_strings, kPathOk);  // first failing stage's status
+  DevBuf fail(num_strings * 4ull);  // first failing stage's status, per string (device)
+  if (!fail.p || hipMemset(fail.p, 0, num_strings * 4ull) != hipSuccess) return FST_OOM;
   uint64_t in_total = total;
   HostPaths h;
+  std::unique_ptr<DevOut> keep;
+  prof.lap(0);
   for (uint32_t k = 0; k < num_stages; ++k) {
     DeviceFst* D = fs[k]->device(dev);
     if (!D) return FST_OOM;
     ChainInput in{(const uint32_t*)lab->p, (const uint64_t*)off->p, num_strings, max_len};
-    const bool last = k + 1 == num_stages;
-    std::unique_ptr<DevOut> keep;
-    FstError e = run_chain_batch_dev(*D, in, in_total, n, semantics, dev, &h, last ? nullptr : &keep);
+    keep.reset();
+    FstError e = run_chain_batch_dev(*D, in, in_total, n, semantics, dev, &h, &keep);
     if (e != FST_OK) return e;
-    if (last) break;
     if (!keep) return FST_OOM;  // run_chain_batch_dev sets it on FST_OK; never dereference null
+    if (k + 1 == num_stages) break;
     // project this stage's outputs into the next stage's inputs, on the device
     unsigned long long used = 0;
     if (hipMemcpy(&used, keep->v.cursor, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
@@ -885,25 +1010,26 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
       DeviceEngine& E = DeviceEngine::get(dev);
       std::lock_guard<std::mutex> lk(E.mutex());
       if (E.project_output(keep->v, num_strings, (uint32_t*)nlab->p, (uint64_t*)noff->p,
-                           (int32_t*)pst.p, &max_len, nullptr) != hipSuccess)
+                           (int32_t*)pst.p, &max_len, nullptr) != hipSuccess ||
+          E.merge_status((int32_t*)fail.p, (const int32_t*)pst.p, num_strings, nullptr) !=
+              hipSuccess)
         return FST_OOM;
     }
-    std::vector<int32_t> ps(num_strings);
-    if (num_strings &&
-        hipMemcpy(ps.data(), pst.p, num_strings * 4ull, hipMemcpyDeviceToHost) != hipSuccess)
-      return FST_OOM;
-    for (uint32_t i = 0; i < num_strings; ++i)
-      if (fail[i] == kPathOk && ps[i] != kPathOk) fail[i] = ps[i];
-    uint64_t nt = 0;
+    uint64_t nt = 0;  // (synchronises: pst may go back to the pool)
     if (hipMemcpy(&nt, (uint64_t*)noff->p + num_strings, 8, hipMemcpyDeviceToHost) != hipSuccess)
       return FST_OOM;
     in_total = nt;
     lab = std::move(nlab);
     off = std::move(noff);
+    prof.lap(4);
   }
-  for (uint32_t i = 0; i < num_strings; ++i)
-    if (fail[i] != kPathOk) h.status[i] = fail[i];
-  fill_batch_result(h, num_strings, out);
+  FstError e = download_batch_result(dev, *keep, num_strings, (const int32_t*)fail.p, out);
+  if (e != FST_OK) {
+    fst_batch_result_free(out);
+    return e;
+  }
+  prof.lap(5);
+  prof.print("fst_pipeline_batch");
   return FST_OK;
 }
 

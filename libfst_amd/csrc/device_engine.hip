@@ -1416,6 +1416,75 @@ hipError_t DeviceEngine::project_output(const BatchOutDev& stage, uint32_t num,
   return hipStreamSynchronize(stream);
 }
 
+__global__ void csr_count_kernel(BatchOutDev s, uint32_t num, const int32_t* fail,
+                                 int32_t* status, uint64_t* counts, double* fin) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > num) return;
+  if (i == num) {  // the scan's last element: offsets[num] = the total
+    counts[num] = 0;
+    return;
+  }
+  int32_t st = s.status[i];
+  if (fail && fail[i] != kPathOk) st = fail[i];
+  status[i] = st;
+  const bool ok = st == kPathOk;
+  counts[i] = ok ? s.path_len[i] : 0u;
+  fin[i] = ok ? s.final_w[i] : w_zero();
+}
+
+// One wavefront per string (grid-stride): the lanes copy its arcs, coalesced on both sides.
+__global__ void __launch_bounds__(64) csr_gather_kernel(BatchOutDev s, uint32_t num,
+                                                        const int32_t* status,
+                                                        const uint64_t* offsets, uint32_t* il,
+                                                        uint32_t* ol, double* w) {
+  for (uint32_t i = blockIdx.x; i < num; i += gridDim.x) {
+    if (status[i] != kPathOk) continue;
+    const uint64_t src = s.path_off[i], dst = offsets[i];
+    const uint32_t L = s.path_len[i];
+    for (uint32_t k = threadIdx.x; k < L; k += 64) {
+      il[dst + k] = s.out_il[src + k];
+      ol[dst + k] = s.out_ol[src + k];
+      w[dst + k] = s.out_w[src + k];
+    }
+  }
+}
+
+__global__ void merge_status_kernel(int32_t* fail, const int32_t* st, uint32_t num) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < num && fail[i] == kPathOk && st[i] != kPathOk) fail[i] = st[i];
+}
+
+hipError_t DeviceEngine::compact_paths(const BatchOutDev& s, uint32_t num, const int32_t* fail,
+                                       int32_t* status, uint64_t* offsets, uint32_t* il,
+                                       uint32_t* ol, double* w, double* fin, uint64_t* total,
+                                       hipStream_t stream) {
+  HIP_TRY(hipSetDevice(dev_));
+  uint64_t* counts = (uint64_t*)scratch(kProjCount, ((size_t)num + 1) * 8 + 16);
+  if (!counts) return hipErrorOutOfMemory;
+  csr_count_kernel<<<(num + 256) / 256, 256, 0, stream>>>(s, num, fail, status, counts, fin);
+  HIP_TRY(hipGetLastError());
+  size_t tbytes = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, counts, offsets, num + 1, stream));
+  void* temp = scratch(kProjTemp, tbytes + 16);
+  if (!temp) return hipErrorOutOfMemory;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(temp, tbytes, counts, offsets, num + 1, stream));
+  if (num) {
+    const uint32_t grid = std::min<uint32_t>(num, (uint32_t)num_cus_ * 32);
+    csr_gather_kernel<<<grid, 64, 0, stream>>>(s, num, status, offsets, il, ol, w);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpyAsync(total, offsets + num, 8, hipMemcpyDeviceToHost, stream));
+  return hipStreamSynchronize(stream);
+}
+
+hipError_t DeviceEngine::merge_status(int32_t* fail, const int32_t* st, uint32_t num,
+                                      hipStream_t stream) {
+  HIP_TRY(hipSetDevice(dev_));
+  if (num) merge_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(fail, st, num);
+  HIP_TRY(hipGetLastError());
+  return hipSuccess;
+}
+
 hipError_t DeviceEngine::run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n,
                                    int semantics, const BatchOutDev& out, hipStream_t stream,
                                    LaunchStats* stats) {

@@ -196,6 +196,15 @@ class DeviceEngine {
   hipError_t project_output(const BatchOutDev& stage, uint32_t num, uint32_t* next_labels,
                             uint64_t* next_offsets, int32_t* proj_status, uint32_t* max_len,
                             hipStream_t stream);
+  // The batch result in CSR order, on the device: status (with `fail`, when given, taking
+  // precedence: a pipeline's first failing stage), path offsets over the OK strings'
+  // paths, the arcs gathered from the arena, final weights (+inf unless OK).  il / ol / w
+  // hold at least the arena's used arcs.  Synchronises on `stream`; *total = arcs.
+  hipError_t compact_paths(const BatchOutDev& s, uint32_t num, const int32_t* fail,
+                           int32_t* status, uint64_t* offsets, uint32_t* il, uint32_t* ol,
+                           double* w, double* fin, uint64_t* total, hipStream_t stream);
+  // fail[i] = st[i] where fail[i] is still OK (the first failing stage wins).
+  hipError_t merge_status(int32_t* fail, const int32_t* st, uint32_t num, hipStream_t stream);
   // fst_shortest_path on an explicit graph; `g` holds the FST itself (CSR, arcs in
   // insertion order).  nonneg: every weight >= +0 (parallel fixpoint); otherwise the exact
   // one-lane replay of the reference's heap order (sp_replay_kernel).  No NaN weights.
