@@ -358,6 +358,7 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
 struct HostProf {
   bool on = std::getenv("FSTAMD_HOST_PROF") != nullptr;
   double ms[8] = {};  // inputs H2D, output alloc, engine + sync, download, project, result
+  int runs = 0;       // engine runs (a full arena reruns the batch with 4x the arcs)
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   void lap(int i) {
     if (!on) return;
@@ -369,8 +370,8 @@ struct HostProf {
     if (!on) return;
     std::fprintf(stderr,
                  "[libfst_amd host] %s: inputs %.2f alloc %.2f engine %.2f download %.2f "
-                 "project %.2f result %.2f ms\n",
-                 what, ms[0], ms[1], ms[2], ms[3], ms[4], ms[5]);
+                 "project %.2f result %.2f ms (engine: %d launch(es))\n",
+                 what, ms[0], ms[1], ms[2], ms[3], ms[4], ms[5], runs);
   }
 };
 thread_local HostProf* t_prof = nullptr;
@@ -450,8 +451,10 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
                              uint32_t n, int semantics, int dev, HostPaths* h,
                              std::unique_ptr<DevOut>* keep) {
   const uint32_t num = in.num_strings;
-  // Arena: chains without rhs epsilons produce exactly L arcs per path.
-  uint64_t arc_cap = std::max<uint64_t>(total_labels + 16, 1024);
+  // Arena: chains without rhs epsilons produce exactly L arcs per path; with them a path
+  // also carries the rhs epsilon arcs (a tagger's or verbalizer's multi-symbol outputs),
+  // so start at 4 arcs per label rather than run the whole batch twice on OUTPUT_FULL.
+  uint64_t arc_cap = std::max<uint64_t>((D.has_eps ? 4 : 1) * total_labels + 16, 1024);
   if (const char* e = std::getenv("FSTAMD_ARENA_ARCS"))  // test override: first arena size
     if (*e) arc_cap = std::max<uint64_t>(std::strtoull(e, nullptr, 10), 1);
   DeviceEngine& E = DeviceEngine::get(dev);
@@ -465,7 +468,10 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
     LaunchStats st;
     hipError_t err = E.run_chain(D, in, n, semantics, out->v, nullptr, &st);
     if (err == hipSuccess) err = hipDeviceSynchronize();
-    if (t_prof) t_prof->lap(2);
+    if (t_prof) {
+      t_prof->lap(2);
+      ++t_prof->runs;
+    }
     if (err != hipSuccess) {
       std::fprintf(stderr, "[libfst_amd] batch engine failed: %s\n", hipGetErrorString(err));
       return FST_OOM;
