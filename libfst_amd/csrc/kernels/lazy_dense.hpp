@@ -162,12 +162,17 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
   const unsigned long long t0 = V.t0;
   const uint32_t NS = rhs.num_states;
   const uint32_t LC = L + 1;  // the dense index's position stride (state-major)
+#ifdef FSTAMD_LD_KMAJOR  // A/B: position-major (k * NS + s2) * 2 + f
+  auto dix = [&](uint32_t k_, uint32_t s_) { return k_ * NS + s_; };
+#else
+  auto dix = [&](uint32_t k_, uint32_t s_) { return s_ * LC + k_; };
+#endif
   if (prof && lane == 0) prof[3] += 1;
   const uint32_t nsum_s = (uint32_t)(((uint64_t)LC * 2 * NS + 4095) / 4096);
   const unsigned long long wd = ws.wd_ticks + (uint64_t)LC * 2 * NS * ws.wd_tuple_ticks;
 
   // ---- init tuple (fst1.start, fst2.start, 0), id 0, dist One (:146-153) ----
-  const uint32_t x0 = 2 * rhs.start * LC;
+  const uint32_t x0 = 2 * dix(0, rhs.start);
   if (lane == 0) {
     R[x0] = ld_rec(w_one(), 0u, kLdNoPrev);
     ids[0] = x0;
@@ -307,8 +312,13 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
       site = 2;
       break;
     }
+#ifdef FSTAMD_LD_KMAJOR
+    const uint32_t k = (x >> 1) / NS;
+    const uint32_t s = (x >> 1) - k * NS;
+#else
     const uint32_t s = (x >> 1) / LC;
     const uint32_t k = (x >> 1) - s * LC;
+#endif
     if (k > L || s >= NS || pid >= nn) {  // invariant guard: never walk on garbage
       fail = kPathInternal;
       site = 3;
@@ -348,7 +358,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
       if (p1 || p3) {
         const uint32_t rank = p1 ? (uint32_t)__popcll(m1 & lanemask_lt())
                                  : n1 + (uint32_t)__popcll(m3 & lanemask_lt());
-        S.x[rank] = p1 ? 2 * (r.next * LC + k + 1) : 2 * (r.next * LC + k) + 1;
+        S.x[rank] = p1 ? 2 * dix(k + 1, r.next) : 2 * dix(k, r.next) + 1;
         S.a[rank] = aoff + lane;
         S.il[rank] = il;
         S.ol[rank] = r.olabel;
@@ -374,7 +384,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
           const bool p1 = c < n1;
           const uint32_t a = p1 ? lo1 + c : lo3 + (c - n1);
           const ArcRec r = rhs.rec[a];
-          S.x[lane] = p1 ? 2 * (r.next * LC + k + 1) : 2 * (r.next * LC + k) + 1;
+          S.x[lane] = p1 ? 2 * dix(k + 1, r.next) : 2 * dix(k, r.next) + 1;
           S.a[lane] = a;
           S.il[lane] = p1 ? label : kEpsilon;
           S.ol[lane] = r.olabel;
