@@ -19,6 +19,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/fst_batch.h"
@@ -285,6 +286,7 @@ struct GraphUpload {
         vol.push_back(x.olabel);
         vw.push_back(x.weight);
         vnx.push_back(x.nextstate);
+        if (x.olabel == kEpsilon) g.eps_out = 1;
         if (neg(x.weight)) nonneg = false;
         if (std::isnan(x.weight)) nan = true;
       }
@@ -768,8 +770,11 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
   const int dev = current_device();
   DeviceFst* D = dev >= 0 ? b->device(dev) : nullptr;
   if (!D) return kInvalid;
+  const bool hprof = std::getenv("FSTAMD_HOST_PROF") != nullptr;
+  const double t_up0 = us();
   GraphUpload up(*a);
   if (!up.ok) return kInvalid;
+  const double t_up1 = us();
   HostLattice lat;
   LaunchStats st;
   {
@@ -782,16 +787,37 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
     }
   }
   t_last_stats = st;
+  const double t_gpu = us();
   MutableFst result;
   if (lat.n_nodes > 0) {
     result.add_states(lat.n_nodes);
     result.set_start(0);
-    for (uint32_t s2 = 0; s2 < lat.n_nodes; ++s2) {
-      if (!w_is_zero(lat.nfin[s2])) result.set_final(s2, lat.nfin[s2]);
-      for (uint32_t k = lat.aoff[s2]; k < lat.aoff[s2 + 1]; ++k)
-        result.add_arc(s2, Arc{lat.ail[k], lat.aol[k], lat.aw[k], lat.anext[k]});
-    }
+    // states in contiguous ranges, one host thread each (a 10 M-arc lattice: ~80 ms on
+    // one thread); every state's arc vector is its own allocation
+    auto build = [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t s2 = lo; s2 < hi; ++s2) {
+        if (!w_is_zero(lat.nfin[s2])) result.set_final(s2, lat.nfin[s2]);
+        const uint32_t k0 = lat.aoff[s2], k1 = lat.aoff[s2 + 1];
+        result.reserve_arcs(s2, k1 - k0);
+        for (uint32_t k = k0; k < k1; ++k)
+          result.add_arc(s2, Arc{lat.ail[k], lat.aol[k], lat.aw[k], lat.anext[k]});
+      }
+    };
+    const uint32_t nt = lat.n_arcs < (1u << 18) ? 1u
+                        : std::min<uint32_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; ++t)
+      th.emplace_back(build, (uint32_t)((uint64_t)lat.n_nodes * t / nt),
+                      (uint32_t)((uint64_t)lat.n_nodes * (t + 1) / nt));
+    build(0, (uint32_t)((uint64_t)lat.n_nodes / nt));
+    for (auto& x : th) x.join();
   }
+  if (hprof)
+    std::fprintf(stderr,
+                 "[libfst_amd host] fst_compose_frozen: upload %.2f compose+download %.2f "
+                 "(kernel %.2f, %u launch(es)) result %.2f ms\n",
+                 (t_up1 - t_up0) / 1e3, (t_gpu - t_up1) / 1e3, st.kernel_ms, st.launches,
+                 (us() - t_gpu) / 1e3);
   trace("ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
         result.total_arcs(), us(), st.kernel_ms);
   std::lock_guard<std::mutex> g(g_api_mu);

@@ -1204,7 +1204,21 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!ctr) return hipErrorOutOfMemory;
   BatchOutDev none_out{};
-  for (int tier = 1;; ++tier) {  // one lattice: start at 128K tuples
+  // First tier: 128K tuples, or the smallest one that holds every tuple the product can
+  // have -- |lhs| x |rhs| per filter value in use (compose.zig: filter 1 needs an rhs input
+  // epsilon, filter 2 an lhs output epsilon) -- so a large lattice does not first run
+  // until it overflows a small tier (config 1: 781K tuples, 78 ms lost in tier 1).
+  const uint64_t bound = (uint64_t)lhs.num_states * rhs.view.num_states *
+                         (1u + (rhs.has_eps ? 1u : 0u) + (lhs.eps_out ? 1u : 0u));
+  int tier0 = 1;
+  while (bfs_caps(tier0).ncap < bound && bfs_caps(tier0 + 1).stride <= kBfsBudget &&
+         bfs_caps(tier0).ncap < (1u << 30))
+    ++tier0;
+  // One 1024-thread workgroup: the ~4,200 BFS levels of config 1 are ~190 tuples wide
+  // (kernel 182 vs 214 ms with 256 threads).  FSTAMD_LATTICE_WG=256 for A/B runs.
+  const char* lwg = std::getenv("FSTAMD_LATTICE_WG");
+  const bool wg1k = !(lwg && std::strcmp(lwg, "256") == 0);
+  for (int tier = tier0;; ++tier) {
     const BfsCaps c = bfs_caps(tier);
     if (c.stride > kBfsBudget) {
       lat->status = kPathOverflow;
@@ -1224,15 +1238,19 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
     HIP_TRY(hipMemset(ctr, 0, 64));
     if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
     ChainInput none{};
-    eager_bfs_kernel<kBfsWG, true><<<1, kBfsWG, 0, nullptr>>>(rhs.view, none, lhs, 1, ctr,
-                                                              nullptr, nullptr, 1, ws, none_out);
+    if (wg1k)
+      eager_bfs_kernel<1024, true><<<1, 1024, 0, nullptr>>>(rhs.view, none, lhs, 1, ctr, nullptr,
+                                                            nullptr, 1, ws, none_out);
+    else
+      eager_bfs_kernel<kBfsWG, true><<<1, kBfsWG, 0, nullptr>>>(rhs.view, none, lhs, 1, ctr,
+                                                                nullptr, nullptr, 1, ws, none_out);
     HIP_TRY(hipGetLastError());
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, nullptr));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
       stats->engine = 2;
       stats->grid = 1;
-      stats->launches = tier;
+      stats->launches = tier - tier0 + 1;
     }
     uint32_t hdr[8];
     HIP_TRY(hipMemcpy(hdr, ws.hdr, sizeof(hdr), hipMemcpyDeviceToHost));

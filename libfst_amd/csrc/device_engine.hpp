@@ -136,6 +136,7 @@ struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
   uint32_t start;
   uint32_t max_outdeg;     // largest lhs out-degree (sizes the per-pop table)
   uint32_t ncap;           // product-tuple capacity for this run (power of two)
+  uint32_t eps_out;        // 1: some lhs arc has output epsilon (filter-2 tuples exist)
 };
 
 // Lattice of one fst_compose_frozen call, downloaded from the device (CSR by source id).

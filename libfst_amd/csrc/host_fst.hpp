@@ -32,6 +32,7 @@ class MutableFst {
   void set_start(StateId s) { start_ = s; }
   void set_final(StateId s, double w) { states_[s].final_weight = w; }
   void add_arc(StateId src, const Arc& a) { states_[src].arcs.push_back(a); }
+  void reserve_arcs(StateId src, size_t n) { states_[src].arcs.reserve(n); }
 
   StateId start() const { return start_; }
   size_t num_states() const { return states_.size(); }
