@@ -1328,12 +1328,22 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
     }
     return hipDeviceSynchronize();
   }
-  // work arrays: distances, back-pointers, the one "level" [0, N)
-  uint8_t* w = (uint8_t*)scratch(kBfsSlab, (size_t)N * 16 + 256);
-  uint32_t* lv = (uint32_t*)scratch(kBfsHdr, 16);
+  // work arrays: distances, back-pointers, stamps, settled flags, two frontiers, the
+  // pending list (one entry per arc at most); the one "level" [0, N) and the distance
+  // kernels' flags in the header
+  const size_t n_b = ((size_t)N * 4 + 255) & ~(size_t)255;
+  uint32_t A = 0;
+  if (N) HIP_TRY(hipMemcpy(&A, g.state_off + N, 4, hipMemcpyDeviceToHost));
+  uint8_t* w = (uint8_t*)scratch(kBfsSlab, (size_t)N * 16 + 256 + 4 * n_b + ((size_t)A + 64) * 4);
+  uint32_t* lv = (uint32_t*)scratch(kBfsHdr, 32);
   if (!w || !lv) return hipErrorOutOfMemory;
-  const uint32_t lvh[2] = {0, N};
-  HIP_TRY(hipMemcpy(lv, lvh, 8, hipMemcpyHostToDevice));
+  const uint32_t lvh[8] = {0, N, 0, 0, 0, 0, 0, 0};  // [2..3]: have_dist, expired; [4..5] prof
+  HIP_TRY(hipMemcpy(lv, lvh, 32, hipMemcpyHostToDevice));
+  uint32_t* mark = (uint32_t*)(w + (((size_t)N * 16 + 255) & ~(size_t)255));
+  uint32_t* fa = (uint32_t*)((uint8_t*)mark + n_b);
+  uint32_t* fb = (uint32_t*)((uint8_t*)fa + n_b);
+  uint32_t* stl = (uint32_t*)((uint8_t*)fb + n_b);
+  uint32_t* pend = (uint32_t*)((uint8_t*)stl + n_b);
   HIP_TRY(hipMemset(out.cursor, 0, 8));
   BfsTables T{};
   T.aoff = const_cast<uint32_t*>(g.state_off);
@@ -1346,7 +1356,46 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
   T.nd = (unsigned long long*)w;
   T.nback = (unsigned long long*)(w + (size_t)N * 8);
   if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
-  sp_graph_kernel<kBfsWG><<<1, kBfsWG, 0, nullptr>>>(T, N, g.start, n, out, watchdog_ticks());
+  // FSTAMD_SP_SWEEP=1: the Gauss-Seidel sweeps over every arc instead of the frontier
+  const bool sweep = std::getenv("FSTAMD_SP_SWEEP") != nullptr;
+  const bool hprof = std::getenv("FSTAMD_HOST_PROF") != nullptr;
+  hipEvent_t em = nullptr;
+  if (hprof) {
+    HIP_TRY(hipEventCreate(&em));
+    HIP_TRY(hipEventRecord(ev0_, nullptr));
+  }
+  // distances: settled in distance order (sp_settle_kernel); after more than
+  // FSTAMD_SP_MAX_ADV (256) distinct distances, label correcting (sp_frontier_kernel)
+  uint32_t sf[4] = {0, 0, 0, 0};  // fallback, expired, rounds, advances
+  if (!sweep && g.start < N && n == 1) {
+    const char* ma = std::getenv("FSTAMD_SP_MAX_ADV");
+    const uint32_t max_adv = ma ? (uint32_t)std::strtoul(ma, nullptr, 10) : 256u;
+    sp_settle_kernel<1024><<<1, 1024, 0, nullptr>>>(T, N, g.start, mark, stl, fa, fb, pend,
+                                                    lv + 4, max_adv, watchdog_ticks());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(sf, lv + 4, 16, hipMemcpyDeviceToHost));
+    if (sf[1]) {  // its watchdog fired: the path reports INTERNAL
+      const uint32_t one = 1;
+      HIP_TRY(hipMemcpy(lv + 3, &one, 4, hipMemcpyHostToDevice));
+    } else if (sf[0]) {
+      sp_frontier_kernel<1024><<<1, 1024, 0, nullptr>>>(T, N, g.start, mark, fa, fb, lv + 3,
+                                                        watchdog_ticks());
+    }
+  }
+  if (hprof) HIP_TRY(hipEventRecord(em, nullptr));
+  sp_graph_kernel<1024><<<1, 1024, 0, nullptr>>>(
+      T, N, g.start, n, out, watchdog_ticks(), sweep || g.start >= N || n != 1 ? nullptr : lv + 2);
+  if (hprof) {
+    HIP_TRY(hipEventRecord(ev1_, nullptr));
+    HIP_TRY(hipEventSynchronize(ev1_));
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&a, ev0_, em));
+    HIP_TRY(hipEventElapsedTime(&b, em, ev1_));
+    std::fprintf(stderr, "[libfst_amd host] fst_shortest_path: distances %.2f ms (settle: %u "
+                 "rounds, %u advances%s), back-pointers + best + path %.2f ms (%u states)\n",
+                 a, sf[2], sf[3], sf[0] ? ", then label correcting" : "", b, N);
+    HIP_TRY(hipEventDestroy(em));
+  }
   HIP_TRY(hipGetLastError());
   if (stats) {
     HIP_TRY(hipEventRecord(ev1_, nullptr));

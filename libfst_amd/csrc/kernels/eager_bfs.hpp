@@ -1190,10 +1190,286 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
 
 // fst_shortest_path on an explicit FST held as a lattice (T.aoff/anext/ail/aol/aw/nfin
 // are the FST's own CSR, T.lvl = {0, N}: one "level", Jacobi-style sweeps).
+// Distances of fst_shortest_path (weights >= 0) by label correcting over a frontier, one
+// workgroup: a round relaxes the out-arcs of the nodes whose distance dropped in the
+// previous round (atomicMin on the order-preserving key); a node whose key drops joins the
+// next frontier once per round (stamp).  It converges to the least fixpoint, which is
+// Dijkstra's distance for weights >= 0, after as many rounds as the
+// longest shortest path has arcs, touching only the frontier's arcs: on config 1's lattice
+// (781 K states, 10 M arcs, ~4,200 levels) the sweeps over every arc took 34 s.
+// A round takes the frontier WG nodes at a time: their spans and distances go to LDS with a
+// scan of the out-degrees, then the chunk's ARCS are spread over the threads (binary
+// search of the arc's node in LDS), kArcUnroll at a time so that their loads and atomics
+// are in flight together.  *expired = 1 when the watchdog stops it.
+constexpr int kSpArcUnroll = 4;
+
+template <int WG>
+__global__ void __launch_bounds__(WG)
+sp_frontier_kernel(BfsTables T, uint32_t n_nodes, uint32_t start, uint32_t* mark,
+                   uint32_t* fa, uint32_t* fb, uint32_t* expired, unsigned long long wd_ticks) {
+  __shared__ uint32_t cnt[3];
+  __shared__ uint32_t stop;
+  __shared__ uint32_t scan[16];
+  __shared__ uint32_t c_off[WG + 1];   // chunk: first arc (chunk-relative) of each node
+  __shared__ uint32_t c_a0[WG];        // its first arc in the graph
+  __shared__ double c_ds[WG];          // its distance
+  const uint32_t tid = threadIdx.x;
+  if (start >= n_nodes) return;
+  for (uint32_t i = tid; i < n_nodes; i += WG) {
+    T.nd[i] = i == start ? okey(w_one()) : okey(w_zero());
+    mark[i] = ~0u;
+  }
+  if (tid == 0) {
+    fa[0] = start;
+    cnt[0] = 1;  // round 0's frontier
+    cnt[1] = 0;
+    cnt[2] = 0;
+    stop = 0;
+  }
+  __syncthreads();
+  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + wd_ticks;
+  uint32_t* cur = fa;
+  uint32_t* nxt = fb;
+  for (uint32_t r = 0;; ++r) {
+    const uint32_t fsize = cnt[r % 3];  // written before the last barrier
+    if (fsize == 0 || stop) break;
+    // the counter round r + 1 pushes into was last read before the previous barrier
+    if (tid == 0) {
+      cnt[(r + 1) % 3] = 0;
+      if ((r & 63u) == 63u && __builtin_amdgcn_s_memrealtime() > deadline) stop = 1;
+    }
+    uint32_t* const push = &cnt[(r + 1) % 3];
+    for (uint32_t c0 = 0; c0 < fsize; c0 += WG) {
+      // (1) the chunk's nodes: span and distance into LDS, out-degree scan
+      uint32_t deg = 0;
+      const uint32_t q = c0 + tid;
+      if (q < fsize) {
+        const uint32_t s = ld_agent(&cur[q]);
+        const uint32_t a0 = T.aoff[s];
+        deg = T.aoff[s + 1] - a0;
+        c_a0[tid] = a0;
+        c_ds[tid] = from_okey(ld_agent(&T.nd[s]));
+      }
+      uint32_t total;
+      const uint32_t ex = block_excl_scan<WG>(deg, scan, total);  // (its barriers publish LDS)
+      c_off[tid] = ex;
+      if (tid == 0) c_off[WG] = total;
+      const uint32_t nn = min(WG, fsize - c0);
+      __syncthreads();
+      // (2) the chunk's arcs, kSpArcUnroll per thread at a time
+      for (uint32_t b = 0; b < total; b += WG * kSpArcUnroll) {
+        uint32_t x[kSpArcUnroll];
+        unsigned long long v[kSpArcUnroll];
+        bool act[kSpArcUnroll];
+#pragma unroll
+        for (int u = 0; u < kSpArcUnroll; ++u) {
+          const uint32_t i = b + (uint32_t)u * WG + tid;
+          act[u] = i < total;
+          x[u] = 0;
+          v[u] = ~0ull;
+          if (act[u]) {
+            uint32_t lo = 0, hi = nn;  // the node whose arc range holds i
+            while (hi - lo > 1) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (c_off[mid] <= i) lo = mid;
+              else hi = mid;
+            }
+            const uint32_t a = c_a0[lo] + (i - c_off[lo]);
+            x[u] = T.anext[a];
+            v[u] = okey(w_times(c_ds[lo], T.aw[a]));  // shortest-path.zig:72
+          }
+        }
+        unsigned long long old[kSpArcUnroll];
+#pragma unroll
+        for (int u = 0; u < kSpArcUnroll; ++u)
+          old[u] = act[u] ? atomicMin(&T.nd[x[u]], v[u]) : 0ull;
+#pragma unroll
+        for (int u = 0; u < kSpArcUnroll; ++u)
+          if (act[u] && v[u] < old[u] && atomicExch(&mark[x[u]], r) != r)
+            nxt[atomicAdd(push, 1u)] = x[u];
+      }
+      __syncthreads();  // the chunk's LDS is reused by the next one
+    }
+    uint32_t* t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  if (tid == 0 && stop) *expired = 1;
+}
+
+// Distances of fst_shortest_path (weights >= 0) settled in distance order, one workgroup:
+// every node at the smallest open distance dcur is final (no arc can lower it), so a round
+// settles the frontier at dcur and relaxes each settled node's arcs exactly once; targets
+// reached at dcur (0-weight arcs) form the next round's frontier, the others go to a
+// pending list.  When the frontier is empty the pending list is scanned for the next
+// distance (its settled and stale entries dropped).  Unlike label correcting this does no
+// rework (config 1's lattice: label correcting took every node 33 times); its cost is one
+// pending scan per distinct distance, so after max_adv advances it gives up (*fallback = 1)
+// and the host runs sp_frontier_kernel instead.  pend holds at most one entry per arc.
+template <int WG>
+__global__ void __launch_bounds__(WG)
+sp_settle_kernel(BfsTables T, uint32_t n_nodes, uint32_t start, uint32_t* mark, uint32_t* st,
+                 uint32_t* fa, uint32_t* fb, uint32_t* pend, uint32_t* flags, uint32_t max_adv,
+                 unsigned long long wd_ticks) {
+  __shared__ uint32_t cnt[3];
+  __shared__ uint32_t stop, pcount;
+  __shared__ unsigned long long dmin_s;
+  __shared__ uint32_t scan[16];
+  __shared__ uint32_t c_off[WG + 1];
+  __shared__ uint32_t c_a0[WG];
+  const uint32_t tid = threadIdx.x;
+  if (start >= n_nodes) return;
+  for (uint32_t i = tid; i < n_nodes; i += WG) {
+    T.nd[i] = i == start ? okey(w_one()) : okey(w_zero());
+    mark[i] = ~0u;
+    st[i] = 0;
+  }
+  if (tid == 0) {
+    fa[0] = start;
+    cnt[0] = 1;
+    cnt[1] = 0;
+    cnt[2] = 0;
+    stop = 0;
+    pcount = 0;
+  }
+  __syncthreads();
+  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + wd_ticks;
+  unsigned long long dcur = okey(w_one());
+  uint32_t* cur = fa;
+  uint32_t* nxt = fb;
+  uint32_t r = 0, adv = 0, rounds = 0;
+  for (;;) {
+    // ---- settle rounds at dcur ----
+    for (;; ++r) {
+      const uint32_t fsize = cnt[r % 3];
+      if (fsize == 0 || stop) break;
+      ++rounds;
+      if (tid == 0) {
+        cnt[(r + 1) % 3] = 0;
+        if ((rounds & 63u) == 63u && __builtin_amdgcn_s_memrealtime() > deadline) stop = 1;
+      }
+      uint32_t* const push = &cnt[(r + 1) % 3];
+      const double ds = from_okey(dcur);
+      for (uint32_t c0 = 0; c0 < fsize; c0 += WG) {
+        uint32_t deg = 0;
+        const uint32_t q = c0 + tid;
+        if (q < fsize) {
+          const uint32_t s = ld_agent(&cur[q]);
+          if (atomicExch(&st[s], 1u) == 0u) {  // settle s once; its arcs are relaxed once
+            const uint32_t a0 = T.aoff[s];
+            deg = T.aoff[s + 1] - a0;
+            c_a0[tid] = a0;
+          }
+        }
+        uint32_t total;
+        const uint32_t ex = block_excl_scan<WG>(deg, scan, total);
+        c_off[tid] = ex;
+        const uint32_t nn = min(WG, fsize - c0);
+        __syncthreads();
+        for (uint32_t b = 0; b < total; b += WG * kSpArcUnroll) {
+          uint32_t x[kSpArcUnroll];
+          unsigned long long v[kSpArcUnroll];
+          bool act[kSpArcUnroll];
+#pragma unroll
+          for (int u = 0; u < kSpArcUnroll; ++u) {
+            const uint32_t i = b + (uint32_t)u * WG + tid;
+            act[u] = i < total;
+            x[u] = 0;
+            v[u] = ~0ull;
+            if (act[u]) {
+              uint32_t lo = 0, hi = nn;
+              while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (c_off[mid] <= i) lo = mid;
+                else hi = mid;
+              }
+              const uint32_t a = c_a0[lo] + (i - c_off[lo]);
+              x[u] = T.anext[a];
+              v[u] = okey(w_times(ds, T.aw[a]));  // shortest-path.zig:72
+            }
+          }
+          unsigned long long old[kSpArcUnroll];
+#pragma unroll
+          for (int u = 0; u < kSpArcUnroll; ++u)
+            old[u] = act[u] ? atomicMin(&T.nd[x[u]], v[u]) : 0ull;
+#pragma unroll
+          for (int u = 0; u < kSpArcUnroll; ++u) {
+            if (!act[u] || !(v[u] < old[u])) continue;
+            if (v[u] == dcur) {  // reached at dcur: settled next round
+              if (atomicExch(&mark[x[u]], r) != r) nxt[atomicAdd(push, 1u)] = x[u];
+            } else {
+              pend[atomicAdd(&pcount, 1u)] = x[u];
+            }
+          }
+        }
+        __syncthreads();
+      }
+      uint32_t* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+    if (stop) break;
+    // ---- advance: the smallest open distance among the pending entries ----
+    const uint32_t pn = pcount;
+    unsigned long long m = ~0ull;
+    for (uint32_t i = tid; i < pn; i += WG) {
+      const uint32_t x = ld_agent(&pend[i]);
+      if (ld_agent(&st[x]) == 0u) {
+        const unsigned long long d = ld_agent(&T.nd[x]);
+        m = d < m ? d : m;
+      }
+    }
+    if (tid == 0) dmin_s = ~0ull;
+    __syncthreads();
+    if (m != ~0ull) atomicMin(&dmin_s, m);
+    __syncthreads();
+    const unsigned long long dmin = dmin_s;
+    if (dmin == ~0ull || dmin == okey(w_zero())) break;  // nothing open: done
+    if (++adv > max_adv) {
+      if (tid == 0) flags[0] = 1;  // fallback: label correcting
+      return;
+    }
+    // entries at dmin -> the frontier (once per node), the rest stay (compacted in place)
+    ++r;
+    if (tid == 0) {
+      cnt[r % 3] = 0;
+      cnt[(r + 1) % 3] = 0;
+    }
+    __syncthreads();
+    uint32_t kept = 0;
+    for (uint32_t c0 = 0; c0 < pn; c0 += WG) {
+      const uint32_t i = c0 + tid;
+      uint32_t x = 0, keep = 0;
+      if (i < pn) {
+        x = ld_agent(&pend[i]);
+        if (ld_agent(&st[x]) == 0u) {
+          if (ld_agent(&T.nd[x]) == dmin) {
+            if (atomicExch(&mark[x], r) != r) cur[atomicAdd(&cnt[r % 3], 1u)] = x;
+          } else {
+            keep = 1;
+          }
+        }
+      }
+      uint32_t tot;
+      const uint32_t rank = block_excl_scan<WG>(keep, scan, tot);  // reads done: barrier
+      if (keep) pend[kept + rank] = x;  // kept + rank <= c0 + tid: never an unread entry
+      kept += tot;
+    }
+    if (tid == 0) pcount = kept;
+    dcur = dmin;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (stop) flags[1] = 1;
+    flags[2] = rounds;
+    flags[3] = adv;
+  }
+}
+
 template <int WG>
 __global__ void __launch_bounds__(WG)
 sp_graph_kernel(BfsTables T, uint32_t n_nodes, uint32_t start, uint32_t n_best, BatchOutDev out,
-                unsigned long long wd_ticks) {
+                unsigned long long wd_ticks, const uint32_t* have_dist) {
   __shared__ BfsShared SH;
   if (start == kNoState || n_best == 0 || n_nodes == 0) {  // shortest-path.zig:21-23
     if (threadIdx.x == 0) write_status(out, 0, kPathEmpty, 0, 0);
@@ -1203,8 +1479,13 @@ sp_graph_kernel(BfsTables T, uint32_t n_nodes, uint32_t start, uint32_t n_best, 
     if (threadIdx.x == 0) write_status(out, 0, kPathErrorN, 0, 0);
     return;
   }
+  // have_dist: sp_frontier_kernel left the distances in T.nd ([1]: its watchdog fired)
+  if (have_dist && have_dist[1]) {
+    if (threadIdx.x == 0) write_status(out, 0, kPathInternal, n_nodes, T.aoff[n_nodes]);
+    return;
+  }
   bfs_shortest_path<WG>(T, n_nodes, T.aoff[n_nodes], 1u, start, out, 0u, SH,
-                        __builtin_amdgcn_s_memrealtime() + wd_ticks);
+                        __builtin_amdgcn_s_memrealtime() + wd_ticks, !have_dist, have_dist != nullptr);
 }
 
 __global__ void __launch_bounds__(64)

@@ -107,13 +107,39 @@ def compare_sp(f: O.Fst, n=1):
     assert lattice_lists(got) == oracle_lists(ref)
 
 
+@pytest.fixture(params=["settle", "label-correcting", "sweeps"])
+def sp_mode(request, monkeypatch):
+    # the distances of fst_shortest_path: settled in distance order (default), label
+    # correcting over a frontier (its fallback, forced by FSTAMD_SP_MAX_ADV=0 here), or
+    # Gauss-Seidel sweeps over every arc (FSTAMD_SP_SWEEP)
+    monkeypatch.delenv("FSTAMD_SP_SWEEP", raising=False)
+    monkeypatch.delenv("FSTAMD_SP_MAX_ADV", raising=False)
+    if request.param == "label-correcting":
+        monkeypatch.setenv("FSTAMD_SP_MAX_ADV", "0")
+    elif request.param == "sweeps":
+        monkeypatch.setenv("FSTAMD_SP_SWEEP", "1")
+    return request.param
+
+
 @pytest.mark.parametrize("seed", range(12))
-def test_shortest_path_random_graphs(seed):
+def test_shortest_path_random_graphs(seed, sp_mode):
     rng = np.random.default_rng(6000 + seed)
     f = random_rhs(rng, int(rng.integers(1, 30)), int(rng.integers(0, 120)), 4, eps=True,
                    frac=seed % 3 == 0)
     for n in (0, 1, 2):
         compare_sp(f, n)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_shortest_path_large_tie_heavy_graphs(seed, sp_mode):
+    # hundreds of nodes, 0-weight cycles and many equal distances: frontiers of several
+    # chunks of 1024 nodes, nodes reached first at a larger distance and then lowered, and
+    # (fractional weights) many distinct distances
+    rng = np.random.default_rng(6100 + seed)
+    ns = int(rng.integers(500, 3000))
+    f = random_rhs(rng, ns, ns * int(rng.integers(2, 6)), 3, eps=True, wmax=2,
+                   frac=seed % 2 == 1)
+    compare_sp(f, 1)
 
 
 def test_shortest_path_on_compose_result():
