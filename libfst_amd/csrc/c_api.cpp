@@ -261,47 +261,110 @@ MutableFst chain_result(const HostPaths& h, uint32_t i) {
 
 // A MutableFst uploaded as CSR (arcs in insertion order): the lhs of the single-call
 // compose entries, or the FST itself for fst_shortest_path.
+// A MutableFst flattened to CSR on the host (arcs in insertion order), the device upload's
+// source.  Large FSTs are flattened on host threads by state ranges (fst_shortest_path on a
+// 10 M-arc lattice: a deep copy plus a push_back pass took ~150 ms).
+// Host array without value-initialisation (the flatten writes every element, on the
+// threads that first touch its pages).
+template <class T>
+struct RawVec {
+  std::unique_ptr<T[]> p;
+  size_t n = 0;
+  void resize(size_t k) {
+    p.reset(k ? new T[k] : nullptr);
+    n = k;
+  }
+  size_t size() const { return n; }
+  T* data() { return p.get(); }
+  const T* data() const { return p.get(); }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+};
+
+struct HostGraph {
+  std::vector<uint32_t> soff;
+  RawVec<uint32_t> il, ol, nx;
+  RawVec<double> w, fin;
+  uint32_t start = kNoState, maxdeg = 0;
+  bool nonneg = true;  // every arc and final weight >= +0.0 (no -0.0, no NaN)
+  bool nan = false;    // some arc or final weight is NaN
+  bool eps_out = false;
+
+  explicit HostGraph(const MutableFst& a) {
+    const uint32_t ns = (uint32_t)a.num_states();
+    start = a.start();
+    soff.assign(ns + 1, 0);
+    fin.resize(ns);
+    for (uint32_t s = 0; s < ns; ++s) {
+      const uint32_t d = (uint32_t)a.num_arcs(s);
+      soff[s + 1] = soff[s] + d;
+      maxdeg = std::max(maxdeg, d);
+    }
+    const size_t na = soff[ns];
+    il.resize(na);
+    ol.resize(na);
+    nx.resize(na);
+    w.resize(na);
+    auto neg = [](double x) { return x < 0.0 || std::isnan(x) || (x == 0.0 && std::signbit(x)); };
+    const uint32_t nt = na < (1u << 18) ? 1u
+                        : std::min<uint32_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<uint8_t> flags(nt, 0);  // per thread: 1 negative, 2 NaN, 4 output epsilon
+    auto fill = [&](uint32_t t) {
+      const uint32_t lo = (uint32_t)((uint64_t)ns * t / nt), hi = (uint32_t)((uint64_t)ns * (t + 1) / nt);
+      uint8_t fl = 0;
+      for (uint32_t s = lo; s < hi; ++s) {
+        fin[s] = a.final_weight(s);
+        if (neg(fin[s])) fl |= 1;
+        if (std::isnan(fin[s])) fl |= 2;
+        uint32_t k = soff[s];
+        for (const Arc& x : a.arcs(s)) {
+          il[k] = x.ilabel;
+          ol[k] = x.olabel;
+          w[k] = x.weight;
+          nx[k] = x.nextstate;
+          if (x.olabel == kEpsilon) fl |= 4;
+          if (neg(x.weight)) fl |= 1;
+          if (std::isnan(x.weight)) fl |= 2;
+          ++k;
+        }
+      }
+      flags[t] = fl;
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; ++t) th.emplace_back(fill, t);
+    fill(0);
+    for (auto& x : th) x.join();
+    for (uint8_t fl : flags) {
+      if (fl & 1) nonneg = false;
+      if (fl & 2) nan = true;
+      if (fl & 4) eps_out = true;
+    }
+  }
+};
+
 struct GraphUpload {
   DevBuf off, il, ol, w, nx, fin;
   GraphInput g{};
   bool ok = false;
-  bool nonneg = true;  // every arc and final weight >= +0.0 (no -0.0, no NaN)
-  bool nan = false;    // some arc or final weight is NaN
-  explicit GraphUpload(const MutableFst& a)
-      : off((a.num_states() + 1) * 4ull), il(a.total_arcs() * 4), ol(a.total_arcs() * 4),
-        w(a.total_arcs() * 8), nx(a.total_arcs() * 4), fin(a.num_states() * 8ull) {
-    const uint32_t ns = (uint32_t)a.num_states();
-    std::vector<uint32_t> soff(ns + 1, 0), vil, vol, vnx;
-    std::vector<double> vw, vfin(ns);
-    uint32_t maxdeg = 0;
-    auto neg = [](double x) { return x < 0.0 || std::isnan(x) || (x == 0.0 && std::signbit(x)); };
-    for (uint32_t s = 0; s < ns; ++s) {
-      soff[s] = (uint32_t)vil.size();
-      vfin[s] = a.final_weight(s);
-      if (neg(vfin[s])) nonneg = false;
-      if (std::isnan(vfin[s])) nan = true;
-      maxdeg = std::max<uint32_t>(maxdeg, (uint32_t)a.arcs(s).size());
-      for (const Arc& x : a.arcs(s)) {
-        vil.push_back(x.ilabel);
-        vol.push_back(x.olabel);
-        vw.push_back(x.weight);
-        vnx.push_back(x.nextstate);
-        if (x.olabel == kEpsilon) g.eps_out = 1;
-        if (neg(x.weight)) nonneg = false;
-        if (std::isnan(x.weight)) nan = true;
-      }
-    }
-    soff[ns] = (uint32_t)vil.size();
-    const size_t na = vil.size();
+  bool nonneg = true;
+  bool nan = false;
+  explicit GraphUpload(const MutableFst& a) : GraphUpload(HostGraph(a)) {}
+  explicit GraphUpload(const HostGraph& h)
+      : off(h.soff.size() * 4ull), il(h.il.size() * 4), ol(h.ol.size() * 4), w(h.w.size() * 8),
+        nx(h.nx.size() * 4), fin(h.fin.size() * 8ull) {
+    nonneg = h.nonneg;
+    nan = h.nan;
+    const uint32_t ns = (uint32_t)h.fin.size();
+    const size_t na = h.il.size();
     if (!off.p || !il.p || !ol.p || !w.p || !nx.p || !fin.p) return;
-    bool good = hipMemcpy(off.p, soff.data(), (ns + 1) * 4ull, hipMemcpyHostToDevice) == hipSuccess;
+    bool good = hipMemcpy(off.p, h.soff.data(), (ns + 1) * 4ull, hipMemcpyHostToDevice) == hipSuccess;
     if (na) {
-      good = good && hipMemcpy(il.p, vil.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(ol.p, vol.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(w.p, vw.data(), na * 8, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(nx.p, vnx.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess;
+      good = good && hipMemcpy(il.p, h.il.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(ol.p, h.ol.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(w.p, h.w.data(), na * 8, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(nx.p, h.nx.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess;
     }
-    if (ns) good = good && hipMemcpy(fin.p, vfin.data(), ns * 8ull, hipMemcpyHostToDevice) == hipSuccess;
+    if (ns) good = good && hipMemcpy(fin.p, h.fin.data(), ns * 8ull, hipMemcpyHostToDevice) == hipSuccess;
     g.state_off = (const uint32_t*)off.p;
     g.arc_il = (const uint32_t*)il.p;
     g.arc_ol = (const uint32_t*)ol.p;
@@ -309,8 +372,9 @@ struct GraphUpload {
     g.arc_next = (const uint32_t*)nx.p;
     g.final_w = (const double*)fin.p;
     g.num_states = ns;
-    g.start = a.start();
-    g.max_outdeg = maxdeg;
+    g.start = h.start;
+    g.max_outdeg = h.maxdeg;
+    g.eps_out = h.eps_out ? 1u : 0u;
     ok = good;
   }
 };
@@ -826,27 +890,36 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
 
 FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
   // src/c-api.zig:897-916 -> src/ops/shortest-path.zig:18-139 on the GPU.
-  std::shared_ptr<MutableFst> m;
+  const bool hprof = std::getenv("FSTAMD_HOST_PROF") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
+  std::unique_ptr<HostGraph> m;
   {
     std::lock_guard<std::mutex> g(g_api_mu);
     auto h = g_mut.get(handle);
     if (!h) return kInvalid;
-    m = std::make_shared<MutableFst>(*h);  // snapshot
+    m = std::make_unique<HostGraph>(*h);  // snapshot, flattened to CSR under the lock
   }
+  const double t_snap = ms();
   MutableFst result;
-  if (m->start() == kNoState || n == 0) {  // :21-23 -> empty
-  } else if (n != 1) {                     // :24 UnsupportedNShortest
+  const uint32_t m_states = (uint32_t)m->fin.size();
+  if (m->start == kNoState || n == 0) {  // :21-23 -> empty
+  } else if (n != 1) {                   // :24 UnsupportedNShortest
     return kInvalid;
   } else {
     if (!gpu_available()) return kInvalid;
     const int dev = current_device();
     if (dev < 0) return kInvalid;
     GraphUpload up(*m);
+    m.reset();
+    const double t_up = ms();
     // Non-negative weights: the parallel fixpoint (eager_bfs.hpp); a negative weight:
     // the exact replay of the reference's heap order (sp_replay_kernel).  NaN has no
     // order in the reference's compare (std.math.order): reported as an error.
     if (!up.ok || up.nan) return kInvalid;
-    const uint64_t cap = std::max<uint64_t>(m->num_states() + 16, 1024);
+    const uint64_t cap = std::max<uint64_t>(m_states + 16, 1024);
     DevOut out(1, cap);
     if (!out.ok()) return kInvalid;
     LaunchStats st;
@@ -862,6 +935,10 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
         hp.status[0] == kPathOutputFull)
       return kInvalid;
     result = chain_result(hp, 0);  // OK or EMPTY
+    if (hprof)
+      std::fprintf(stderr,
+                   "[libfst_amd host] fst_shortest_path call: snapshot %.2f upload %.2f engine + "
+                   "result %.2f ms\n", t_snap, t_up - t_snap, ms() - t_up);
   }
   std::lock_guard<std::mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
