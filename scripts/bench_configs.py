@@ -133,11 +133,37 @@ def config3(T=1024, n=4096):
             "cpu_kind": "port, 1 thread"}
 
 
+def cpu_pipeline_rate(blobs, labels, offsets, sem, threads=16):
+    """CPU port, two stages on `threads` host threads: each stage's compose timed by the
+    oracle (or_batch_time), the projection between them (printOutputString ->
+    compileString) done untimed in numpy."""
+    secs = 0.0
+    num = len(offsets) - 1
+    for k, blob in enumerate(blobs):
+        t, _ = O.batch_time(blob, labels, offsets, sem, threads)
+        secs += t
+        if k + 1 == len(blobs):
+            break
+        ref = O.batch_run(blob, labels, offsets, sem, 1, threads)
+        seqs = []
+        for i in range(num):
+            ol = ref.olabels[int(ref.offsets[i]):int(ref.offsets[i + 1])]
+            ok = ref.status[i] == 0 and ref.empty[i] == 0
+            seqs.append(ol[ol != 0] if ok else np.array([0xFFFFFFFF], np.uint32))
+        lens = [len(x) for x in seqs]
+        offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        labels = np.concatenate(seqs).astype(np.uint32) if seqs else np.zeros(0, np.uint32)
+    return num / secs
+
+
 def config4(n=65536):
     stages = [SY.to_mutable(SY.tagger()).freeze(), SY.to_mutable(SY.verbalizer()).freeze()]
     rng = np.random.default_rng(44)
     texts = SY.utterances(rng, n)
     labels, offsets = SY.to_labels(texts)
+    blobs = [D.blob_bytes(f) for f in stages]
+    threads = min(16, os.cpu_count() or 1)
+    ncpu = min(n, 16384)
     out = []
     for sem, name in ((F.FST_SEM_LAZY, "lazy (fst_compose_frozen_shortest_path)"),
                       (F.FST_SEM_EAGER, "eager")):
@@ -150,8 +176,12 @@ def config4(n=65536):
             walls.append(time.perf_counter() - t0)
         wall = float(np.median(walls))
         ok = int((r.status == 0).sum())
+        cpu = cpu_pipeline_rate(blobs, labels[:int(offsets[ncpu])], offsets[:ncpu + 1],
+                                0 if sem == F.FST_SEM_LAZY else 1, threads)
         out.append({"config": 4, "workload": f"tagger -> verbalizer (synthetic stand-ins), {n} utterances, {name}",
                     "strings_per_s": n / wall, "ok": ok, "walls_s": walls,
+                    "cpu_oracle_strings_per_s": cpu, "cpu_sample": ncpu,
+                    "cpu_kind": f"port, {threads} threads, both stages (projection untimed)",
                     "note": "host API end to end: H2D inputs, 2 stages + device projection, "
                             "D2H results; median of 3 after a full-size warm-up call"})
     return out
