@@ -521,12 +521,18 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
   // also carries the rhs epsilon arcs (a tagger's or verbalizer's multi-symbol outputs),
   // so start at 4 arcs per label rather than run the whole batch twice on OUTPUT_FULL.
   uint64_t arc_cap = std::max<uint64_t>((D.has_eps ? 4 : 1) * total_labels + 16, 1024);
-  if (const char* e = std::getenv("FSTAMD_ARENA_ARCS"))  // test override: first arena size
-    if (*e) arc_cap = std::max<uint64_t>(std::strtoull(e, nullptr, 10), 1);
+  // test override: the first arena size, grown x4 per attempt (so that 6 attempts can run
+  // out, tests/test_gpu_watchdog.py) instead of sized from the demand
+  bool fixed_growth = false;
+  if (const char* e = std::getenv("FSTAMD_ARENA_ARCS"))
+    if (*e) {
+      arc_cap = std::max<uint64_t>(std::strtoull(e, nullptr, 10), 1);
+      fixed_growth = true;
+    }
   DeviceEngine& E = DeviceEngine::get(dev);
   std::lock_guard<std::mutex> lk(E.mutex());
   constexpr int kAttempts = 6;
-  for (int attempt = 0; attempt < kAttempts; ++attempt, arc_cap *= 4) {
+  for (int attempt = 0; attempt < kAttempts; ++attempt) {
     if (t_prof) t_prof->lap(7);
     auto out = std::make_unique<DevOut>(num, arc_cap);
     if (!out->ok()) return FST_OOM;
@@ -560,6 +566,11 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
       if (keep) *keep = std::move(out);
       return FST_OK;
     }
+    // every engine reserves a path with atomicAdd on the cursor before it checks the
+    // capacity, so the cursor ends at the arcs the whole batch needs: one rerun suffices
+    unsigned long long need = 0;
+    if (hipMemcpy(&need, out->v.cursor, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
+    arc_cap = fixed_growth ? arc_cap * 4 : std::max<uint64_t>(arc_cap * 2, need + 1024);
   }
   return FST_OOM;  // unreachable: the last attempt returns above
 }
