@@ -700,7 +700,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                               (uint64_t)ws.ncap * (8 + 8 + 16 + 8) +
                               (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
     if (per_wave > (24ull << 30)) return hipErrorOutOfMemory;
-    uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 16, num_items);
+    uint32_t grid =
+        (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 4 * FSTAMD_REPLAY_WAVES, num_items);
     // latency-bound: as many waves in flight as the SIMDs hold (4/SIMD), within 20 GB of
     // the 288 GB HBM
     const uint64_t budget = 20ull << 30;
@@ -1139,7 +1140,7 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     // barriers, 4x the strings in flight); FSTAMD_BFS_WG0=256 for A/B runs
     const char* wge = std::getenv("FSTAMD_BFS_WG0");
     const bool wave = tier == 0 && !(wge && std::strcmp(wge, "256") == 0);
-    const uint64_t per_cu = tier == 0 ? (wave ? 4 * kBfsWgPerCu0 : kBfsWgPerCu0) : 1;
+    const uint64_t per_cu = tier == 0 ? (wave ? 4 * FSTAMD_BFS_WAVES64 : kBfsWgPerCu0) : 1;
     const uint32_t grid =
         (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_ * per_cu, fit});
     BfsWs ws{};

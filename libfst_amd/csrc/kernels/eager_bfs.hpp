@@ -935,8 +935,12 @@ __device__ void sp_replay(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
 }
 
 
+#ifndef FSTAMD_BFS_WAVES64  // waves per SIMD of the one-wavefront instance (config 4 eager:
+// 6 waves, 84 B of spills, engine 39.5 ms vs 47.2 ms at 4 waves spill-free; 8: 40.0 ms)
+#define FSTAMD_BFS_WAVES64 6
+#endif
 template <int WG, bool kGraph>
-__global__ void __launch_bounds__(WG)
+__global__ void __launch_bounds__(WG, WG == 64 ? FSTAMD_BFS_WAVES64 : 1)
 eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, const uint32_t* num_items_dev,
                  uint32_t num_items_host, BfsWs ws, BatchOutDev out) {

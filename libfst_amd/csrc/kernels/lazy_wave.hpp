@@ -268,8 +268,12 @@ struct LazyLds {
   uint32_t id[64];
 };
 
+#ifndef FSTAMD_REPLAY_WAVES  // waves per SIMD of the hashed replay (config 4 lazy: 4 spill-free
+// 18.4 ms per call, 6 and 8 with spills 20.4 ms)
+#define FSTAMD_REPLAY_WAVES 4
+#endif
 template <bool kGraph>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, FSTAMD_REPLAY_WAVES)
 lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, uint32_t num_items, LazyWs ws,
                  BatchOutDev out) {
