@@ -291,12 +291,32 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint32_t ruu =
             (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ou) >> 32) &
             kLpRunMask;
+        // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
+        // round trip: its certificate alone usually settles C
+        const uint32_t ob = pres ? (c & 0x1FFFu) : 8u * W;
+        const double tbb = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + ob);
+        const uint32_t rbb =
+            (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ob) >> 32) &
+            kLpRunMask;
         const double tx = du;
         const uint32_t rx = 1u + (tbu == tx ? ruu : 0u);
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
-        // source certified by (tb, run)
+        // source certified by (tb, run).  The back source is tight, so its certificate is
+        // sufficient; the loop over every tight in-arc runs only for rows where some lane
+        // is left without one
+        const bool fast = !pres || tpos || tbb < tx || (tbb == tx && rbb < rx);
+#ifdef FSTAMD_LP_NOCERT  // timing experiment only: no certificate check
+        if (false) {
+#elif defined(FSTAMD_LP_FULLCERT)  // A/B: the full loop on every row that needs it
         if (check_c && __ballot(pres && (!tpos || nb > 1))) {
+#else
+        if (check_c && __ballot(!fast)) {
+#endif
+#ifdef FSTAMD_LP_FULLCERT
           bool cert = !pres || tpos;
+#else
+          bool cert = fast;
+#endif
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
             const uint32_t o = bpk[m] & 0x1FFFu;
@@ -467,13 +487,16 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           wave_lds_sync();
           uint32_t ck[EW], cw[EW];
 #pragma unroll
-          for (int e = 0; e < EW; ++e) {
+          for (int e = 0; e < EW; ++e) {  // every row's (key, slot) in one LDS round trip
             ck[e] = 0;
+            if ((uint32_t)e < rows_s && (uint32_t)e * 64 + lane < n_next) ck[e] = S.ord0[e * 64 + lane];
+          }
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {
             cw[e] = 0;
             if ((uint32_t)e >= rows_s) continue;  // uniform
             const uint32_t q = (uint32_t)e * 64 + lane;
             const bool valid = q < n_next;
-            ck[e] = valid ? S.ord0[q] : 0u;
             const uint32_t key = ck[e] >> 9;
             if (valid) atomicOr(&S.mask[key], 1ull << lane);
             wave_lds_sync();
