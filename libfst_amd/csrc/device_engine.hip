@@ -618,17 +618,17 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   //    then the general rounds engine (eager_bfs.hpp, bfs_lazy_path) for its leftovers;
   //  * rhs with input epsilons: the dense replay (kernels/lazy_dense.hpp) -- on epsilon-
   //    dense lattices nearly every tuple sits at one distance and the rounds degenerate to
-  //    one pop each -- with the general rounds engine for its leftovers; small lattices
-  //    ((max_len + 1) * NS <= 16K, e.g. config 4's tagger) go to the hashed replay.
+  //    one pop each -- with the general rounds engine for its leftovers.  Small lattices
+  //    too (config 4's tagger and verbalizer: 15.2 ms per two-stage call of 64K
+  //    utterances vs 18.4 ms in the hashed replay, whose per-wave tables live in HBM).
   // FSTAMD_LAZY_ENGINE=rounds | replay | dense forces one engine (A/B runs, tests).
   const char* le = std::getenv("FSTAMD_LAZY_ENGINE");
   const bool force_rounds = le && std::strcmp(le, "rounds") == 0;
   const bool force_replay = le && std::strcmp(le, "replay") == 0;
   const bool force_dense = le && std::strcmp(le, "dense") == 0;
-  const bool small = (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
   const bool exact_ok = rhs.nonneg && rhs.finite && !force_replay;
-  const bool use_dense = exact_ok && !force_rounds && (force_dense || (rhs.has_eps && !small));
-  const bool use_rounds = exact_ok && !use_dense && (force_rounds || !rhs.has_eps || !small);
+  const bool use_dense = exact_ok && !force_rounds && (force_dense || rhs.has_eps);
+  const bool use_rounds = exact_ok && !use_dense;
   if (use_dense) {
     if (stats) {
       stats->engine = 5;
