@@ -1109,6 +1109,20 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
   return hipSuccess;
 }
 
+namespace {
+// resident tiny-tier workgroups per CU (LDS-bound), asked of the runtime once
+int tiny_per_cu() {
+  static const int occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &o, (const void*)eager_bfs_kernel<64, false, true>, 64, 0) != hipSuccess)
+      o = 1;
+    return std::max(o, 1);
+  }();
+  return occ;
+}
+}  // namespace
+
 hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                        const BatchOutDev& out, hipStream_t stream, bool all,
                                        bool lazy, bool replay) {
@@ -1132,21 +1146,28 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
   uint32_t count = 0;
   HIP_TRY(hipMemcpyAsync(&count, cnt, 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  for (int tier = 0; count > 0; ++tier) {
-    const BfsCaps c = bfs_caps(tier);
-    const uint64_t fit = std::max<uint64_t>(1, kBfsBudget / c.stride);
+  // Tier -1 (tiny, tables in LDS, kernels/eager_bfs.hpp kTiny*) first when the lattices are
+  // small by the product bound; not for the exact heap replay (negative weights), whose
+  // heap lives in HBM.  FSTAMD_BFS_TINY=0 turns it off (A/B runs, tests).
+  const char* te = std::getenv("FSTAMD_BFS_TINY");
+  const bool tiny = !replay && !(te && std::strcmp(te, "0") == 0) &&
+                    (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
+  for (int tier = tiny ? -1 : 0; count > 0; ++tier) {
+    const BfsCaps c = tier < 0 ? BfsCaps{kTinyN, kTinyA, kTinyH, kTinyL, 0} : bfs_caps(tier);
+    const uint64_t fit = tier < 0 ? ~0ull : std::max<uint64_t>(1, kBfsBudget / c.stride);
     if (kBfsBudget < c.stride) break;  // beyond the budget: those strings stay OVERFLOW
     // tier 0: small lattices -> one wavefront per string by default (wave-level
     // barriers, 4x the strings in flight); FSTAMD_BFS_WG0=256 for A/B runs
     const char* wge = std::getenv("FSTAMD_BFS_WG0");
     const bool wave = tier == 0 && !(wge && std::strcmp(wge, "256") == 0);
-    const uint64_t per_cu = tier == 0 ? (wave ? 4 * FSTAMD_BFS_WAVES64 : kBfsWgPerCu0) : 1;
+    const uint64_t per_cu = tier < 0 ? (uint64_t)tiny_per_cu()
+                            : tier == 0 ? (wave ? 4 * FSTAMD_BFS_WAVES64 : kBfsWgPerCu0) : 1;
     const uint32_t grid =
         (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_ * per_cu, fit});
     BfsWs ws{};
-    ws.slab = (uint8_t*)scratch(kBfsSlab, (size_t)grid * c.stride);
+    ws.slab = tier < 0 ? nullptr : (uint8_t*)scratch(kBfsSlab, (size_t)grid * c.stride);
     ws.hdr = (uint32_t*)scratch(kBfsHdr, (size_t)grid * 8 * 4);
-    if (!ws.slab || !ws.hdr) return hipErrorOutOfMemory;
+    if ((tier >= 0 && !ws.slab) || !ws.hdr) return hipErrorOutOfMemory;
     ws.stride = c.stride;
     ws.ncap = c.ncap;
     ws.acap = c.acap;
@@ -1165,7 +1186,10 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)grid * 64, stream));
     HIP_TRY(hipMemsetAsync(cnt + 1, 0, 8, stream));  // item counter + next list count
     GraphInput none{};
-    if (wave)
+    if (tier < 0)
+      eager_bfs_kernel<64, false, true><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1,
+                                                                 list, cnt, 0, ws, out);
+    else if (wave)
       eager_bfs_kernel<64, false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1, list,
                                                            cnt, 0, ws, out);
     else
@@ -1182,7 +1206,7 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
                    "[bfs prof] tier %d grid %u wg %d items %llu | us/item: compose %.1f "
                    "fixpoint %.1f rounds %.1f tail %.1f | rounds/item %.1f active/round %.1f "
                    "members/round %.1f\n",
-                   tier, grid, wave ? 64 : kBfsWG, sum[4], sum[0] / 100.0 / sum[4],
+                   tier, grid, (wave || tier < 0) ? 64 : kBfsWG, sum[4], sum[0] / 100.0 / sum[4],
                    sum[1] / 100.0 / sum[4], sum[2] / 100.0 / sum[4], sum[3] / 100.0 / sum[4],
                    (double)sum[5] / sum[4], (double)sum[6] / std::max(1ull, sum[5]),
                    (double)sum[7] / std::max(1ull, sum[5]));

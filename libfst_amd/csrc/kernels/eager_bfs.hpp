@@ -76,9 +76,9 @@ struct BfsTables {
   uint32_t* cslot;           // [acap + ncap] hash slot of the arc's target (level scratch)
 };
 
-__host__ __device__ inline size_t bfs_slab_bytes(uint32_t ncap, uint32_t acap, uint32_t hcap,
-                                                 uint32_t lcap) {
-  auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+__host__ __device__ constexpr size_t bfs_slab_bytes(uint32_t ncap, uint32_t acap, uint32_t hcap,
+                                                    uint32_t lcap, size_t align = 256) {
+  auto r = [align](size_t b) { return (b + align - 1) & ~(align - 1); };
   return r((size_t)hcap * 8) + r((size_t)hcap * 4) + r((size_t)ncap * 8) +
          r(((size_t)ncap + 1) * 4) + r(((size_t)lcap + 2) * 4) + r((size_t)ncap * 8) +
          r((size_t)ncap * 8) + r((size_t)ncap * 8) + r((size_t)acap * 4) * 3 +
@@ -86,10 +86,10 @@ __host__ __device__ inline size_t bfs_slab_bytes(uint32_t ncap, uint32_t acap, u
 }
 
 __device__ inline BfsTables bfs_carve(uint8_t* p, uint32_t ncap, uint32_t acap, uint32_t hcap,
-                                      uint32_t lcap) {
+                                      uint32_t lcap, size_t align = 256) {
   auto take = [&](size_t b) {
     uint8_t* q = p;
-    p += (b + 255) & ~(size_t)255;
+    p += (b + align - 1) & ~(align - 1);
     return q;
   };
   BfsTables t;
@@ -939,15 +939,36 @@ __device__ void sp_replay(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
 // 6 waves, 84 B of spills, engine 39.5 ms vs 47.2 ms at 4 waves spill-free; 8: 40.0 ms)
 #define FSTAMD_BFS_WAVES64 6
 #endif
-template <int WG, bool kGraph>
-__global__ void __launch_bounds__(WG, WG == 64 ? FSTAMD_BFS_WAVES64 : 1)
+// The tiny tier: small lattices (config 4's tagger and verbalizer: 43 / 72 tuples per
+// utterance on average) keep every table in LDS instead of an HBM slab, so a BFS level
+// costs LDS round trips rather than HBM ones, and no string clears a 384 KB HBM hash.
+// Strings that outgrow it report OVERFLOW and move on to tier 0.  The caps are the
+// host's ws.* values for this tier (device_engine.hip run_bfs_chain).
+constexpr uint32_t kTinyN = 128, kTinyA = 448, kTinyH = 256, kTinyL = 128;
+constexpr size_t kTinyAlign = 16;
+constexpr size_t kTinyBytes = bfs_slab_bytes(kTinyN, kTinyA, kTinyH, kTinyL, kTinyAlign);
+constexpr int kTinyWaves = 2;  // per SIMD: ~20 KB of LDS each, 8 workgroups per CU
+// (A/B on config 4: with the ~3 KB rhs copied into LDS as well a string took 143 / 288 us
+// instead of 178 / 338 us, but 6 workgroups fit per CU instead of 8: no faster overall)
+
+template <int WG, bool kGraph, bool kTiny = false>
+__global__ void __launch_bounds__(WG, WG == 64 ? (kTiny ? kTinyWaves : FSTAMD_BFS_WAVES64) : 1)
 eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, const uint32_t* num_items_dev,
                  uint32_t num_items_host, BfsWs ws, BatchOutDev out) {
+  static_assert(!kTiny || (!kGraph && WG == 64), "the tiny tier is the chain batch's wave tier");
   __shared__ BfsShared SH;
   const uint32_t tid = threadIdx.x;
-  BfsTables T = bfs_carve(ws.slab + (size_t)blockIdx.x * ws.stride, ws.ncap, ws.acap, ws.hcap,
-                          ws.lcap);
+  BfsTables T;
+  [[maybe_unused]] uint32_t* tiny_lab = nullptr;
+  if constexpr (kTiny) {
+    __shared__ __attribute__((aligned(16))) uint8_t tiny_slab[kTinyBytes];
+    __shared__ uint32_t tiny_labels[kTinyL];
+    T = bfs_carve(tiny_slab, kTinyN, kTinyA, kTinyH, kTinyL, kTinyAlign);
+    tiny_lab = tiny_labels;
+  } else {
+    T = bfs_carve(ws.slab + (size_t)blockIdx.x * ws.stride, ws.ncap, ws.acap, ws.hcap, ws.lcap);
+  }
   uint32_t* hdr = ws.hdr + (size_t)blockIdx.x * 8;
   unsigned long long* prof = ws.prof ? ws.prof + (size_t)blockIdx.x * 8 : nullptr;
   const uint32_t num_items = num_items_dev ? *num_items_dev : num_items_host;
@@ -977,6 +998,15 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       const uint64_t off = in.offsets[si];
       lhs.labels = in.labels + off;
       lhs.L = (uint32_t)(in.offsets[si + 1] - off);
+      if constexpr (kTiny) {  // the labels in LDS; a chain this long needs more levels anyway
+        if (lhs.L + 2 > kTinyL) {
+          if (tid == 0) write_status(out, si, kPathOverflow, 0, 0);
+          continue;
+        }
+        for (uint32_t i = tid; i < lhs.L; i += WG) tiny_lab[i] = lhs.labels[i];
+        lhs.labels = tiny_lab;
+        __syncthreads();
+      }
     }
     const bool no_start = rhs.start == kNoState || lhs.start() == kNoState;
     if (!ws.lattice_only && (no_start || n_best != 1)) {

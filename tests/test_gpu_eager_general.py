@@ -243,3 +243,37 @@ def test_batch_eager_negative_weights(seed):
             for i in range(48)]
     check(blob, *csr(seqs), EAGER)
     assert F.last_launch_stats().engine == 6
+
+
+@pytest.mark.parametrize("sem", ["eager", "lazy_rounds"])
+@pytest.mark.parametrize("seed", range(6))
+def test_batch_tiny_tier_mixed_sizes(monkeypatch, sem, seed):
+    # the general engine's tiny tier (tables and labels in LDS: eager_bfs.hpp kTiny*) takes
+    # the short strings; strings past its label / node / arc caps report OVERFLOW there and
+    # finish in the HBM tiers.  Bit-exact against the oracle, for both semantics (lazy
+    # through the general rounds engine)
+    if sem == "lazy_rounds":
+        monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "rounds")
+    rng = np.random.default_rng(8100 + seed)
+    f = random_rhs(rng, int(rng.integers(3, 24)), int(rng.integers(8, 80)), 4, eps=True,
+                   frac=seed % 2 == 1)
+    blob = O.freeze(f)
+    lens = [int(x) for x in rng.integers(0, 24, 56)] + [100, 125, 126, 127, 140, 60, 90, 33]
+    seqs = [[int(x) for x in rng.integers(1 if i % 5 else 0, 5, L)] for i, L in enumerate(lens)]
+    check(blob, *csr(seqs), EAGER if sem == "eager" else LAZY)
+
+
+def test_batch_tiny_tier_off_matches(monkeypatch):
+    # FSTAMD_BFS_TINY=0 (HBM tiers only) gives the same bits as the default on config 4's
+    # stand-ins (the tiny tier with the rhs in LDS)
+    import libfst_amd.synthetic as SY
+    stages = [SY.to_mutable(SY.tagger()).freeze(), SY.to_mutable(SY.verbalizer()).freeze()]
+    labels, offsets = SY.to_labels(SY.utterances(np.random.default_rng(9), 512))
+    a = F.pipeline_batch(stages, labels, offsets, 1, EAGER)
+    monkeypatch.setenv("FSTAMD_BFS_TINY", "0")
+    b = F.pipeline_batch(stages, labels, offsets, 1, EAGER)
+    assert np.array_equal(a.status, b.status) and np.all(a.status == F.FST_PATH_OK)
+    assert np.array_equal(a.offsets, b.offsets)
+    assert np.array_equal(a.ilabels, b.ilabels) and np.array_equal(a.olabels, b.olabels)
+    assert np.array_equal(a.weights.view(np.uint64), b.weights.view(np.uint64))
+    assert np.array_equal(a.finals.view(np.uint64), b.finals.view(np.uint64))
