@@ -167,9 +167,10 @@ def config4(n=65536):
     out = []
     for sem, name in ((F.FST_SEM_LAZY, "lazy (fst_compose_frozen_shortest_path)"),
                       (F.FST_SEM_EAGER, "eager")):
-        # one untimed call with the full batch (workspace growth), then the median of 7
-        # (host-side outliers of 10-20 ms hit single calls of either semantics)
-        F.pipeline_batch(stages, labels, offsets, 1, sem)
+        # three untimed calls with the full batch (workspace growth: the first lazy calls
+        # after start-up still run 2x slower on the host side), then the median of 7
+        for _ in range(3):
+            F.pipeline_batch(stages, labels, offsets, 1, sem)
         walls = []
         for _ in range(7):
             t0 = time.perf_counter()
@@ -184,7 +185,7 @@ def config4(n=65536):
                     "cpu_oracle_strings_per_s": cpu, "cpu_sample": ncpu,
                     "cpu_kind": f"port, {threads} threads, both stages (projection untimed)",
                     "note": "host API end to end: H2D inputs, 2 stages + device projection, "
-                            "D2H results; median of 7 after a full-size warm-up call"})
+                            "D2H results; median of 7 after 3 full-size warm-up calls"})
     return out
 
 
