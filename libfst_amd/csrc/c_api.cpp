@@ -379,6 +379,36 @@ struct GraphUpload {
   }
 };
 
+// A single-call lhs that is exactly a compileString acceptor (src/string.zig:24-50: states
+// 0..L, arc k = (c, c, One, k + 1), final(L) = One, no other final) is the batch API's chain
+// input: its labels.  Such a call runs the batch engines on one string (the layered pull
+// tiers, the dense replay), not the general-lhs hashed replay: 1^64 on the metric rhs took
+// 93 ms there (one wave popping 8,385 tuples through HBM tables).
+bool as_chain(const MutableFst& a, std::vector<uint32_t>* labels) {
+  const size_t ns = a.num_states();
+  if (ns == 0 || a.start() != 0 || ns > (1u << 30)) return false;
+  auto bits = [](double x) {
+    uint64_t u;
+    std::memcpy(&u, &x, 8);
+    return u;
+  };
+  const uint32_t L = (uint32_t)(ns - 1);
+  labels->resize(L);
+  for (uint32_t k = 0; k <= L; ++k) {
+    const auto& arcs = a.arcs(k);
+    if (k == L) {
+      if (!arcs.empty() || bits(a.final_weight(k)) != bits(w_one())) return false;
+      break;
+    }
+    if (arcs.size() != 1 || !std::isinf(a.final_weight(k)) || a.final_weight(k) < 0) return false;
+    const Arc& x = arcs[0];
+    if (x.nextstate != k + 1 || x.ilabel != x.olabel || bits(x.weight) != bits(w_one()))
+      return false;
+    (*labels)[k] = x.ilabel;
+  }
+  return true;
+}
+
 // Lazy 1-best of one general lhs on the GPU (single-call C ABI path).
 int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* result,
                     double* kernel_ms) {
@@ -805,7 +835,24 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
   } else {
     if (!gpu_available()) return kInvalid;
     double kms = 0;
-    const int rc = run_lazy_single(*a, *b, n, &result, &kms);
+    int rc = -1;
+    std::vector<uint32_t> chain;
+    if (as_chain(*a, &chain)) {  // the batch engines on one string
+      const uint64_t offs[2] = {0, chain.size()};
+      HostPaths h;
+      if (run_chain_batch_host(*b, chain.data(), offs, 1, n, FST_SEM_LAZY, -1, &h) == FST_OK) {
+        const int32_t st = h.status[0];
+        if (st == kPathOk || st == kPathEmpty) {
+          result = chain_result(h, 0);
+          rc = 0;
+        } else if (st == kPathCycle) {
+          rc = 3;  // as the general path: the reference would not terminate
+        }
+        kms = t_last_stats.kernel_ms;
+      }
+    }
+    // anything else (a general lhs; a string the batch engines handed back): one general lhs
+    if (rc < 0) rc = run_lazy_single(*a, *b, n, &result, &kms);
     if (rc != 0) {
       trace("sp_compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(),
             kms);

@@ -246,3 +246,34 @@ def test_single_call_random_graphs(seed):
     lhs = random_rhs(rng, int(rng.integers(1, 10)), int(rng.integers(1, 30)), 3, eps=True)
     rhs = random_rhs(rng, int(rng.integers(1, 20)), int(rng.integers(1, 80)), 3, eps=True)
     compare_single(lhs, O.freeze(rhs))
+
+
+@pytest.mark.parametrize("rhs_kind", ["ambiguous", "eps_dense", "random_eps"])
+def test_single_call_chain_route(rhs_kind):
+    # a compileString lhs runs the batch engines on one string (c_api.cpp as_chain): the
+    # layered pull tier on the metric rhs, the dense replay on an epsilon rhs; near-chains
+    # (a weight, a second final, an output label that differs) keep the general-lhs path.
+    # Both bit-exact against the oracle's composeShortestPath
+    rng = np.random.default_rng(41)
+    if rhs_kind == "ambiguous":
+        blob = O.freeze(O.gen("ambiguous", 512, 12))
+    elif rhs_kind == "eps_dense":
+        blob = O.freeze(O.gen("eps_dense", 128, 6))
+    else:
+        blob = O.freeze(random_rhs(rng, 12, 60, 4, eps=True))
+    for text in (b"", b"\x00", b"\x00" * 37, bytes(rng.integers(0, 4, 19).tolist())):
+        lhs = O.compile_string(text)
+        compare_single(lhs, blob)
+        if rhs_kind == "ambiguous" and text:
+            assert F.last_launch_stats().engine == 7  # the lazy pull tier took it
+        if len(text) > 2:
+            near = O.compile_string(text)
+            near.arcs[1] = [(near.arcs[1][0][0], near.arcs[1][0][1], 0.5, 2)]
+            compare_single(near, blob)
+            near = O.compile_string(text)
+            near.finals[1] = 0.25
+            compare_single(near, blob)
+            near = O.compile_string(text)
+            a = near.arcs[0][0]
+            near.arcs[0] = [(a[0], a[1] + 1, a[2], a[3])]
+            compare_single(near, blob)
