@@ -840,7 +840,12 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
     if (as_chain(*a, &chain)) {  // the batch engines on one string
       const uint64_t offs[2] = {0, chain.size()};
       HostPaths h;
-      if (run_chain_batch_host(*b, chain.data(), offs, 1, n, FST_SEM_LAZY, -1, &h) == FST_OK) {
+      HostProf prof;  // FSTAMD_HOST_PROF=1: where the call's time goes
+      t_prof = &prof;
+      const FstError e = run_chain_batch_host(*b, chain.data(), offs, 1, n, FST_SEM_LAZY, -1, &h);
+      t_prof = nullptr;
+      prof.print("fst_compose_frozen_shortest_path");
+      if (e == FST_OK) {
         const int32_t st = h.status[0];
         if (st == kPathOk || st == kPathEmpty) {
           result = chain_result(h, 0);
