@@ -944,10 +944,11 @@ __device__ void sp_replay(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
 // costs LDS round trips rather than HBM ones, and no string clears a 384 KB HBM hash.
 // Strings that outgrow it report OVERFLOW and move on to tier 0.  The caps are the
 // host's ws.* values for this tier (device_engine.hip run_bfs_chain).
-constexpr uint32_t kTinyN = 128, kTinyA = 448, kTinyH = 256, kTinyL = 128;
+// (config 4's lattices: at most 87 / 159 tuples and 1.0-1.3 arcs per tuple)
+constexpr uint32_t kTinyN = 128, kTinyA = 192, kTinyH = 256, kTinyL = 128;
 constexpr size_t kTinyAlign = 16;
 constexpr size_t kTinyBytes = bfs_slab_bytes(kTinyN, kTinyA, kTinyH, kTinyL, kTinyAlign);
-constexpr int kTinyWaves = 2;  // per SIMD: ~20 KB of LDS each, 8 workgroups per CU
+constexpr int kTinyWaves = 3;  // per SIMD: ~14 KB of LDS each, 11 workgroups per CU
 // (A/B on config 4: with the ~3 KB rhs copied into LDS as well a string took 143 / 288 us
 // instead of 178 / 338 us, but 6 workgroups fit per CU instead of 8: no faster overall)
 
