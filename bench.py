@@ -208,7 +208,7 @@ def timed(batch, rhs, sem, dev_index, steps, warmup, world):
     return el, kms, st
 
 
-def cpu_baseline(args, blob_bytes, sem):
+def cpu_baseline(args, blob_bytes, sem, seconds=None):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ffi as O  # checker / CPU baseline only
 
@@ -224,7 +224,8 @@ def cpu_baseline(args, blob_bytes, sem):
     probe = 64
     s = run(probe, 1)
     single = probe / s
-    n = int(max(threads * 8, min(2_000_000, single * threads * args.cpu_seconds * 0.8)))
+    budget = args.cpu_seconds if seconds is None else seconds
+    n = int(max(threads * 8, min(2_000_000, single * threads * budget * 0.8)))
     s = run(n, threads)
     return {"value": n / s, "unit": "strings/s", "cores": threads, "kind": "port",
             "single_thread_value": single,
@@ -309,6 +310,8 @@ def main():
                          "batch": args.lazy_batch,
                          "checked_vs_oracle": check_sample(lb, blob_check, F.FST_SEM_LAZY),
                          "note": "fst_compose_frozen_shortest_path semantics (lazy_pull_kernel, exact vs the oracle)"}
+        if rank == 0 and not args.no_cpu and world == 1:  # the CPU port beside it (~3 s)
+            extra["lazy"]["cpu_baseline"] = cpu_baseline(args, blob_check, 0, seconds=3.0)
 
     if rank == 0:
         traffic, traffic_src = measured_traffic(args, sem)
