@@ -281,6 +281,10 @@ def main():
     avg_k = float(np.mean(kms))
     balg = b_alg_bytes(work, lengths, plen)   # bytes per launch on this rank
     achieved = balg / (avg_k * 1e-3) / 1e9
+    # relaxations per second and the compulsory HBM bytes (labels in,
+    # path + status/offset/final out) beside the logical bytes
+    relax_per_s = float(work[1::2].astype(np.int64).sum()) / (avg_k * 1e-3)
+    compulsory = int((4 * lengths + 16 * plen + 24).sum())
 
     extra = {}
     if args.varied:
@@ -342,6 +346,8 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel_ms": avg_k, "b_alg_per_string": balg / args.batch,
+                         "relaxations_per_s": relax_per_s,
+                         "compulsory_bytes_per_string": compulsory / args.batch,
                          "kernel": EAGER_KERNEL if sem else LAZY_KERNEL,
                          # measured DRAM bytes / kernel time: what really crosses HBM
                          "hbm_traffic_gbs": (traffic / (avg_k * 1e-3) / 1e9) if traffic else None,
