@@ -112,8 +112,22 @@ __device__ __forceinline__ void span_summary(const RhsView& r, uint32_t s, uint3
   }
 }
 
-// Wavefront inclusive prefix sum (64 lanes).
+// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8, row_bcast 15/31):
+// six VALU ops, no LDS round trip; every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+// Wavefront inclusive prefix sum (64 lanes): DPP when the whole wave is active (the
+// callers' usual case: uniform control flow), else shuffles (six ds_bpermute round trips).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  if (__builtin_amdgcn_read_exec() == ~0ull) return wave_incl_scan_dpp(x);
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -130,7 +144,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t inc = wave_incl_scan(v);
   if constexpr (WG == 64) {
-    total = __shfl(inc, 63, 64);
+    total = __builtin_amdgcn_readlane(inc, 63);
     return inc - v;
   } else {
     if (lane == 63) scratch[w] = inc;

@@ -63,18 +63,6 @@ struct PullLds {
   ChaseJob job[kChaseBatch];
 };
 
-// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8, row_bcast 15/31);
-// every lane must be active.
-__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-  return x;
-}
-
 // One in-arc record against the current layer's cells: its candidate key and distance.
 template <int W>
 __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec& r,
