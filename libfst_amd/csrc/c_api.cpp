@@ -188,6 +188,70 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
 };
 
+// Result arrays of the batch entries (FstBatchResult) come from a pool of pinned host
+// blocks: the device writes them by DMA, with no staging through the runtime's bounce
+// buffers and no page faults on freshly malloc'd pages every call (config 4 returns ~50 MB
+// of paths per 64 K utterances).  fst_batch_result_free gives them back; beyond
+// kPinPoolMax held they are freed.  A failed pinned allocation falls back to malloc.
+constexpr size_t kPinPoolMax = 4ull << 30;
+struct PinPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free;       // size class -> pinned block
+  std::map<void*, std::pair<size_t, bool>> live;  // block -> (size class, pinned)
+  size_t held = 0;
+};
+PinPool& pin_pool() {
+  static PinPool* p = new PinPool;  // never destroyed: results may outlive static teardown
+  return *p;
+}
+void* pin_alloc(size_t n) {
+  size_t c = 4096;
+  while (c < n) c <<= 1;
+  PinPool& P = pin_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  auto it = P.free.find(c);
+  if (it != P.free.end()) {
+    void* p = it->second;
+    P.free.erase(it);
+    P.held -= c;
+    P.live[p] = {c, true};
+    return p;
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, c, hipHostMallocDefault) == hipSuccess && p) {
+    P.live[p] = {c, true};
+    return p;
+  }
+  p = std::malloc(c);
+  if (p) P.live[p] = {c, false};
+  return p;
+}
+void pin_release(void* p) {
+  if (!p) return;
+  PinPool& P = pin_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  auto it = P.live.find(p);
+  if (it == P.live.end()) return;  // not ours (never happens through the API)
+  const size_t c = it->second.first;
+  const bool pinned = it->second.second;
+  P.live.erase(it);
+  if (!pinned) {
+    std::free(p);
+  } else if (P.held + c <= kPinPoolMax) {
+    P.free.insert({c, p});
+    P.held += c;
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+void pin_pool_clear() {
+  PinPool& P = pin_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  for (auto& kv : P.free) (void)hipHostFree(kv.second);
+  P.free.clear();
+  P.held = 0;
+}
+
 struct HostPaths {
   std::vector<int32_t> status;
   std::vector<uint32_t> len;
@@ -520,12 +584,12 @@ FstError download_batch_result(int dev, const DevOut& o, uint32_t num, const int
   if (t_prof) t_prof->lap(4);
   out->num_strings = num;
   out->total_arcs = tot;
-  out->status = (int32_t*)std::malloc(std::max<size_t>(num, 1) * 4);
-  out->path_offsets = (uint64_t*)std::malloc((num + 1ull) * 8);
-  out->final_weights = (double*)std::malloc(std::max<size_t>(num, 1) * 8);
-  out->ilabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
-  out->olabels = (uint32_t*)std::malloc(std::max<uint64_t>(tot, 1) * 4);
-  out->weights = (double*)std::malloc(std::max<uint64_t>(tot, 1) * 8);
+  out->status = (int32_t*)pin_alloc(std::max<size_t>(num, 1) * 4);
+  out->path_offsets = (uint64_t*)pin_alloc((num + 1ull) * 8);
+  out->final_weights = (double*)pin_alloc(std::max<size_t>(num, 1) * 8);
+  out->ilabels = (uint32_t*)pin_alloc(std::max<uint64_t>(tot, 1) * 4);
+  out->olabels = (uint32_t*)pin_alloc(std::max<uint64_t>(tot, 1) * 4);
+  out->weights = (double*)pin_alloc(std::max<uint64_t>(tot, 1) * 8);
   if (!out->status || !out->path_offsets || !out->final_weights || !out->ilabels ||
       !out->olabels || !out->weights)
     return FST_OOM;
@@ -1042,6 +1106,7 @@ void fst_teardown(void) {
     g_fst.clear();
   }
   pool_clear();
+  pin_pool_clear();
 }
 
 // ---- Batched entries (fst_batch.h) ----------------------------------------------------
@@ -1089,12 +1154,12 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
 
 void fst_batch_result_free(FstBatchResult* r) {
   if (!r) return;
-  std::free(r->status);
-  std::free(r->path_offsets);
-  std::free(r->ilabels);
-  std::free(r->olabels);
-  std::free(r->weights);
-  std::free(r->final_weights);
+  pin_release(r->status);
+  pin_release(r->path_offsets);
+  pin_release(r->ilabels);
+  pin_release(r->olabels);
+  pin_release(r->weights);
+  pin_release(r->final_weights);
   std::memset(r, 0, sizeof(*r));
 }
 

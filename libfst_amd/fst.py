@@ -324,22 +324,38 @@ def pipeline_batch(stages, labels, offsets, n: int = 1, semantics: int = FST_SEM
     return _take_result(res, num)
 
 
-def _take_result(res, num) -> BatchResult:
-    L = lib()
-    tot = int(res.total_arcs)
+class _ResultOwner:
+    """Owns one FstBatchResult; fst_batch_result_free runs once no array views it."""
 
-    def arr(p, cnt, dt):
+    def __init__(self, res):
+        self.res = res
+
+    def __del__(self):
+        try:
+            lib().fst_batch_result_free(C.byref(self.res))
+        except Exception:  # interpreter shutdown
+            pass
+
+
+def _take_result(res, num) -> BatchResult:
+    """Numpy views of the library's (pinned) result arrays, no copy: they stay valid while
+    any of the arrays lives, then go back to the library's pool."""
+    tot = int(res.total_arcs)
+    owner = _ResultOwner(res)
+
+    def arr(p, cnt, dt, ct):
         if cnt == 0:
             return np.zeros(0, dt)
-        return np.ctypeslib.as_array(p, shape=(cnt,)).astype(dt, copy=True)
+        buf = (ct * cnt).from_address(C.cast(p, C.c_void_p).value)
+        buf._owner = owner  # the view keeps the result alive
+        return np.frombuffer(buf, dtype=dt)
 
-    out = BatchResult(status=arr(res.status, num, np.int32),
-                      offsets=arr(res.path_offsets, num + 1, np.uint64),
-                      ilabels=arr(res.ilabels, tot, np.uint32), olabels=arr(res.olabels, tot, np.uint32),
-                      weights=arr(res.weights, tot, np.float64),
-                      finals=arr(res.final_weights, num, np.float64))
-    L.fst_batch_result_free(C.byref(res))
-    return out
+    return BatchResult(status=arr(res.status, num, np.int32, C.c_int32),
+                       offsets=arr(res.path_offsets, num + 1, np.uint64, C.c_uint64),
+                       ilabels=arr(res.ilabels, tot, np.uint32, C.c_uint32),
+                       olabels=arr(res.olabels, tot, np.uint32, C.c_uint32),
+                       weights=arr(res.weights, tot, np.float64, C.c_double),
+                       finals=arr(res.final_weights, num, np.float64, C.c_double))
 
 
 def last_launch_stats() -> FstLaunchStats:
