@@ -44,7 +44,8 @@ typedef enum {
     FST_PATH_INTERNAL = 7,     /* engine invariant violated (a bug), reported, never silent */
 } FstPathStatus;
 
-/* Host-memory result of a batch (allocated by the library). */
+/* Host-memory result of a batch, allocated by the library (pooled pinned host blocks the
+ * device writes by DMA) and valid until fst_batch_result_free(), which returns them. */
 typedef struct {
     uint32_t num_strings;
     int32_t* status;          /* [num_strings] FstPathStatus */
