@@ -1110,12 +1110,13 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
 }
 
 namespace {
-// resident tiny-tier workgroups per CU (LDS-bound), asked of the runtime once
+// resident tiny-tier workgroups per CU (LDS-bound), asked of the runtime once per size
+template <int K>
 int tiny_per_cu() {
   static const int occ = [] {
     int o = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &o, (const void*)eager_bfs_kernel<64, false, true>, 64, 0) != hipSuccess)
+            &o, (const void*)eager_bfs_kernel<64, false, K>, 64, 0) != hipSuccess)
       o = 1;
     return std::max(o, 1);
   }();
@@ -1146,21 +1147,23 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
   uint32_t count = 0;
   HIP_TRY(hipMemcpyAsync(&count, cnt, 4, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  // Tier -1 (tiny, tables in LDS, kernels/eager_bfs.hpp kTiny*) first when the lattices are
+  // Tiers -2 and -1 (tiny, tables in LDS, kernels/eager_bfs.hpp tiny_caps) first when the lattices are
   // small by the product bound; not for the exact heap replay (negative weights), whose
   // heap lives in HBM.  FSTAMD_BFS_TINY=0 turns it off (A/B runs, tests).
   const char* te = std::getenv("FSTAMD_BFS_TINY");
   const bool tiny = !replay && !(te && std::strcmp(te, "0") == 0) &&
                     (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
-  for (int tier = tiny ? -1 : 0; count > 0; ++tier) {
-    const BfsCaps c = tier < 0 ? BfsCaps{kTinyN, kTinyA, kTinyH, kTinyL, 0} : bfs_caps(tier);
+  // tier -2: the 128-tuple tiny size, tier -1: the 256-tuple one, then the HBM tiers
+  for (int tier = tiny ? -2 : 0; count > 0; ++tier) {
+    const TinyCaps tc = tiny_caps(tier == -2 ? 1 : 2);
+    const BfsCaps c = tier < 0 ? BfsCaps{tc.n, tc.a, tc.h, tc.l, 0} : bfs_caps(tier);
     const uint64_t fit = tier < 0 ? ~0ull : std::max<uint64_t>(1, kBfsBudget / c.stride);
     if (kBfsBudget < c.stride) break;  // beyond the budget: those strings stay OVERFLOW
     // tier 0: small lattices -> one wavefront per string by default (wave-level
     // barriers, 4x the strings in flight); FSTAMD_BFS_WG0=256 for A/B runs
     const char* wge = std::getenv("FSTAMD_BFS_WG0");
     const bool wave = tier == 0 && !(wge && std::strcmp(wge, "256") == 0);
-    const uint64_t per_cu = tier < 0 ? (uint64_t)tiny_per_cu()
+    const uint64_t per_cu = tier < 0 ? (uint64_t)(tier == -2 ? tiny_per_cu<1>() : tiny_per_cu<2>())
                             : tier == 0 ? (wave ? 4 * FSTAMD_BFS_WAVES64 : kBfsWgPerCu0) : 1;
     const uint32_t grid =
         (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_ * per_cu, fit});
@@ -1186,9 +1189,12 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)grid * 64, stream));
     HIP_TRY(hipMemsetAsync(cnt + 1, 0, 8, stream));  // item counter + next list count
     GraphInput none{};
-    if (tier < 0)
-      eager_bfs_kernel<64, false, true><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1,
-                                                                 list, cnt, 0, ws, out);
+    if (tier == -2)
+      eager_bfs_kernel<64, false, 1><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1,
+                                                              list, cnt, 0, ws, out);
+    else if (tier == -1)
+      eager_bfs_kernel<64, false, 2><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1,
+                                                              list, cnt, 0, ws, out);
     else if (wave)
       eager_bfs_kernel<64, false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1, list,
                                                            cnt, 0, ws, out);

@@ -944,28 +944,42 @@ __device__ void sp_replay(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
 // costs LDS round trips rather than HBM ones, and no string clears a 384 KB HBM hash.
 // Strings that outgrow it report OVERFLOW and move on to tier 0.  The caps are the
 // host's ws.* values for this tier (device_engine.hip run_bfs_chain).
-// (config 4's lattices: at most 87 / 159 tuples and 1.0-1.3 arcs per tuple)
-constexpr uint32_t kTinyN = 128, kTinyA = 192, kTinyH = 256, kTinyL = 128;
+// Two sizes (config 4's lattices: at most 87 / 159 tuples, 1.0-1.3 arcs per tuple, and up
+// to ~150 BFS levels: a verbalizer word is an epsilon chain of 3-5 levels; what outgrows the
+// first size finishes in the second rather than in HBM):
+// kTiny = 1: 128 tuples / 176 arcs / 256 slots / 256 levels, ~14.6 KB, 10-11 per CU;
+// kTiny = 2: 256 tuples / 384 arcs / 512 slots / 512 levels, ~28 KB, 5 per CU.
+// Both hold chains of up to 126 labels in LDS.
+struct TinyCaps {
+  uint32_t n, a, h, l, lab;
+};
+__host__ __device__ constexpr TinyCaps tiny_caps(int k) {
+  return k == 1 ? TinyCaps{128, 176, 256, 256, 128} : TinyCaps{256, 384, 512, 512, 128};
+}
 constexpr size_t kTinyAlign = 16;
-constexpr size_t kTinyBytes = bfs_slab_bytes(kTinyN, kTinyA, kTinyH, kTinyL, kTinyAlign);
-constexpr int kTinyWaves = 3;  // per SIMD: ~14 KB of LDS each, 11 workgroups per CU
+__host__ __device__ constexpr size_t tiny_bytes(int k) {
+  return bfs_slab_bytes(tiny_caps(k).n, tiny_caps(k).a, tiny_caps(k).h, tiny_caps(k).l,
+                        kTinyAlign);
+}
+__host__ __device__ constexpr int tiny_waves(int k) { return k == 1 ? 3 : 2; }  // per SIMD
 // (A/B on config 4: with the ~3 KB rhs copied into LDS as well a string took 143 / 288 us
 // instead of 178 / 338 us, but 6 workgroups fit per CU instead of 8: no faster overall)
 
-template <int WG, bool kGraph, bool kTiny = false>
-__global__ void __launch_bounds__(WG, WG == 64 ? (kTiny ? kTinyWaves : FSTAMD_BFS_WAVES64) : 1)
+template <int WG, bool kGraph, int kTiny = 0>
+__global__ void __launch_bounds__(WG, WG == 64 ? (kTiny ? tiny_waves(kTiny) : FSTAMD_BFS_WAVES64) : 1)
 eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, const uint32_t* num_items_dev,
                  uint32_t num_items_host, BfsWs ws, BatchOutDev out) {
-  static_assert(!kTiny || (!kGraph && WG == 64), "the tiny tier is the chain batch's wave tier");
+  static_assert(kTiny == 0 || (!kGraph && WG == 64), "the tiny tiers are the chain batch's");
   __shared__ BfsShared SH;
   const uint32_t tid = threadIdx.x;
   BfsTables T;
   [[maybe_unused]] uint32_t* tiny_lab = nullptr;
-  if constexpr (kTiny) {
-    __shared__ __attribute__((aligned(16))) uint8_t tiny_slab[kTinyBytes];
-    __shared__ uint32_t tiny_labels[kTinyL];
-    T = bfs_carve(tiny_slab, kTinyN, kTinyA, kTinyH, kTinyL, kTinyAlign);
+  constexpr TinyCaps kTC = tiny_caps(kTiny);
+  if constexpr (kTiny != 0) {
+    __shared__ __attribute__((aligned(16))) uint8_t tiny_slab[tiny_bytes(kTiny)];
+    __shared__ uint32_t tiny_labels[kTC.lab];
+    T = bfs_carve(tiny_slab, kTC.n, kTC.a, kTC.h, kTC.l, kTinyAlign);
     tiny_lab = tiny_labels;
   } else {
     T = bfs_carve(ws.slab + (size_t)blockIdx.x * ws.stride, ws.ncap, ws.acap, ws.hcap, ws.lcap);
@@ -999,8 +1013,8 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       const uint64_t off = in.offsets[si];
       lhs.labels = in.labels + off;
       lhs.L = (uint32_t)(in.offsets[si + 1] - off);
-      if constexpr (kTiny) {  // the labels in LDS; a chain this long needs more levels anyway
-        if (lhs.L + 2 > kTinyL) {
+      if constexpr (kTiny != 0) {  // the labels in LDS; a chain this long needs more levels
+        if (lhs.L + 2 > kTC.lab) {
           if (tid == 0) write_status(out, si, kPathOverflow, 0, 0);
           continue;
         }
