@@ -626,6 +626,13 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   const bool force_rounds = le && std::strcmp(le, "rounds") == 0;
   const bool force_replay = le && std::strcmp(le, "replay") == 0;
   const bool force_dense = le && std::strcmp(le, "dense") == 0;
+  // The hashed replay (below) starts small lattices with its tables in LDS, then HBM for
+  // what outgrows them; FSTAMD_LAZY_TINY=0 skips that.  (As the engine for config 4's small
+  // epsilon lattices it measured level with the dense replay, 15.8 vs 15.0 ms per two-stage
+  // call: the pop's rhs reads and shuffles bind, not the tables.)
+  const char* lte = std::getenv("FSTAMD_LAZY_TINY");
+  const bool tiny_ok = !(lte && std::strcmp(lte, "0") == 0) &&
+                       (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
   const bool exact_ok = rhs.nonneg && rhs.finite && !force_replay;
   const bool use_dense = exact_ok && !force_rounds && (force_dense || rhs.has_eps);
   const bool use_rounds = exact_ok && !use_dense;
@@ -745,7 +752,30 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     HIP_TRY(hipEventRecord(ev0_, stream));
   }
   uint32_t grid0 = 0;
-  HIP_TRY(launch_lazy(want, nullptr, in.num_strings, counter, &grid0));
+  const bool tiny_first = tiny_ok;
+  if (tiny_first) {  // LDS tables (kernels/lazy_wave.hpp kLzTiny*): stamps from 1 per launch
+    static const int occ = [] {
+      int o = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &o, (const void*)lazy_wave_kernel<false, true>, 64, 0) != hipSuccess)
+        o = 1;
+      return std::max(o, 1);
+    }();
+    LazyWs ws{};
+    ws.hcap = kLzTinyH;
+    ws.ncap = kLzTinyN;
+    ws.qcap = kLzTinyQ;
+    ws.gcap = 0;
+    ws.stamp_base = 0;
+    ws.max_pops = kLzTinyQ + 1;
+    ws.wd_ticks = watchdog_ticks();
+    grid0 = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(in.num_strings, 1u));
+    lazy_wave_kernel<false, true><<<grid0, 64, 0, stream>>>(rhs.view, in, none, n, counter,
+                                                            nullptr, in.num_strings, ws, out);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(launch_lazy(want, nullptr, in.num_strings, counter, &grid0));
+  }
   if (stats) stats->grid = grid0;
   // retry tiers for OVERFLOW strings (host reads the count: this path is for outliers)
   uint32_t* list = (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4);
@@ -760,7 +790,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     HIP_TRY(hipMemcpyAsync(&cnt, ctr + 1, 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     if (cnt == 0) break;
-    want *= 8;
+    if (!(tiny_first && tier == 1)) want *= 8;  // after the tiny launch: HBM at `want` first
     uint32_t g = 0;
     if (launch_lazy(want, list, cnt, ctr, &g) != hipSuccess) break;  // stays OVERFLOW
     if (stats) stats->launches += 2;

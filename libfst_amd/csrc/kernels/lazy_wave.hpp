@@ -272,22 +272,57 @@ struct LazyLds {
 // 18.4 ms per call, 6 and 8 with spills 20.4 ms)
 #define FSTAMD_REPLAY_WAVES 4
 #endif
-template <bool kGraph>
-__global__ void __launch_bounds__(64, FSTAMD_REPLAY_WAVES)
+// The tiny replay (kTiny): small lattices (config 4's tagger / verbalizer: 43 / 72 tuples
+// per utterance on average) keep the wave's hash, node arrays and heap in LDS instead of
+// HBM slabs, ~15 KB, 10 waves per CU; strings that outgrow it report OVERFLOW and are rerun
+// in HBM.  The host sets ws.{hcap, ncap, qcap, max_pops} to these caps for that launch.
+constexpr uint32_t kLzTinyN = 128, kLzTinyH = 256, kLzTinyQ = 384;
+
+template <bool kGraph, bool kTiny = false>
+__global__ void __launch_bounds__(64, kTiny ? 3 : FSTAMD_REPLAY_WAVES)
 lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, uint32_t num_items, LazyWs ws,
                  BatchOutDev out) {
+  static_assert(!kTiny || !kGraph, "the tiny replay is the chain batch's");
   __shared__ LazyLds S;
   const uint32_t lane = lane_id();
   const size_t w = blockIdx.x;
-  uint4* hslot = ws.hslot + w * ws.hcap;
-  unsigned long long* nkey = ws.nkey + w * ws.ncap;
-  double* ndist = ws.ndist + w * ws.ncap;
-  uint4* nback = ws.nback + w * ws.ncap;
-  double* nbw = ws.nbw + w * ws.ncap;
-  double* qd = ws.qd + w * ws.qcap;
-  uint32_t* qid = ws.qid + w * ws.qcap;
-  uint4* tbl = ws.gscratch + w * ws.gcap;
+  uint4* hslot;
+  unsigned long long* nkey;
+  double* ndist;
+  uint4* nback;
+  double* nbw;
+  double* qd;
+  uint32_t* qid;
+  uint4* tbl = nullptr;
+  if constexpr (kTiny) {
+    __shared__ uint4 t_hslot[kLzTinyH];
+    __shared__ unsigned long long t_nkey[kLzTinyN];
+    __shared__ double t_ndist[kLzTinyN];
+    __shared__ uint4 t_nback[kLzTinyN];
+    __shared__ double t_nbw[kLzTinyN];
+    __shared__ double t_qd[kLzTinyQ];
+    __shared__ uint32_t t_qid[kLzTinyQ];
+    hslot = t_hslot;
+    nkey = t_nkey;
+    ndist = t_ndist;
+    nback = t_nback;
+    nbw = t_nbw;
+    qd = t_qd;
+    qid = t_qid;
+    // stamps start at ws.stamp_base + 1 > 0: a zeroed table is empty for every string
+    for (uint32_t i = lane; i < kLzTinyH; i += 64) t_hslot[i] = make_uint4(0u, 0u, 0u, 0u);
+    wave_fence();
+  } else {
+    hslot = ws.hslot + w * ws.hcap;
+    nkey = ws.nkey + w * ws.ncap;
+    ndist = ws.ndist + w * ws.ncap;
+    nback = ws.nback + w * ws.ncap;
+    nbw = ws.nbw + w * ws.ncap;
+    qd = ws.qd + w * ws.qcap;
+    qid = ws.qid + w * ws.qcap;
+    tbl = ws.gscratch + w * ws.gcap;
+  }
   const uint32_t hmask = ws.hcap - 1;
   // per-string watchdog: both are reset when a string starts, so every string gets the
   // full limit however long the launch has been running

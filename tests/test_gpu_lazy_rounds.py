@@ -19,10 +19,15 @@ from test_gpu_parity import LAZY, check, csr, load_blob, random_rhs
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["rounds", "general", "replay", "dense"])
+@pytest.fixture(params=["rounds", "general", "replay", "replay_hbm", "dense"])
 def engine(request, monkeypatch):
     monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
     monkeypatch.delenv("FSTAMD_LAZY_LAYERED", raising=False)
+    monkeypatch.delenv("FSTAMD_LAZY_TINY", raising=False)
+    if request.param == "replay_hbm":  # the hashed replay without its LDS first launch
+        monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
+        monkeypatch.setenv("FSTAMD_LAZY_TINY", "0")
+        return "replay"
     if request.param in ("replay", "dense"):
         monkeypatch.setenv("FSTAMD_LAZY_ENGINE", request.param)
         return request.param
