@@ -201,3 +201,47 @@ def test_log_weight_blobs_load_through_batch_loaders(tmp_path):
     assert fz.weight_type == 1
     for s in range(fz.num_states):
         assert fz.arcs(s) == g.arcs(s)
+
+
+def test_batch_result_views_free_once(monkeypatch):
+    # the Python mirror's BatchResult arrays view the library's result buffers without a
+    # copy, and fst_batch_result_free runs exactly once, after the last view is gone
+    import ctypes as C
+    import gc
+    import libfst_amd.fst as FF
+
+    freed = []
+
+    class FakeLib:
+        def fst_batch_result_free(self, ref):
+            freed.append(1)
+
+    monkeypatch.setattr(FF, "lib", lambda: FakeLib())
+    status = np.array([0, 1, 0], np.int32)
+    offs = np.array([0, 2, 2, 3], np.uint64)
+    il = np.array([5, 6, 7], np.uint32)
+    ol = np.array([8, 9, 10], np.uint32)
+    w = np.array([0.5, 1.0, 2.0])
+    fin = np.array([0.0, np.inf, 1.5])
+    res = FF.FstBatchResult()
+    res.num_strings = 3
+    res.total_arcs = 3
+    res.status = status.ctypes.data_as(C.POINTER(C.c_int32))
+    res.path_offsets = offs.ctypes.data_as(C.POINTER(C.c_uint64))
+    res.ilabels = il.ctypes.data_as(C.POINTER(C.c_uint32))
+    res.olabels = ol.ctypes.data_as(C.POINTER(C.c_uint32))
+    res.weights = w.ctypes.data_as(C.POINTER(C.c_double))
+    res.final_weights = fin.ctypes.data_as(C.POINTER(C.c_double))
+    out = FF._take_result(res, 3)
+    assert np.array_equal(out.status, status) and np.array_equal(out.offsets, offs)
+    assert np.array_equal(out.ilabels, il) and np.array_equal(out.olabels, ol)
+    assert np.array_equal(out.weights, w) and np.array_equal(out.finals, fin)
+    il[0] = 42  # a view, not a copy
+    assert out.ilabels[0] == 42
+    keep = out.weights
+    del out
+    gc.collect()
+    assert freed == []  # one view still lives
+    del keep
+    gc.collect()
+    assert freed == [1]
