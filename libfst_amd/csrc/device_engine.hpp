@@ -14,6 +14,7 @@
 
 #include <cstdint>
 #include <mutex>
+#include <new>
 #include <vector>
 
 #include "fst_core.hpp"
@@ -140,11 +141,35 @@ struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
 };
 
 // Lattice of one fst_compose_frozen call, downloaded from the device (CSR by source id).
+// Pooled pinned host memory (c_api.cpp): D2H / H2D of it is one DMA, without the
+// runtime's staging copies.
+void* pin_host_alloc(size_t bytes);
+void pin_host_release(void* p);
+template <class T>
+struct PinnedAllocator {
+  using value_type = T;
+  PinnedAllocator() = default;
+  template <class U>
+  PinnedAllocator(const PinnedAllocator<U>&) {}
+  T* allocate(size_t n) {
+    void* p = pin_host_alloc(n * sizeof(T));
+    if (!p) throw std::bad_alloc();
+    return (T*)p;
+  }
+  void deallocate(T* p, size_t) { pin_host_release(p); }
+  template <class U>
+  bool operator==(const PinnedAllocator<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const PinnedAllocator<U>&) const { return false; }
+};
+template <class T>
+using PinnedVec = std::vector<T, PinnedAllocator<T>>;
+
 struct HostLattice {
   int32_t status = 0;  // PathStatus of the compose (kPathOk or kPathOverflow/kPathInternal)
   uint32_t n_nodes = 0, n_arcs = 0;
-  std::vector<uint32_t> aoff, anext, ail, aol;
-  std::vector<double> aw, nfin;
+  PinnedVec<uint32_t> aoff, anext, ail, aol;  // downloaded from the device (config 1: 10 M arcs)
+  PinnedVec<double> aw, nfin;
 };
 
 struct LaunchStats {
