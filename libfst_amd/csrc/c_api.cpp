@@ -253,13 +253,13 @@ void pin_pool_clear() {
   P.held = 0;
 }
 
-struct HostPaths {
-  std::vector<int32_t> status;
-  std::vector<uint32_t> len;
-  std::vector<uint64_t> off;
-  std::vector<double> fin;
-  std::vector<uint32_t> il, ol;
-  std::vector<double> w;
+struct HostPaths {  // pinned: each array is one DMA (single calls download all of them)
+  PinnedVec<int32_t> status;
+  PinnedVec<uint32_t> len;
+  PinnedVec<uint64_t> off;
+  PinnedVec<double> fin;
+  PinnedVec<uint32_t> il, ol;
+  PinnedVec<double> w;
 };
 
 // Device outputs for `num` strings with `arc_cap` arena slots.
