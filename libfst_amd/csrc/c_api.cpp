@@ -294,18 +294,17 @@ struct DevOut {
     h->il.resize(used);
     h->ol.resize(used);
     h->w.resize(used);
-    if (num &&
-        (hipMemcpy(h->status.data(), status.p, num * 4ull, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(h->len.data(), len.p, num * 4ull, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(h->off.data(), off.p, num * 8ull, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(h->fin.data(), fin.p, num * 8ull, hipMemcpyDeviceToHost) != hipSuccess))
+    // HostPaths is pinned: the copies run asynchronously, one synchronisation for all
+    const auto d2h = [](void* dst, const void* src, size_t b) {
+      return hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, nullptr) == hipSuccess;
+    };
+    if (num && !(d2h(h->status.data(), status.p, num * 4ull) && d2h(h->len.data(), len.p, num * 4ull) &&
+                 d2h(h->off.data(), off.p, num * 8ull) && d2h(h->fin.data(), fin.p, num * 8ull)))
       return false;
-    if (used &&
-        (hipMemcpy(h->il.data(), il.p, used * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(h->ol.data(), ol.p, used * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(h->w.data(), w.p, used * 8, hipMemcpyDeviceToHost) != hipSuccess))
+    if (used && !(d2h(h->il.data(), il.p, used * 4) && d2h(h->ol.data(), ol.p, used * 4) &&
+                  d2h(h->w.data(), w.p, used * 8)))
       return false;
-    return true;
+    return hipStreamSynchronize(nullptr) == hipSuccess;
   }
 };
 
