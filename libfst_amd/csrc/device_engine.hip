@@ -962,8 +962,15 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
   // dense arrays already held count as free for them) less a 24 GB reserve, 90 % of it;
   // 128 GB when the runtime cannot say.  Arrays above 128 GB are released after the call
   // so that later calls of other engines find their memory.  FSTAMD_DENSE_BUDGET_GB sets it.
+  // (the runtime is asked only when the plan could need more than 16 GB: small calls skip
+  // the query)
   uint64_t budget = 128ull << 30;
-  {
+  bool budget_known = false;
+  if (const char* be = std::getenv("FSTAMD_DENSE_BUDGET_GB")) {
+    budget = (uint64_t)std::max(1, std::atoi(be)) << 30;
+    budget_known = true;
+  }
+  auto query_budget = [&] {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
       uint64_t avail = fr;
@@ -971,9 +978,8 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
       const uint64_t reserve = 24ull << 30;
       budget = avail > 2 * reserve ? (avail - reserve) / 10 * 9 : avail / 2;
     }
-    if (const char* be = std::getenv("FSTAMD_DENSE_BUDGET_GB"))
-      budget = (uint64_t)std::max(1, std::atoi(be)) << 30;
-  }
+    budget_known = true;
+  };
   const uint32_t max_waves = (uint32_t)num_cus_ * 16;
   const char* ge = std::getenv("FSTAMD_DENSE_GRID");  // debug: fewer waves
   auto make_plan = [&](uint32_t max_len, uint32_t count, Plan& p) -> bool {
@@ -990,6 +996,9 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     if (p.lds > kLdMaxDynLds) return false;
     p.fcap = (uint32_t)std::max<uint64_t>(4096, p.dn / 4);
     const uint64_t per_wave = p.dn * (16 + 4 + 4) + (uint64_t)p.nleaf * 8 + (uint64_t)p.fcap * 16;
+    if (!budget_known &&
+        std::min<uint64_t>(max_waves, count) * per_wave > (16ull << 30))
+      query_budget();
     p.grid = (uint32_t)std::min<uint64_t>(
         {(uint64_t)max_waves, (uint64_t)count, std::max<uint64_t>(1, budget / per_wave)});
     if (ge) p.grid = std::min<uint32_t>(p.grid, (uint32_t)std::max(1, std::atoi(ge)));
