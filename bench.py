@@ -30,6 +30,11 @@ from libfst_amd import dist as D  # noqa: E402
 from libfst_amd import fst as FF  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs, each SIMD busy with VALU at most every cycle of the
+# 2.4 GHz max clock (MI355X_MICROARCH.md: 4 SIMDs per CU, max clock 2400 MHz)
+SIMDS = 256 * 4
+CLOCK_GHZ = 2.4
+VALU_PEAK_GCYC = SIMDS * CLOCK_GHZ   # G SIMD-cycles/s
 # Measured HBM traffic of the metric kernel: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 # over this same command (scripts/profile_bench.sh), reduced by scripts/pmc_summary.py.
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -57,9 +62,10 @@ def measured_traffic(args, sem):
     return t["traffic_per_string"] * args.batch, t.get("source", TRAFFIC_FILE)
 
 
-def issue_profile(sem):
-    """VALU issue figures of the eager metric kernel from the committed SQ summary."""
-    if sem != F.FST_SEM_EAGER:
+def issue_profile(args, sem):
+    """SQ instruction mix of the eager metric kernel (committed summary of rocprofv3 --pmc
+    SQ_* passes over this command at 65,536 strings), or None for another workload."""
+    if sem != F.FST_SEM_EAGER or (args.len, args.transducer_len, args.branches) != (64, 4096, 12):
         return None
     try:
         t = json.load(open(ISSUE_FILE))
@@ -67,13 +73,56 @@ def issue_profile(sem):
         return None
     if t.get("kernel") != EAGER_KERNEL:
         return None
-    ps, wc = t["per_string"], t["of_wave_cycles"]
-    return {"bound": "valu-issue",
-            "valu_insts_per_string": ps.get("SQ_INSTS_VALU"),
-            "salu_insts_per_string": ps.get("SQ_INSTS_SALU"),
-            "lds_insts_per_string": ps.get("SQ_INSTS_LDS"),
-            "valu_active_per_wave": wc.get("SQ_ACTIVE_INST_VALU"),
-            "source": t.get("source", ISSUE_FILE)}
+    return t
+
+
+def roofline_block(args, sem, avg_k_ms, balg, work, lengths, plen, traffic, traffic_src):
+    """The roofline of the dominant kernel against the resource that binds it.
+
+    The metric kernel is bound by VALU issue (SQ counters: VALU busy ~2/3 of SIMD cycles,
+    HBM ~1/5 of peak), so `achieved` = VALU-busy SIMD cycles per second: the committed SQ
+    profile's SQ_ACTIVE_INST_VALU per string (quad-cycles, x4) x the strings of this launch
+    / the kernel time measured live (HIP events on the launch stream); `peak` = 1024 SIMDs x
+    2.4 GHz.  HBM (PMC-measured bytes / kernel time) and the SURVEY 8(d) logical bytes
+    (B_alg: L2/LDS-served, so above the HBM peak) are reported beside it, each with its own
+    fraction."""
+    ks = avg_k_ms * 1e-3
+    n = args.batch
+    hbm = None
+    if traffic:
+        gbs = traffic / ks / 1e9
+        hbm = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+               "bytes_per_string": traffic / n, "source": traffic_src}
+    logical = balg / ks / 1e9
+    b_alg = {"achieved": logical, "unit": "GB/s", "bytes_per_string": balg / n,
+             "frac_vs_hbm_peak": logical / HBM_PEAK_GBS, "frac_vs_l2_peak": logical / L2_PEAK_GBS,
+             "note": "SURVEY 8(d) B_alg = 24 R + 16 X + 4 L + 16 P per string (exact, from the "
+                     "kernel's work counters); these reads hit the L2-resident rhs mirror and "
+                     "LDS, not HBM, so they are priced against L2 as well"}
+    sq = issue_profile(args, sem)
+    blk = {"kernel": EAGER_KERNEL if sem else LAZY_KERNEL, "kernel_ms": avg_k_ms,
+           "traffic": traffic, "hbm": hbm, "b_alg": b_alg,
+           "relaxations_per_s": float(work[1::2].astype(np.int64).sum()) / ks,
+           "compulsory_bytes_per_string": float((4 * lengths + 16 * plen + 24).sum()) / n}
+    if sq is not None:
+        ps = sq["per_string"]
+        busy_cyc = 4.0 * ps["SQ_ACTIVE_INST_VALU"]          # quad-cycles -> cycles
+        ach = busy_cyc * n / ks / 1e9
+        blk.update({"bound": "valu", "achieved": ach, "peak": VALU_PEAK_GCYC,
+                    "unit": "G SIMD-cycles/s (VALU busy)", "frac": ach / VALU_PEAK_GCYC,
+                    "valu_insts_per_string": ps.get("SQ_INSTS_VALU"),
+                    "valu_busy_cycles_per_string": busy_cyc,
+                    "salu_insts_per_string": ps.get("SQ_INSTS_SALU"),
+                    "lds_insts_per_string": ps.get("SQ_INSTS_LDS"),
+                    "issue_source": sq.get("source", ISSUE_FILE)})
+    elif hbm is not None:
+        blk.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": hbm["frac"]})
+    else:  # no counters for this workload: the logical bytes against HBM (may exceed 1)
+        blk.update({"bound": "hbm", "achieved": logical, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": logical / HBM_PEAK_GBS,
+                    "note": "no PMC/SQ profile for this workload: B_alg logical bytes"})
+    return blk
 
 
 def parse():
@@ -86,13 +135,15 @@ def parse():
     p.add_argument("--transducer-len", type=int, default=4096)
     p.add_argument("--branches", type=int, default=12)
     p.add_argument("--semantics", choices=["eager", "lazy"], default="eager")
-    p.add_argument("--varied", action="store_true",
-                   help="also time a varied batch (lengths 1..len, 10%% dead strings)")
+    p.add_argument("--no-varied", dest="varied", action="store_false",
+                   help="skip the varied batch (lengths 1..len, 10%% dead strings)")
+    p.add_argument("--no-e2e", dest="e2e", action="store_false",
+                   help="skip the end-to-end host-API rate (H2D + kernels + D2H)")
     p.add_argument("--lazy-batch", type=int, default=-1,
                    help="also time the lazy engine on this many metric strings "
                         "(-1 = the eager batch size, 0 = off)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = nproc (os.cpu_count())")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
 
@@ -147,7 +198,7 @@ class DeviceBatch:
         return F.last_launch_stats()
 
 
-def check_sample(batch, blob_bytes, sem, n=256):
+def check_sample(batch, blob_bytes, sem, n=256, threads=1):
     """Bit-compares the first n strings of the last run with the oracle (compose.zig +
     shortest-path.zig, or compose-shortest-path.zig): status, path labels, arc weights and
     final weight, f64 bit patterns.  The oracle is the checker here, never the thing timed."""
@@ -157,7 +208,15 @@ def check_sample(batch, blob_bytes, sem, n=256):
     n = min(n, batch.num)
     offs = batch.offsets[: n + 1].cpu().numpy().astype(np.uint64)
     labels = batch.labels[: int(offs[-1])].cpu().numpy().astype(np.uint32)
-    ref = O.batch_run(blob_bytes, labels, offs, 1 if sem == F.FST_SEM_EAGER else 0, 1)
+    ref = O.batch_run(blob_bytes, labels, offs, 1 if sem == F.FST_SEM_EAGER else 0, 1, threads)
+    return compare_with_ref(batch, ref, n)
+
+
+def compare_with_ref(batch, ref, n):
+    """Asserts that the first n strings of a DeviceBatch equal an oracle BatchResult."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi as O  # checker only
+
     status = batch.status[:n].cpu().numpy()
     exp = np.where(ref.empty == 1, F.FST_PATH_EMPTY, F.FST_PATH_OK)
     assert np.all(ref.status == O.OR_OK) and np.array_equal(status, exp), "status mismatch"
@@ -208,11 +267,22 @@ def timed(batch, rhs, sem, dev_index, steps, warmup, world):
     return el, kms, st
 
 
+def cgroup_cpu_limit():
+    """CPUs the cgroup quota allows (cpu.max), or None when unlimited / unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, blob_bytes, sem, seconds=None):
+    """The CPU port (oracle/fst_oracle.c -O3, the reference's algorithm) on nproc host
+    threads, each composing its share of a bounded sample of the same strings."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ffi as O  # checker / CPU baseline only
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads = args.cpu_threads or (os.cpu_count() or 1)
     L = args.len
 
     def run(n, th):
@@ -224,14 +294,43 @@ def cpu_baseline(args, blob_bytes, sem, seconds=None):
     probe = 64
     s = run(probe, 1)
     single = probe / s
+    # all threads on a small sample first: a cgroup quota below nproc would otherwise make
+    # the main run many times longer than its budget
+    n0 = threads * 4
+    agg0 = n0 / run(n0, threads)
     budget = args.cpu_seconds if seconds is None else seconds
-    n = int(max(threads * 8, min(2_000_000, single * threads * budget * 0.8)))
+    n = int(max(n0, min(4_000_000, agg0 * budget)))
     s = run(n, threads)
     return {"value": n / s, "unit": "strings/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cgroup_cpu_limit": cgroup_cpu_limit(),
             "single_thread_value": single,
             "sample": f"{n} strings (1^{L} vs ambiguous T={args.transducer_len} B={args.branches}, "
                       f"{'eager compose+shortestPath' if sem else 'lazy composeShortestPath'}) "
-                      f"on {threads} host threads, oracle/fst_oracle.c -O3"}
+                      f"on {threads} host threads (= nproc), oracle/fst_oracle.c -O3, {s:.1f} s"}
+
+
+def end_to_end(args, rhs, sem, dev_index, steps=3, warmup=1):
+    """The host batch entry fst_compose_frozen_shortest_path_batch on the metric batch: host
+    labels in, H2D, kernels, device CSR compaction, D2H into pooled pinned host arrays,
+    results out (SURVEY 8(d) wall time).  Per-GPU rate of one process."""
+    L, B = args.len, args.batch
+    labels = np.ones(B * L, np.uint32)
+    offsets = np.arange(B + 1, dtype=np.uint64) * L
+    for _ in range(warmup):
+        r = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, dev_index)
+        del r
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, dev_index)
+        assert r.status[0] == F.FST_PATH_OK and int(r.offsets[-1]) == B * L
+        del r
+    el = time.perf_counter() - t0
+    return {"value": B * steps / el, "unit": "strings/s", "ms_per_call": el / steps * 1e3,
+            "calls": steps, "strings_per_call": B,
+            "bytes_in_per_call": int(labels.nbytes + offsets.nbytes),
+            "note": "fst_compose_frozen_shortest_path_batch: host arrays -> H2D -> kernels -> "
+                    "device CSR compaction -> D2H (pinned) -> result, one GPU"}
 
 
 def main():
@@ -280,11 +379,6 @@ def main():
     value = total_strings / el
     avg_k = float(np.mean(kms))
     balg = b_alg_bytes(work, lengths, plen)   # bytes per launch on this rank
-    achieved = balg / (avg_k * 1e-3) / 1e9
-    # relaxations per second and the compulsory HBM bytes (labels in,
-    # path + status/offset/final out) beside the logical bytes
-    relax_per_s = float(work[1::2].astype(np.int64).sum()) / (avg_k * 1e-3)
-    compulsory = int((4 * lengths + 16 * plen + 24).sum())
 
     extra = {}
     if args.varied:
@@ -307,15 +401,26 @@ def main():
     if args.lazy_batch and sem == F.FST_SEM_EAGER:
         lb = DeviceBatch(np.full(args.lazy_batch, L, np.int64),
                          lambda t: torch.ones(t, dtype=torch.int32), dev)
-        lel, lk, lst = timed(lb, rhs, F.FST_SEM_LAZY, local, 3, 1, world)
+        lel, lk, _ = timed(lb, rhs, F.FST_SEM_LAZY, local, 3, 1, world)
         ls = lb.status.cpu().numpy()
         assert np.all(ls == F.FST_PATH_OK)
         extra["lazy"] = {"value": args.lazy_batch * 3 * world / lel, "kernel_ms": float(np.mean(lk)),
                          "batch": args.lazy_batch,
                          "checked_vs_oracle": check_sample(lb, blob_check, F.FST_SEM_LAZY),
                          "note": "fst_compose_frozen_shortest_path semantics (lazy_pull_kernel, exact vs the oracle)"}
+        del lb
         if rank == 0 and not args.no_cpu and world == 1:  # the CPU port beside it (~3 s)
             extra["lazy"]["cpu_baseline"] = cpu_baseline(args, blob_check, 0, seconds=3.0)
+
+    if args.e2e:
+        del batch
+        torch.cuda.empty_cache()
+        extra["end_to_end"] = end_to_end(args, rhs, sem, local)
+        if world > 1:  # every rank ran its own; report the slowest as the job's rate
+            t = torch.tensor([extra["end_to_end"]["ms_per_call"]], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            extra["end_to_end"]["ms_per_call"] = float(t.item())
+            extra["end_to_end"]["value"] = args.batch * world / (float(t.item()) * 1e-3)
 
     if rank == 0:
         traffic, traffic_src = measured_traffic(args, sem)
@@ -342,27 +447,8 @@ def main():
                        "strings_per_gpu": args.batch,
                        "global_batch": args.batch * world,
                        "parallelism": f"dp{world} (string shards, rhs replicated via RCCL broadcast)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel_ms": avg_k, "b_alg_per_string": balg / args.batch,
-                         "relaxations_per_s": relax_per_s,
-                         "compulsory_bytes_per_string": compulsory / args.batch,
-                         "kernel": EAGER_KERNEL if sem else LAZY_KERNEL,
-                         # measured DRAM bytes / kernel time: what really crosses HBM
-                         "hbm_traffic_gbs": (traffic / (avg_k * 1e-3) / 1e9) if traffic else None,
-                         "hbm_traffic_frac": (traffic / (avg_k * 1e-3) / 1e9 / HBM_PEAK_GBS)
-                         if traffic else None,
-                         "l2_peak": L2_PEAK_GBS,
-                         "l2_frac": achieved / L2_PEAK_GBS,
-                         "issue": issue_profile(sem),
-                         "note": "achieved = SURVEY 8(d) logical bytes (24 B per arc relaxed, 16 B "
-                                 "per tuple expanded, labels, path) / kernel time. Those reads hit "
-                                 "the 0.6 MB L2-resident rhs mirror (and LDS), never HBM, so frac "
-                                 "(vs the 8 TB/s HBM peak) exceeds 1; l2_frac prices them against "
-                                 "the 34.5 TB/s L2. hbm_traffic_* is the PMC-measured DRAM traffic "
-                                 "(back records, labels, paths). The kernel is bound by VALU issue "
-                                 "(issue: SQ counters)"},
+            "roofline": roofline_block(args, sem, avg_k, balg, work, lengths, plen, traffic,
+                                       traffic_src),
             "cpu_baseline": cpu,
             "checked_vs_oracle": checked,
         }

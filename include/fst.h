@@ -74,8 +74,14 @@ double fst_final_weight(FstHandle handle, uint32_t state);                /* :55
 uint32_t fst_get_arcs(FstHandle handle, uint32_t state, FstArc* buf, uint32_t buf_len); /* :566 */
 
 /* --- Binary I/O of the frozen blob: src/c-api.zig:601-610, :625-640 --- */
+/* (the file is read straight into a pinned host block and validated there, so the first
+ * device use uploads it with one DMA) */
 FstHandle fst_load(const char* path);                                     /* :601 */
 FstError fst_save(FstHandle handle, const char* path);                    /* :625 */
+/* --- AT&T text (src/io/text.zig:20-115) as the reference's fst_read_text: the asset path
+ * of an OpenFst grammar (fstprint -> text -> fst_read_text -> fst_freeze); no label shift
+ * (tools/att2lfst adds att2lfst.zig's +1, src/tools/att2lfst.zig:54-60) --- */
+FstMutableHandle fst_read_text(const char* path);                         /* :588 */
 
 /* --- The hot path --- */
 /* Eager lattice compose(a, b) with b pinned: src/c-api.zig:675-742 -> src/ops/compose.zig:29-198 */

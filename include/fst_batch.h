@@ -64,7 +64,9 @@ typedef struct {
 } FstBatchOptions;
 
 /* Host arrays in, host result out (H2D, kernels, D2H).  Returns FST_INVALID_ARG for an
- * invalid handle or malformed offsets; per-string outcomes are in out->status. */
+ * invalid handle or malformed offsets; per-string outcomes are in out->status.  Once the
+ * arguments are checked, *out is zeroed before anything else: on any error return it holds
+ * nothing (a result the caller still owned in that struct must be freed beforehand). */
 FstError fst_compose_frozen_shortest_path_batch(FstHandle b, const uint32_t* labels,
                                                 const uint64_t* offsets, uint32_t num_strings,
                                                 uint32_t n, const FstBatchOptions* opts,
@@ -154,6 +156,14 @@ FstHandle fst_bench_transducer_wt(uint32_t kind, uint32_t transducer_len, uint32
  * the same engines. */
 FstHandle fst_batch_load(const char* path);
 FstHandle fst_batch_load_bytes(const void* bytes, uint64_t len);
+/* OpenFst AT&T text -> frozen FST in one call: readText (src/io/text.zig:20-115; files up
+ * to 256 MiB, src/tools/att2lfst.zig:40-45), then with FST_ATT_SHIFT_BYTE_LABELS every
+ * non-epsilon ilabel / olabel + 1 (att2lfst.zig:54-60: OpenFst byte labels -> libfst's
+ * byte + 1, so the asset matches fst_compile_string input), then fromMutable (Tropical).
+ * tools/att2lfst (libfst_amd/att2lfst) is this plus fst_save. */
+#define FST_ATT_SHIFT_BYTE_LABELS 1u
+FstHandle fst_load_att(const char* path, uint32_t flags);
+
 /* Header weight type of a frozen FST: 0 tropical, 1 log, -1 invalid handle. */
 int32_t fst_weight_type(FstHandle b);
 

@@ -127,7 +127,12 @@ bool gpu_available() {
 // synchronises before the buffer goes back, so a block is never reused while a kernel
 // still runs on it.  Blocks beyond kPoolMax bytes held are freed instead; fst_teardown
 // empties the pool.
-constexpr size_t kPoolMax = 16ull << 30;
+// Blocks above kPoolMaxBlock (multi-GB path arenas) are never cached: they would hold HBM
+// the dense replay sizes its waves from (hipMemGetInfo).  A failed hipMalloc releases the
+// device's cached blocks and retries once, so cached blocks of other size classes can never
+// turn into an FST_OOM.
+constexpr size_t kPoolMax = 8ull << 30;
+constexpr size_t kPoolMaxBlock = 1ull << 30;
 struct BufPool {
   std::mutex mu;
   std::multimap<std::pair<int, size_t>, void*> free;
@@ -137,16 +142,26 @@ BufPool& buf_pool() {
   static BufPool* p = new BufPool;  // never destroyed: DevBufs may outlive static teardown
   return *p;
 }
-void pool_clear() {
+// Frees the cached blocks of device `dev` (every device when dev < 0); the calling
+// thread's current device is restored.
+void pool_release(int dev) {
   BufPool& P = buf_pool();
   std::lock_guard<std::mutex> g(P.mu);
-  for (auto& kv : P.free) {
-    (void)hipSetDevice(kv.first.first);
-    (void)hipFree(kv.second);
+  int cur = 0;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  for (auto it = P.free.begin(); it != P.free.end();) {
+    if (dev >= 0 && it->first.first != dev) {
+      ++it;
+      continue;
+    }
+    (void)hipSetDevice(it->first.first);
+    (void)hipFree(it->second);
+    P.held -= it->first.second;
+    it = P.free.erase(it);
   }
-  P.free.clear();
-  P.held = 0;
+  if (have_cur) (void)hipSetDevice(cur);
 }
+void pool_clear() { pool_release(-1); }
 
 // RAII device buffer (pooled)
 struct DevBuf {
@@ -168,13 +183,16 @@ struct DevBuf {
         return;
       }
     }
+    if (hipMalloc(&p, cls) == hipSuccess) return;
+    p = nullptr;
+    pool_release(dev);  // cached blocks of other classes back to the device, then retry
     if (hipMalloc(&p, cls) != hipSuccess) p = nullptr;
   }
   ~DevBuf() {
     if (!p) return;
     BufPool& P = buf_pool();
     std::lock_guard<std::mutex> g(P.mu);
-    if (P.held + cls <= kPoolMax) {
+    if (cls <= kPoolMaxBlock && P.held + cls <= kPoolMax) {
       P.free.insert({{dev, cls}, p});
       P.held += cls;
     } else {
@@ -585,10 +603,11 @@ FstError download_batch_result(int dev, const DevOut& o, uint32_t num, const int
     DeviceEngine& E = DeviceEngine::get(dev);
     std::lock_guard<std::mutex> lk(E.mutex());
     if (E.compact_paths(o.v, num, fail, (int32_t*)st.p, (uint64_t*)off.p, (uint32_t*)il.p,
-                        (uint32_t*)ol.p, (double*)w.p, (double*)fin.p, &tot, nullptr) != hipSuccess)
+                        (uint32_t*)ol.p, (double*)w.p, (double*)fin.p, used, &tot,
+                        nullptr) != hipSuccess)
       return FST_OOM;
   }
-  if (tot > used) return FST_OOM;  // cannot happen: OK paths are in the arena
+  if (tot > used) return FST_OOM;  // an engine bug (the gather wrote nothing past `used`)
   if (t_prof) t_prof->lap(4);
   out->num_strings = num;
   out->total_arcs = tot;
@@ -679,9 +698,10 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
 
 }  // namespace
 
-namespace fstamd {  // the pinned pool for device_engine.hip (HostLattice)
+namespace fstamd {  // the pools for device_engine.hip (HostLattice, the dense replay's budget)
 void* pin_host_alloc(size_t bytes) { return pin_alloc(bytes); }
 void pin_host_release(void* p) { pin_release(p); }
+void device_pool_release(int dev) { pool_release(dev); }
 }  // namespace fstamd
 
 extern "C" {
@@ -844,23 +864,33 @@ uint32_t fst_get_arcs(FstHandle handle, uint32_t state, FstArc* buf, uint32_t bu
 
 FstHandle fst_load(const char* path) {
   if (!path) return kInvalid;
-  FILE* fp = std::fopen(path, "rb");
-  if (!fp) return kInvalid;
-  std::vector<uint8_t> bytes;
-  if (std::fseek(fp, 0, SEEK_END) == 0) {
-    const long sz = std::ftell(fp);
-    if (sz >= 0) {
-      bytes.resize((size_t)sz);
-      std::rewind(fp);
-      if (sz > 0 && std::fread(bytes.data(), 1, (size_t)sz, fp) != (size_t)sz) bytes.clear();
-    }
-  }
-  std::fclose(fp);
-  if (bytes.size() < sizeof(Header)) return kInvalid;
-  auto f = FrozenFst::from_bytes(bytes.data(), bytes.size(), kWeightTropical, nullptr);
+  auto f = FrozenFst::load_file(path, kWeightTropical, nullptr);  // binary.zig:16-36
   if (!f) return kInvalid;
   std::lock_guard<std::mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
+}
+
+// src/c-api.zig:588-599: the whole file (at most 64 MiB, as readFileAlloc's limit there),
+// parsed by readText; no label shift.
+FstMutableHandle fst_read_text(const char* path) {
+  if (!path) return kInvalid;
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return kInvalid;
+  std::vector<char> data;
+  bool ok = std::fseek(fp, 0, SEEK_END) == 0;
+  const long sz = ok ? std::ftell(fp) : -1;
+  ok = sz >= 0 && sz <= (64l << 20);
+  if (ok) {
+    data.resize((size_t)sz);
+    std::rewind(fp);
+    ok = sz == 0 || std::fread(data.data(), 1, (size_t)sz, fp) == (size_t)sz;
+  }
+  std::fclose(fp);
+  if (!ok) return kInvalid;
+  auto m = std::make_shared<MutableFst>();
+  if (!MutableFst::read_text(data.data(), data.size(), m.get())) return kInvalid;
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_mut.insert(std::move(m));
 }
 
 FstError fst_save(FstHandle handle, const char* path) {
@@ -1370,19 +1400,33 @@ FstHandle fst_batch_load_bytes(const void* bytes, uint64_t len) {
 
 FstHandle fst_batch_load(const char* path) {
   if (!path) return kInvalid;
+  auto f = FrozenFst::load_file(path, FrozenFst::kAnyWeightType, nullptr);
+  if (!f) return kInvalid;
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
+}
+
+FstHandle fst_load_att(const char* path, uint32_t flags) {
+  if (!path || (flags & ~FST_ATT_SHIFT_BYTE_LABELS)) return kInvalid;
   FILE* fp = std::fopen(path, "rb");
   if (!fp) return kInvalid;
-  std::vector<uint8_t> bytes;
-  if (std::fseek(fp, 0, SEEK_END) == 0) {
-    const long sz = std::ftell(fp);
-    if (sz >= 0) {
-      bytes.resize((size_t)sz);
-      std::rewind(fp);
-      if (sz > 0 && std::fread(bytes.data(), 1, (size_t)sz, fp) != (size_t)sz) bytes.clear();
-    }
+  std::vector<char> data;
+  bool ok = std::fseek(fp, 0, SEEK_END) == 0;
+  const long sz = ok ? std::ftell(fp) : -1;
+  ok = sz >= 0 && sz <= (256l << 20);  // att2lfst.zig:40-45 (.limited(256 MiB))
+  if (ok) {
+    data.resize((size_t)sz);
+    std::rewind(fp);
+    ok = sz == 0 || std::fread(data.data(), 1, (size_t)sz, fp) == (size_t)sz;
   }
   std::fclose(fp);
-  return fst_batch_load_bytes(bytes.data(), bytes.size());
+  if (!ok) return kInvalid;
+  MutableFst m;
+  if (!MutableFst::read_text(data.data(), data.size(), &m)) return kInvalid;
+  if (flags & FST_ATT_SHIFT_BYTE_LABELS) m.shift_labels();
+  auto f = FrozenFst::from_mutable(m, kWeightTropical);
+  std::lock_guard<std::mutex> g(g_api_mu);
+  return g_fst.insert(std::move(f));
 }
 
 int32_t fst_weight_type(FstHandle b) {

@@ -971,6 +971,7 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     budget_known = true;
   }
   auto query_budget = [&] {
+    device_pool_release(dev_);  // idle pooled blocks count as free HBM
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
       uint64_t avail = fr;
@@ -1570,14 +1571,18 @@ __global__ void csr_count_kernel(BatchOutDev s, uint32_t num, const int32_t* fai
 }
 
 // One wavefront per string (grid-stride): the lanes copy its arcs, coalesced on both sides.
+// A path that would read past the arena or write past `out_cap` is not copied (an engine
+// bug; the host sees the total exceed the arena and fails the call).
 __global__ void __launch_bounds__(64) csr_gather_kernel(BatchOutDev s, uint32_t num,
                                                         const int32_t* status,
                                                         const uint64_t* offsets, uint32_t* il,
-                                                        uint32_t* ol, double* w) {
+                                                        uint32_t* ol, double* w,
+                                                        uint64_t out_cap) {
   for (uint32_t i = blockIdx.x; i < num; i += gridDim.x) {
     if (status[i] != kPathOk) continue;
     const uint64_t src = s.path_off[i], dst = offsets[i];
     const uint32_t L = s.path_len[i];
+    if (dst + L > out_cap || src + L > s.arc_cap) continue;
     for (uint32_t k = threadIdx.x; k < L; k += 64) {
       il[dst + k] = s.out_il[src + k];
       ol[dst + k] = s.out_ol[src + k];
@@ -1593,8 +1598,8 @@ __global__ void merge_status_kernel(int32_t* fail, const int32_t* st, uint32_t n
 
 hipError_t DeviceEngine::compact_paths(const BatchOutDev& s, uint32_t num, const int32_t* fail,
                                        int32_t* status, uint64_t* offsets, uint32_t* il,
-                                       uint32_t* ol, double* w, double* fin, uint64_t* total,
-                                       hipStream_t stream) {
+                                       uint32_t* ol, double* w, double* fin, uint64_t out_cap,
+                                       uint64_t* total, hipStream_t stream) {
   HIP_TRY(hipSetDevice(dev_));
   uint64_t* counts = (uint64_t*)scratch(kProjCount, ((size_t)num + 1) * 8 + 16);
   if (!counts) return hipErrorOutOfMemory;
@@ -1607,7 +1612,7 @@ hipError_t DeviceEngine::compact_paths(const BatchOutDev& s, uint32_t num, const
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(temp, tbytes, counts, offsets, num + 1, stream));
   if (num) {
     const uint32_t grid = std::min<uint32_t>(num, (uint32_t)num_cus_ * 32);
-    csr_gather_kernel<<<grid, 64, 0, stream>>>(s, num, status, offsets, il, ol, w);
+    csr_gather_kernel<<<grid, 64, 0, stream>>>(s, num, status, offsets, il, ol, w, out_cap);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemcpyAsync(total, offsets + num, 8, hipMemcpyDeviceToHost, stream));

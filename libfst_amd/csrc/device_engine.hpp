@@ -145,6 +145,9 @@ struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
 // runtime's staging copies.
 void* pin_host_alloc(size_t bytes);
 void pin_host_release(void* p);
+// Frees the device block pool's cached blocks of `dev` (c_api.cpp), so that a free-HBM query
+// sees them as free.
+void device_pool_release(int dev);
 template <class T>
 struct PinnedAllocator {
   using value_type = T;
@@ -225,10 +228,12 @@ class DeviceEngine {
   // The batch result in CSR order, on the device: status (with `fail`, when given, taking
   // precedence: a pipeline's first failing stage), path offsets over the OK strings'
   // paths, the arcs gathered from the arena, final weights (+inf unless OK).  il / ol / w
-  // hold at least the arena's used arcs.  Synchronises on `stream`; *total = arcs.
+  // hold out_cap arcs (the arena's used arcs); no path is written past them.  Synchronises
+  // on `stream`; *total = arcs (> out_cap only if an engine broke its arena invariant).
   hipError_t compact_paths(const BatchOutDev& s, uint32_t num, const int32_t* fail,
                            int32_t* status, uint64_t* offsets, uint32_t* il, uint32_t* ol,
-                           double* w, double* fin, uint64_t* total, hipStream_t stream);
+                           double* w, double* fin, uint64_t out_cap, uint64_t* total,
+                           hipStream_t stream);
   // fail[i] = st[i] where fail[i] is still OK (the first failing stage wins).
   hipError_t merge_status(int32_t* fail, const int32_t* st, uint32_t num, hipStream_t stream);
   // fst_shortest_path on an explicit graph; `g` holds the FST itself (CSR, arcs in

@@ -1,11 +1,154 @@
 // host_fst.cpp -- MutableFst helpers and the frozen blob (see host_fst.hpp).
 #include "host_fst.hpp"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cctype>
+#include <cstdlib>
+#include <string>
+#include <thread>
 
 #include "device_engine.hpp"
 
 namespace fstamd {
+
+// ---- AT&T text (src/io/text.zig:20-123) ---------------------------------------------
+
+namespace {
+
+// std.fmt.parseInt(u32, s, 10): optional sign, decimal digits, '_' between digits;
+// out of range (or a negative non-zero) is an error.
+bool parse_u32(const char* b, const char* e, uint32_t* out) {
+  if (b == e) return false;
+  bool neg = false;
+  if (*b == '+' || *b == '-') {
+    neg = *b == '-';
+    ++b;
+  }
+  if (b == e || *b == '_' || e[-1] == '_') return false;
+  uint64_t x = 0;
+  for (const char* c = b; c < e; ++c) {
+    if (*c == '_') continue;
+    if (*c < '0' || *c > '9') return false;
+    x = x * 10 + (uint64_t)(*c - '0');
+    if (x > 0xFFFFFFFFull) return false;
+  }
+  if (neg && x != 0) return false;
+  *out = (uint32_t)x;
+  return true;
+}
+
+// parseWeight (:117-123): "inf" / "Infinity" -> Zero, else std.fmt.parseFloat(f64).
+bool parse_weight(const char* b, const char* e, double* out) {
+  const std::string t(b, e);
+  if (t == "inf" || t == "Infinity") {
+    *out = w_zero();
+    return true;
+  }
+  if (t.empty() || std::isspace((unsigned char)t[0])) return false;
+  errno = 0;
+  char* end = nullptr;
+  const double v = std::strtod(t.c_str(), &end);
+  if (end != t.c_str() + t.size()) return false;
+  *out = v;
+  return true;
+}
+
+}  // namespace
+
+bool MutableFst::read_text(const char* data, size_t len, MutableFst* out) {
+  MutableFst f;
+  bool start_set = false;
+  auto ensure = [&](uint32_t s) {
+    if (f.num_states() <= s) f.add_states((size_t)s + 1 - f.num_states());
+  };
+  const char* p = data;
+  const char* end = data + len;
+  while (p <= end) {
+    const char* nl = (const char*)std::memchr(p, '\n', (size_t)(end - p));
+    const char* le = nl ? nl : end;
+    // trim '\r', ' ', '\t' on both sides
+    const char* b = p;
+    const char* e = le;
+    auto ws = [](char c) { return c == '\r' || c == ' ' || c == '\t'; };
+    while (b < e && ws(*b)) ++b;
+    while (e > b && ws(e[-1])) --e;
+    p = le + 1;
+    if (b == e) {
+      if (!nl) break;
+      continue;
+    }
+    // tokenizeAny(" \t")
+    const char* tb[6];
+    const char* te[6];
+    int nt = 0;
+    for (const char* c = b; c < e && nt < 6;) {
+      while (c < e && (*c == ' ' || *c == '\t')) ++c;
+      if (c == e) break;
+      tb[nt] = c;
+      while (c < e && *c != ' ' && *c != '\t') ++c;
+      te[nt++] = c;
+    }
+    uint32_t src;
+    if (!parse_u32(tb[0], te[0], &src)) return false;
+    ensure(src);
+    if (!start_set) {
+      f.set_start(src);
+      start_set = true;
+    }
+    if (nt == 1) {  // single field: final with One
+      f.set_final(src, w_one());
+    } else {
+      uint32_t dest;
+      if (!parse_u32(tb[1], te[1], &dest)) {  // "state weight"
+        double w;
+        if (!parse_weight(tb[1], te[1], &w) || nt > 2) return false;
+        f.set_final(src, w);
+      } else if (nt == 2) {
+        double w;
+        if (parse_weight(tb[1], te[1], &w)) {
+          f.set_final(src, w);
+        } else {  // "src dest": an epsilon arc
+          ensure(dest);
+          f.add_arc(src, Arc{kEpsilon, kEpsilon, w_one(), dest});
+        }
+      } else {
+        ensure(dest);
+        uint32_t il;
+        if (!parse_u32(tb[2], te[2], &il) || nt > 5) return false;
+        uint32_t ol = il;
+        double w = w_one();
+        if (nt >= 4) {
+          if (!parse_u32(tb[3], te[3], &ol)) {  // the fourth field is the weight
+            ol = il;
+            if (!parse_weight(tb[3], te[3], &w)) return false;
+            f.add_arc(src, Arc{il, ol, w, dest});
+            if (!nl) break;
+            continue;
+          }
+          if (nt == 5 && !parse_weight(tb[4], te[4], &w)) return false;
+        }
+        f.add_arc(src, Arc{il, ol, w, dest});
+      }
+    }
+    if (!nl) break;
+  }
+  *out = std::move(f);
+  return true;
+}
+
+void MutableFst::shift_labels() {
+  for (State& s : states_)
+    for (Arc& a : s.arcs) {
+      if (a.ilabel != kEpsilon) a.ilabel += 1;
+      if (a.olabel != kEpsilon) a.olabel += 1;
+    }
+}
 
 MutableFst MutableFst::compile_string(const uint8_t* in, uint32_t in_len, const uint8_t* out,
                                       uint32_t out_len) {
@@ -54,9 +197,10 @@ std::shared_ptr<FrozenFst> FrozenFst::from_mutable(const MutableFst& m, uint8_t 
   std::shared_ptr<FrozenFst> f(new FrozenFst());
   const uint32_t ns = (uint32_t)m.num_states();
   const uint64_t na = m.total_arcs();
-  f->size_ = sizeof(Header) + (size_t)ns * sizeof(StateEntry) + (size_t)na * sizeof(PackedArc);
-  f->buf_.assign((f->size_ + 7) / 8, 0);
-  uint8_t* b = reinterpret_cast<uint8_t*>(f->buf_.data());
+  const size_t len = sizeof(Header) + (size_t)ns * sizeof(StateEntry) + (size_t)na * sizeof(PackedArc);
+  if (!f->alloc(len)) throw std::bad_alloc();
+  uint8_t* b = f->buf_;
+  std::memset(b, 0, len);  // header and arc padding are zero (byte-identical blobs)
   Header* h = reinterpret_cast<Header*>(b);
   h->magic = kMagic;
   h->version = kVersion;
@@ -128,9 +272,81 @@ std::shared_ptr<FrozenFst> FrozenFst::from_bytes(const uint8_t* bytes, size_t le
   if (err) *err = e;
   if (e != BlobError::kOk) return nullptr;
   std::shared_ptr<FrozenFst> f(new FrozenFst());
-  f->size_ = len;
-  f->buf_.assign((len + 7) / 8, 0);
-  std::memcpy(f->buf_.data(), bytes, len);
+  if (!f->alloc(len)) return nullptr;
+  std::memcpy(f->buf_, bytes, len);
+  f->analyze();
+  return f;
+}
+
+bool FrozenFst::alloc(size_t len) {
+  const size_t cap = (len + 7) & ~(size_t)7;
+  void* p = nullptr;
+  // small blobs (test graphs, toy grammars) stay pageable: pinning costs a syscall and a
+  // page per blob, and their upload is tiny either way
+  if (cap >= (64u << 10) &&
+      hipHostMalloc(&p, cap, hipHostMallocDefault) == hipSuccess && p) {
+    pinned_ = true;
+  } else {
+    (void)hipGetLastError();  // no device: clear the runtime's sticky error
+    p = std::aligned_alloc(8, std::max<size_t>(cap, 8));
+    if (!p) return false;
+    pinned_ = false;
+  }
+  buf_ = (uint8_t*)p;
+  size_ = len;
+  if (cap > len) std::memset(buf_ + len, 0, cap - len);
+  return true;
+}
+
+std::shared_ptr<FrozenFst> FrozenFst::load_file(const char* path, uint8_t expect_wt,
+                                                BlobError* err) {
+  if (err) *err = BlobError::kInvalidFormat;
+  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return nullptr;
+  struct stat st;
+  if (::fstat(fd, &st) != 0 || st.st_size < (off_t)sizeof(Header)) {
+    ::close(fd);
+    return nullptr;
+  }
+  const size_t len = (size_t)st.st_size;
+  (void)::posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  std::shared_ptr<FrozenFst> f(new FrozenFst());
+  if (!f->alloc(len)) {
+    ::close(fd);
+    return nullptr;
+  }
+  // pread straight into the pinned block; files of many MB on several threads (a WeText
+  // tagger is tens of MB, config 3's rhs 21.5 MB)
+  const size_t piece = 16ull << 20;
+  const uint32_t nth = (uint32_t)std::min<size_t>(8, std::max<size_t>(1, len / piece));
+  std::vector<uint8_t> ok(nth, 1);
+  auto rd = [&](uint32_t t) {
+    size_t lo = len * t / nth, hi = len * (t + 1) / nth;
+    while (lo < hi) {
+      const ssize_t r = ::pread(fd, f->buf_ + lo, hi - lo, (off_t)lo);
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) {
+        ok[t] = 0;
+        return;
+      }
+      lo += (size_t)r;
+    }
+  };
+  std::vector<std::thread> th;
+  for (uint32_t t = 1; t < nth; ++t) th.emplace_back(rd, t);
+  rd(0);
+  for (auto& x : th) x.join();
+  ::close(fd);
+  for (uint8_t o : ok)
+    if (!o) return nullptr;
+  uint8_t wt = expect_wt;
+  if (expect_wt == kAnyWeightType) {
+    wt = reinterpret_cast<const Header*>(f->buf_)->weight_type;
+    if (wt != kWeightTropical && wt != kWeightLog) return nullptr;
+  }
+  const BlobError e = validate(f->buf_, len, wt);
+  if (err) *err = e;
+  if (e != BlobError::kOk) return nullptr;
   f->analyze();
   return f;
 }
@@ -194,6 +410,10 @@ void FrozenFst::adopt_device(int dev, DeviceFst* d) {
 FrozenFst::~FrozenFst() {
   for (DeviceFst* d : dev_)
     if (d) DeviceFst::destroy(d);
+  if (buf_) {
+    if (pinned_) (void)hipHostFree(buf_);
+    else std::free(buf_);
+  }
 }
 
 }  // namespace fstamd

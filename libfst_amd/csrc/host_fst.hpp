@@ -50,6 +50,12 @@ class MutableFst {
                                    uint32_t out_len);
   // printStringFromTape, src/string.zig:64-97.  Returns false for "null".
   bool print_string(bool output_tape, std::vector<uint8_t>* bytes) const;
+  // readText, src/io/text.zig:20-115 (OpenFst AT&T text: "src dest il [ol] [w]" arcs,
+  // "state [w]" finals, first source = start).  Returns false for error.InvalidFormat.
+  static bool read_text(const char* data, size_t len, MutableFst* out);
+  // att2lfst's label normalisation (src/tools/att2lfst.zig:54-60): every non-epsilon
+  // ilabel / olabel + 1 (OpenFst byte labels -> libfst's byte + 1 convention).
+  void shift_labels();
 
  private:
   std::vector<State> states_;
@@ -70,10 +76,18 @@ class FrozenFst {
   static std::shared_ptr<FrozenFst> from_bytes(const uint8_t* bytes, size_t len,
                                                uint8_t expect_weight_type, BlobError* err);
   static BlobError validate(const uint8_t* bytes, size_t len, uint8_t expect_weight_type);
+  // readBinary + fromBytes (src/io/binary.zig:16-36, src/fst.zig:227-273) without the
+  // intermediate copy: the file is read straight into the blob's own pinned host block and
+  // validated there, so the device copy is one DMA.  expect_weight_type 0xFF accepts either
+  // semiring (the batch loaders); the reference's fst_load expects Tropical (0).
+  static std::shared_ptr<FrozenFst> load_file(const char* path, uint8_t expect_weight_type,
+                                              BlobError* err);
+  static constexpr uint8_t kAnyWeightType = 0xFF;
 
   ~FrozenFst();
 
-  const uint8_t* bytes() const { return reinterpret_cast<const uint8_t*>(buf_.data()); }
+  const uint8_t* bytes() const { return buf_; }
+  bool pinned() const { return pinned_; }
   size_t size() const { return size_; }
   const Header& header() const { return *reinterpret_cast<const Header*>(bytes()); }
   const StateEntry* states() const {
@@ -105,8 +119,15 @@ class FrozenFst {
 
  private:
   FrozenFst() = default;
+  FrozenFst(const FrozenFst&) = delete;
+  FrozenFst& operator=(const FrozenFst&) = delete;
   void analyze();
-  std::vector<uint64_t> buf_;  // 8-aligned storage
+  // The blob's storage: a page-aligned pinned host block when the HIP runtime grants one
+  // (device uploads are then one DMA, not staged through the runtime's bounce buffers),
+  // 8-aligned malloc otherwise (no GPU).  Zero-filled past size_ to the next 8 bytes.
+  bool alloc(size_t len);
+  uint8_t* buf_ = nullptr;
+  bool pinned_ = false;
   size_t size_ = 0;
   bool has_eps_ = false;
   bool nonneg_ = true;

@@ -104,6 +104,8 @@ SIGNATURES = {
     "fst_batch_load": (_u64, [C.c_char_p]),
     "fst_batch_load_bytes": (_u64, [C.c_void_p, C.c_uint64]),
     "fst_weight_type": (C.c_int32, [_u64]),
+    "fst_read_text": (_u64, [C.c_char_p]),
+    "fst_load_att": (_u64, [C.c_char_p, _u32]),
     "fst_device_project_output": (C.c_int, [C.c_void_p, _u32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(_u32), C.c_void_p]),
     "fst_pipeline_batch": (C.c_int, [C.c_void_p, _u32, C.c_void_p, C.c_void_p, _u32, _u32,
@@ -196,6 +198,32 @@ class MutableFst:
         return (self.start, [self.final_weight(s) for s in range(ns)],
                 [self.arcs(s) for s in range(ns)])
 
+    def to_arrays(self):
+        """(start, offsets u64[ns + 1], arcs, finals f64[ns]) with `arcs` a numpy record
+        array of FstArc {ilabel, olabel, weight, nextstate}: large results (config 1's
+        lattice has 10 M arcs) without Python tuples."""
+        L, ns = lib(), self.num_states
+        cnt = np.fromiter((L.fst_mutable_num_arcs(self.h, s) for s in range(ns)), np.uint64, ns)
+        off = np.zeros(ns + 1, np.uint64)
+        np.cumsum(cnt, out=off[1:])
+        tot = int(off[-1])
+        buf = (FstArc * max(tot, 1))()
+        base, sz, ptr = C.addressof(buf), C.sizeof(FstArc), C.POINTER(FstArc)
+        for s in np.nonzero(cnt)[0]:
+            L.fst_mutable_get_arcs(self.h, int(s), C.cast(base + int(off[s]) * sz, ptr), int(cnt[s]))
+        dt = np.dtype([("il", "<u4"), ("ol", "<u4"), ("w", "<f8"), ("next", "<u4"), ("pad", "<u4")])
+        arcs = np.frombuffer(buf, dtype=dt, count=tot).copy()
+        fin = np.fromiter((L.fst_mutable_final_weight(self.h, s) for s in range(ns)), np.float64, ns)
+        return self.start, off, arcs, fin
+
+    @staticmethod
+    def read_text(path) -> "MutableFst":
+        """fst_read_text: OpenFst AT&T text (src/io/text.zig), labels as written."""
+        h = lib().fst_read_text(os.fsencode(path))
+        if h == FST_INVALID_HANDLE:
+            raise ValueError(f"fst_read_text failed: {path}")
+        return MutableFst(h)
+
     @staticmethod
     def compile_string(data: bytes) -> "MutableFst":
         return MutableFst(lib().fst_compile_string(data, len(data)))
@@ -242,6 +270,14 @@ class Fst:
     def load_any(path) -> "Fst":
         """Tropical or Log blob (fst_batch_load: weight type from the header)."""
         return Fst(lib().fst_batch_load(path.encode()))
+
+    @staticmethod
+    def load_att(path, shift_byte_labels=True) -> "Fst":
+        """fst_load_att: AT&T text -> frozen, with att2lfst's +1 byte-label shift."""
+        h = lib().fst_load_att(os.fsencode(path), 1 if shift_byte_labels else 0)
+        if h == FST_INVALID_HANDLE:
+            raise ValueError(f"fst_load_att failed: {path}")
+        return Fst(h)
 
     @staticmethod
     def from_bytes(blob: bytes) -> "Fst":

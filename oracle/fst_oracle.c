@@ -132,6 +132,18 @@ int or_mfst_get_arc(const or_mfst* m, uint32_t s, uint32_t i, or_arc* out) {
     *out = m->st[s].arcs[i];
     return 0;
 }
+/* Test helper (not in the reference): the whole FST as CSR in state order, arcs in
+ * insertion order; off[num_states + 1], arcs[total_arcs], finals[num_states]. */
+void or_mfst_export(const or_mfst* m, uint64_t* off, or_arc* arcs, double* finals) {
+    uint64_t k = 0;
+    for (uint32_t s = 0; s < m->n; ++s) {
+        off[s] = k;
+        finals[s] = m->st[s].final_w;
+        if (m->st[s].n) memcpy(arcs + k, m->st[s].arcs, (size_t)m->st[s].n * sizeof(or_arc));
+        k += m->st[s].n;
+    }
+    off[m->n] = k;
+}
 
 /* ------------------------------------------------------------------------- */
 /* String helpers, src/string.zig:17-97                                       */

@@ -66,6 +66,8 @@ uint32_t or_mfst_num_arcs(const or_mfst* m, uint32_t s);
 uint64_t or_mfst_total_arcs(const or_mfst* m);
 double or_mfst_final(const or_mfst* m, uint32_t s);
 int or_mfst_get_arc(const or_mfst* m, uint32_t s, uint32_t i, or_arc* out);
+/* test helper: CSR export (off[ns + 1], arcs[total], finals[ns]) */
+void or_mfst_export(const or_mfst* m, uint64_t* off, or_arc* arcs, double* finals);
 
 /* ---- string helpers (src/string.zig:17-97) ---- */
 or_mfst* or_compile_string(const uint8_t* in, uint32_t len);

@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--len", type=int, default=0, help="fixed string length (probes)")
     ap.add_argument("--cpu-n", type=int, default=0,
                     help="also time the CPU port on the first N strings (--cpu-threads)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 16)
     a = ap.parse_args()
     # a launch at T = 65,536 runs for minutes without returning: say so every 30 s (gpurun
     # takes 3 silent minutes for a hang)
@@ -70,25 +70,21 @@ def main():
                 "status": [int(x) for x in status],
                 "tuples_per_string": float(work[0::2].mean()),
                 "relax_per_string": float(work[1::2].mean())}
-        if T <= a.cpu_max_t:
-            L0 = int(lens[0])
-            labels = np.ones(L0, np.uint32)
-            offs = np.array([0, L0], np.uint64)
-            secs, _ = O.batch_time(blob, labels, offs, 0, 1)
-            ref = O.batch_run(blob, labels, offs, 0)
-            got_ok = status[0] == F.FST_PATH_OK
-            line["cpu_s_first_string"] = secs
-            line["cpu_kind"] = "port (oracle/fst_oracle.c -O3), 1 thread, first string"
-            line["parity_first_string"] = bool(got_ok and ref.empty[0] == 0 and int(
-                b.plen[0].item()) == int(ref.offsets[1] - ref.offsets[0]))
-        if a.cpu_n > 0:
-            cl = [int(x) for x in lens[:a.cpu_n]]
+        # every string the CPU port runs is also bit-compared with the GPU's answer (status,
+        # labels, f64 weight bits, final weight): the port is the oracle
+        ncpu = a.cpu_n if a.cpu_n > 0 else (1 if T <= a.cpu_max_t else 0)
+        if ncpu > 0:
+            cl = [int(x) for x in lens[:ncpu]]
             labels = np.ones(sum(cl), np.uint32)
             offs = np.concatenate([[0], np.cumsum(cl)]).astype(np.uint64)
-            secs, _ = O.batch_time(blob, labels, offs, 0, a.cpu_threads)
+            th = a.cpu_threads if a.cpu_n > 0 else 1
+            t0 = time.perf_counter()
+            ref = O.batch_run(blob, labels, offs, 0, 1, th)
+            secs = time.perf_counter() - t0
+            line["bit_exact_vs_oracle"] = bench.compare_with_ref(b, ref, ncpu)
             line["cpu_strings_per_s"] = len(cl) / secs
-            line["cpu_sample"] = (f"first {len(cl)} strings, {a.cpu_threads} threads, "
-                                  "oracle/fst_oracle.c -O3 (port), lazy")
+            line["cpu_sample"] = (f"first {len(cl)} strings, {th} threads, "
+                                  "oracle/fst_oracle.c -O3 (port), lazy; each bit-compared")
         line["lengths"] = f"{len(lens)} strings, L uniform 11..251 (seed 0x5EED), first {list(map(int, lens[:4]))}"
         line["status"] = {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))}
         print(json.dumps(line), flush=True)

@@ -75,6 +75,7 @@ def lib():
         "or_mfst_total_arcs": (u64, [P]),
         "or_mfst_final": (f64, [P, u32]),
         "or_mfst_get_arc": (C.c_int, [P, u32, u32, C.POINTER(OrArc)]),
+        "or_mfst_export": (None, [P, P, P, P]),
         "or_compile_string": (P, [C.c_char_p, u32]),
         "or_compile_string_transducer": (P, [C.c_char_p, u32, C.c_char_p, u32]),
         "or_print_string": (C.c_int32, [P, C.c_int, C.c_char_p, u32]),
@@ -183,6 +184,45 @@ def compose(a: Fst, b, stats=False):
         L.or_mfst_free(mb)
     res = Fst.from_oracle(out.value) if rc == OR_OK else None
     return (rc, res, (st[0], st[1])) if stats else (rc, res)
+
+
+# or_arc / FstArc as a numpy record (24 B: il u32, ol u32, w f64, next u32, pad)
+ARC_DTYPE = np.dtype([("il", "<u4"), ("ol", "<u4"), ("w", "<f8"), ("next", "<u4"),
+                      ("pad", "<u4")])
+
+
+@dataclass
+class Csr:
+    """A whole FST as arrays (large lattices: config 1 has 10 M arcs)."""
+    start: int
+    off: np.ndarray      # u64 [ns + 1]
+    arcs: np.ndarray     # ARC_DTYPE [total]
+    finals: np.ndarray   # f64 [ns]
+
+
+def export_csr(m, free=True) -> Csr:
+    L = lib()
+    ns = L.or_mfst_num_states(m)
+    tot = L.or_mfst_total_arcs(m)
+    off = np.zeros(ns + 1, np.uint64)
+    arcs = np.zeros(max(tot, 1), ARC_DTYPE)
+    fin = np.zeros(max(ns, 1), np.float64)
+    L.or_mfst_export(m, off.ctypes.data, arcs.ctypes.data, fin.ctypes.data)
+    c = Csr(L.or_mfst_start(m), off, arcs[:tot], fin[:ns])
+    if free:
+        L.or_mfst_free(m)
+    return c
+
+
+def compose_csr(a: Fst, blob: bytes):
+    """compose(a, frozen blob) with the result as arrays: (rc, Csr or None)."""
+    L = lib()
+    ma = a.to_oracle()
+    out = C.c_void_p()
+    st = (C.c_uint64 * 2)()
+    rc = L.or_compose(ma, None, blob, C.byref(out), st)
+    L.or_mfst_free(ma)
+    return rc, (export_csr(out.value) if rc == OR_OK else None)
 
 
 def shortest_path(a: Fst, n: int = 1, stats=False):

@@ -261,6 +261,17 @@ def test_single_call_chain_route(rhs_kind):
         blob = O.freeze(O.gen("eps_dense", 128, 6))
     else:
         blob = O.freeze(random_rhs(rng, 12, 60, 4, eps=True))
+    # hand-built compileString-shaped chains with epsilon:epsilon (label 0) arcs: as_chain
+    # takes them, the batch engines hand label-0 strings to the general engine
+    for labels in ([0], [1, 0, 2], [0, 0, 1, 1, 0], [3, 0, 0, 0, 2, 1]):
+        zero = O.Fst()
+        for _ in range(len(labels) + 1):
+            zero.add_state(math.inf)
+        zero.start = 0
+        zero.finals[len(labels)] = 0.0
+        for i, x in enumerate(labels):
+            zero.add_arc(i, x, x, 0.0, i + 1)
+        compare_single(zero, blob)
     for text in (b"", b"\x00", b"\x00" * 37, bytes(rng.integers(0, 4, 19).tolist())):
         lhs = O.compile_string(text)
         compare_single(lhs, blob)
