@@ -143,7 +143,7 @@ def parse():
                    help="also time the lazy engine on this many metric strings "
                         "(-1 = the eager batch size, 0 = off)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = nproc (os.cpu_count())")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = nproc (the affinity mask)")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
 
@@ -267,6 +267,15 @@ def timed(batch, rhs, sem, dev_index, steps, warmup, world):
     return el, kms, st
 
 
+def nproc():
+    """What `nproc` prints: the CPUs this process may run on (its affinity mask).  On the GPU
+    box that is the box's CPU share (16), while os.cpu_count() reports the whole host."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cgroup_cpu_limit():
     """CPUs the cgroup quota allows (cpu.max), or None when unlimited / unknown."""
     try:
@@ -282,7 +291,7 @@ def cpu_baseline(args, blob_bytes, sem, seconds=None):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ffi as O  # checker / CPU baseline only
 
-    threads = args.cpu_threads or (os.cpu_count() or 1)
+    threads = args.cpu_threads or nproc()
     L = args.len
 
     def run(n, th):
@@ -302,7 +311,8 @@ def cpu_baseline(args, blob_bytes, sem, seconds=None):
     n = int(max(n0, min(4_000_000, agg0 * budget)))
     s = run(n, threads)
     return {"value": n / s, "unit": "strings/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(), "cgroup_cpu_limit": cgroup_cpu_limit(),
+            "nproc": nproc(), "os_cpu_count": os.cpu_count(),
+            "cgroup_cpu_limit": cgroup_cpu_limit(),
             "single_thread_value": single,
             "sample": f"{n} strings (1^{L} vs ambiguous T={args.transducer_len} B={args.branches}, "
                       f"{'eager compose+shortestPath' if sem else 'lazy composeShortestPath'}) "

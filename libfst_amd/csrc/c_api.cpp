@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -301,20 +302,22 @@ struct DevOut {
   bool ok() const {
     return status.p && len.p && off.p && fin.p && il.p && ol.p && w.p && cursor.p;
   }
-  bool download(uint32_t num, HostPaths* h) const {
+  bool download(uint32_t num, HostPaths* h, hipStream_t stream) const {
     h->status.resize(num);
     h->len.resize(num);
     h->off.resize(num);
     h->fin.resize(num);
     unsigned long long used = 0;
-    if (hipMemcpy(&used, cursor.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (hipMemcpyAsync(&used, cursor.p, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return false;
     used = std::min<unsigned long long>(used, v.arc_cap);
     h->il.resize(used);
     h->ol.resize(used);
     h->w.resize(used);
     // HostPaths is pinned: the copies run asynchronously, one synchronisation for all
-    const auto d2h = [](void* dst, const void* src, size_t b) {
-      return hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, nullptr) == hipSuccess;
+    const auto d2h = [stream](void* dst, const void* src, size_t b) {
+      return hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, stream) == hipSuccess;
     };
     if (num && !(d2h(h->status.data(), status.p, num * 4ull) && d2h(h->len.data(), len.p, num * 4ull) &&
                  d2h(h->off.data(), off.p, num * 8ull) && d2h(h->fin.data(), fin.p, num * 8ull)))
@@ -322,7 +325,7 @@ struct DevOut {
     if (used && !(d2h(h->il.data(), il.p, used * 4) && d2h(h->ol.data(), ol.p, used * 4) &&
                   d2h(h->w.data(), w.p, used * 8)))
       return false;
-    return hipStreamSynchronize(nullptr) == hipSuccess;
+    return hipStreamSynchronize(stream) == hipSuccess;
   }
 };
 
@@ -438,8 +441,10 @@ struct GraphUpload {
   bool ok = false;
   bool nonneg = true;
   bool nan = false;
-  explicit GraphUpload(const MutableFst& a) : GraphUpload(HostGraph(a)) {}
-  explicit GraphUpload(const HostGraph& h)
+  // Uploads on `stream` (the call's engine stream) and waits for them: the host arrays may
+  // be a temporary.
+  GraphUpload(const MutableFst& a, hipStream_t stream) : GraphUpload(HostGraph(a), stream) {}
+  GraphUpload(const HostGraph& h, hipStream_t stream)
       : off(h.soff.size() * 4ull), il(h.il.size() * 4), ol(h.ol.size() * 4), w(h.w.size() * 8),
         nx(h.nx.size() * 4), fin(h.fin.size() * 8ull) {
     nonneg = h.nonneg;
@@ -447,14 +452,13 @@ struct GraphUpload {
     const uint32_t ns = (uint32_t)h.fin.size();
     const size_t na = h.il.size();
     if (!off.p || !il.p || !ol.p || !w.p || !nx.p || !fin.p) return;
-    bool good = hipMemcpy(off.p, h.soff.data(), (ns + 1) * 4ull, hipMemcpyHostToDevice) == hipSuccess;
-    if (na) {
-      good = good && hipMemcpy(il.p, h.il.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(ol.p, h.ol.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(w.p, h.w.data(), na * 8, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(nx.p, h.nx.data(), na * 4, hipMemcpyHostToDevice) == hipSuccess;
-    }
-    if (ns) good = good && hipMemcpy(fin.p, h.fin.data(), ns * 8ull, hipMemcpyHostToDevice) == hipSuccess;
+    const auto h2d = [stream](void* d, const void* src, size_t b) {
+      return b == 0 || hipMemcpyAsync(d, src, b, hipMemcpyHostToDevice, stream) == hipSuccess;
+    };
+    bool good = h2d(off.p, h.soff.data(), (ns + 1) * 4ull) && h2d(il.p, h.il.data(), na * 4) &&
+                h2d(ol.p, h.ol.data(), na * 4) && h2d(w.p, h.w.data(), na * 8) &&
+                h2d(nx.p, h.nx.data(), na * 4) && h2d(fin.p, h.fin.data(), ns * 8ull);
+    good = hipStreamSynchronize(stream) == hipSuccess && good;
     g.state_off = (const uint32_t*)off.p;
     g.arc_il = (const uint32_t*)il.p;
     g.arc_ol = (const uint32_t*)ol.p;
@@ -506,11 +510,12 @@ int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* r
   if (dev < 0) return -1;
   DeviceFst* D = b.device(dev);
   if (!D) return -1;
-  GraphUpload up(a);
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return -1;
+  const hipStream_t stream = E.stream();
+  GraphUpload up(a, stream);
   if (!up.ok) return -1;
   GraphInput g = up.g;
-  DeviceEngine& E = DeviceEngine::get(dev);
-  std::lock_guard<std::mutex> lk(E.mutex());
   // Grow the tuple capacity on overflow (the reference has no limit but memory).
   for (uint32_t ncap = 1u << 14; ncap <= (1u << 26); ncap <<= 2) {
     g.ncap = ncap;
@@ -518,10 +523,10 @@ int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* r
     DevOut out(1, arc_cap);
     if (!out.ok()) return -1;
     LaunchStats st;
-    if (E.run_graph(*D, g, n, 0, out.v, nullptr, &st) != hipSuccess) return -1;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (E->run_graph(*D, g, n, 0, out.v, stream, &st) != hipSuccess) return -1;
+    if (hipStreamSynchronize(stream) != hipSuccess) return -1;
     HostPaths h;
-    if (!out.download(1, &h)) return -1;
+    if (!out.download(1, &h, stream)) return -1;
     t_last_stats = st;
     if (kernel_ms) *kernel_ms = st.kernel_ms;
     const int32_t s = h.status[0];
@@ -534,8 +539,8 @@ int run_lazy_single(const MutableFst& a, FrozenFst& b, uint32_t n, MutableFst* r
   return -1;
 }
 
-FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_labels,
-                             uint32_t n, int semantics, int dev, HostPaths* h,
+FstError run_chain_batch_dev(DeviceEngine::Lease& E, DeviceFst& D, const ChainInput& in,
+                             uint64_t total_labels, uint32_t n, int semantics, HostPaths* h,
                              std::unique_ptr<DevOut>* keep);
 
 // Chain batch on the GPU from host arrays; fills `h` in input order.
@@ -562,14 +567,15 @@ struct HostProf {
 };
 thread_local HostProf* t_prof = nullptr;
 
-FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
-                              uint32_t num, uint32_t n, int semantics, int dev, HostPaths* h,
-                              std::unique_ptr<DevOut>* keep = nullptr) {
-  if (dev < 0) dev = current_device();
-  if (dev < 0) return FST_INVALID_ARG;
+// The call runs on the engine `E` leases (its stream; E->dev() is the device).
+FstError run_chain_batch_host(DeviceEngine::Lease& E, FrozenFst& b, const uint32_t* labels,
+                              const uint64_t* offsets, uint32_t num, uint32_t n, int semantics,
+                              HostPaths* h, std::unique_ptr<DevOut>* keep = nullptr) {
+  const int dev = E->dev();
   if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
   DeviceFst* D = b.device(dev);
   if (!D) return FST_OOM;
+  const hipStream_t stream = E.stream();
   const uint64_t total = num ? offsets[num] - offsets[0] : 0;
   uint32_t max_len = 0;
   for (uint32_t i = 0; i < num; ++i)
@@ -578,35 +584,37 @@ FstError run_chain_batch_host(FrozenFst& b, const uint32_t* labels, const uint64
   for (uint32_t i = 0; i <= num; ++i) rebased[i] = offsets[i] - offsets[0];
   DevBuf d_lab(total * 4), d_off((num + 1) * 8ull);
   if (!d_lab.p || !d_off.p) return FST_OOM;
-  if (total && hipMemcpy(d_lab.p, labels + offsets[0], total * 4, hipMemcpyHostToDevice) != hipSuccess)
+  // (pageable sources: hipMemcpyAsync stages them before it returns)
+  if (total && hipMemcpyAsync(d_lab.p, labels + offsets[0], total * 4, hipMemcpyHostToDevice,
+                              stream) != hipSuccess)
     return FST_OOM;
-  if (hipMemcpy(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpyAsync(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice, stream) !=
+      hipSuccess)
     return FST_OOM;
   ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
   if (t_prof) t_prof->lap(0);
-  return run_chain_batch_dev(*D, in, total, n, semantics, dev, h, keep);
+  return run_chain_batch_dev(E, *D, in, total, n, semantics, h, keep);
 }
 
 // The batch result straight from the device outputs: compacted to CSR on the device
 // (DeviceEngine::compact_paths), then one copy per array into the caller's result.
 // `fail` (device, optional): a pipeline's first failing stage per string.
-FstError download_batch_result(int dev, const DevOut& o, uint32_t num, const int32_t* fail,
-                               FstBatchResult* out) {
+FstError download_batch_result(DeviceEngine::Lease& E, const DevOut& o, uint32_t num,
+                               const int32_t* fail, FstBatchResult* out) {
+  const hipStream_t stream = E.stream();
   unsigned long long used = 0;
-  if (hipMemcpy(&used, o.cursor.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
+  if (hipMemcpyAsync(&used, o.cursor.p, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return FST_OOM;
   used = std::min<unsigned long long>(used, o.v.arc_cap);
   DevBuf st(num * 4ull), off((num + 1ull) * 8), fin(num * 8ull), il(used * 4), ol(used * 4),
       w(used * 8);
   if (!st.p || !off.p || !fin.p || !il.p || !ol.p || !w.p) return FST_OOM;
   uint64_t tot = 0;
-  {
-    DeviceEngine& E = DeviceEngine::get(dev);
-    std::lock_guard<std::mutex> lk(E.mutex());
-    if (E.compact_paths(o.v, num, fail, (int32_t*)st.p, (uint64_t*)off.p, (uint32_t*)il.p,
-                        (uint32_t*)ol.p, (double*)w.p, (double*)fin.p, used, &tot,
-                        nullptr) != hipSuccess)
-      return FST_OOM;
-  }
+  if (E->compact_paths(o.v, num, fail, (int32_t*)st.p, (uint64_t*)off.p, (uint32_t*)il.p,
+                       (uint32_t*)ol.p, (double*)w.p, (double*)fin.p, used, &tot,
+                       stream) != hipSuccess)
+    return FST_OOM;
   if (tot > used) return FST_OOM;  // an engine bug (the gather wrote nothing past `used`)
   if (t_prof) t_prof->lap(4);
   out->num_strings = num;
@@ -620,13 +628,14 @@ FstError download_batch_result(int dev, const DevOut& o, uint32_t num, const int
   if (!out->status || !out->path_offsets || !out->final_weights || !out->ilabels ||
       !out->olabels || !out->weights)
     return FST_OOM;
-  if ((num && (hipMemcpy(out->status, st.p, num * 4ull, hipMemcpyDeviceToHost) != hipSuccess ||
-               hipMemcpy(out->final_weights, fin.p, num * 8ull, hipMemcpyDeviceToHost) !=
-                   hipSuccess)) ||
-      hipMemcpy(out->path_offsets, off.p, (num + 1ull) * 8, hipMemcpyDeviceToHost) != hipSuccess ||
-      (tot && (hipMemcpy(out->ilabels, il.p, tot * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-               hipMemcpy(out->olabels, ol.p, tot * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-               hipMemcpy(out->weights, w.p, tot * 8, hipMemcpyDeviceToHost) != hipSuccess)))
+  // pinned destinations: asynchronous DMAs on the call's stream, one synchronisation
+  const auto d2h = [stream](void* dst, const void* src, size_t b) {
+    return b == 0 || hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, stream) == hipSuccess;
+  };
+  if (!(d2h(out->status, st.p, num * 4ull) && d2h(out->final_weights, fin.p, num * 8ull) &&
+        d2h(out->path_offsets, off.p, (num + 1ull) * 8) && d2h(out->ilabels, il.p, tot * 4) &&
+        d2h(out->olabels, ol.p, tot * 4) && d2h(out->weights, w.p, tot * 8)) ||
+      hipStreamSynchronize(stream) != hipSuccess)
     return FST_OOM;
   if (t_prof) t_prof->lap(3);
   return FST_OK;
@@ -634,10 +643,11 @@ FstError download_batch_result(int dev, const DevOut& o, uint32_t num, const int
 
 // One batch on device inputs; the path arena grows on OUTPUT_FULL.  With `keep` the
 // device outputs stay alive (pipelines) and `h` receives only the statuses.
-FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_labels,
-                             uint32_t n, int semantics, int dev, HostPaths* h,
+FstError run_chain_batch_dev(DeviceEngine::Lease& E, DeviceFst& D, const ChainInput& in,
+                             uint64_t total_labels, uint32_t n, int semantics, HostPaths* h,
                              std::unique_ptr<DevOut>* keep) {
   const uint32_t num = in.num_strings;
+  const hipStream_t stream = E.stream();
   // Arena: chains without rhs epsilons produce exactly L arcs per path; with them a path
   // also carries the rhs epsilon arcs (a tagger's or verbalizer's multi-symbol outputs),
   // so start at 4 arcs per label rather than run the whole batch twice on OUTPUT_FULL.
@@ -650,8 +660,6 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
       arc_cap = std::max<uint64_t>(std::strtoull(e, nullptr, 10), 1);
       fixed_growth = true;
     }
-  DeviceEngine& E = DeviceEngine::get(dev);
-  std::lock_guard<std::mutex> lk(E.mutex());
   constexpr int kAttempts = 6;
   for (int attempt = 0; attempt < kAttempts; ++attempt) {
     if (t_prof) t_prof->lap(7);
@@ -659,8 +667,8 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
     if (!out->ok()) return FST_OOM;
     if (t_prof) t_prof->lap(1);
     LaunchStats st;
-    hipError_t err = E.run_chain(D, in, n, semantics, out->v, nullptr, &st);
-    if (err == hipSuccess) err = hipDeviceSynchronize();
+    hipError_t err = E->run_chain(D, in, n, semantics, out->v, stream, &st);
+    if (err == hipSuccess) err = hipStreamSynchronize(stream);
     if (t_prof) {
       t_prof->lap(2);
       ++t_prof->runs;
@@ -673,10 +681,11 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
     bool full = false;
     if (keep) {
       h->status.resize(num);
-      if (num && hipMemcpy(h->status.data(), out->v.status, num * 4ull, hipMemcpyDeviceToHost) !=
-                     hipSuccess)
+      if (num && (hipMemcpyAsync(h->status.data(), out->v.status, num * 4ull,
+                                 hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                  hipStreamSynchronize(stream) != hipSuccess))
         return FST_OOM;
-    } else if (!out->download(num, h)) {
+    } else if (!out->download(num, h, stream)) {
       return FST_OOM;
     }
     if (t_prof) t_prof->lap(3);
@@ -690,10 +699,127 @@ FstError run_chain_batch_dev(DeviceFst& D, const ChainInput& in, uint64_t total_
     // every engine reserves a path with atomicAdd on the cursor before it checks the
     // capacity, so the cursor ends at the arcs the whole batch needs: one rerun suffices
     unsigned long long need = 0;
-    if (hipMemcpy(&need, out->v.cursor, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
+    if (hipMemcpyAsync(&need, out->v.cursor, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return FST_OOM;
     arc_cap = fixed_growth ? arc_cap * 4 : std::max<uint64_t>(arc_cap * 2, need + 1024);
   }
   return FST_OOM;  // unreachable: the last attempt returns above
+}
+
+// ---- Coalesced single calls ----------------------------------------------------------
+// fst_compose_frozen_shortest_path on a compileString lhs is one chain string.  Calls that
+// arrive while a batch is in flight are combined (flat combining): the first caller of an
+// idle device becomes a leader, takes every queued call (grouped by rhs and n), runs them
+// as one batch on an engine lease and hands each caller its path; up to kChainLeaders
+// batches run at once (separate engines and streams).  A lone caller runs its own string
+// with no added latency; N concurrent callers share launches and host <-> device trips, so
+// calls/s grows with N (the reference scales calls over threads, README.md:68-82).
+// FSTAMD_COALESCE=0 runs every call on its own.
+struct ChainCall {
+  std::shared_ptr<FrozenFst> rhs;
+  uint32_t n = 1;
+  const std::vector<uint32_t>* labels = nullptr;
+  // result
+  FstError err = FST_OOM;
+  int32_t status = kPathInternal;
+  std::vector<Arc> arcs;
+  double fin = 0;
+  LaunchStats stats;
+  bool done = false;
+};
+
+struct ChainCombiner {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<ChainCall*> q;
+  int leaders = 0;
+};
+constexpr int kChainLeaders = 2;
+constexpr size_t kChainMaxBatch = 1u << 16;
+
+ChainCombiner& chain_combiner(int dev) {
+  static std::mutex mu;
+  static auto* cs = new std::vector<std::unique_ptr<ChainCombiner>>();  // never destroyed
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)cs->size() <= dev) cs->resize(dev + 1);
+  if (!(*cs)[dev]) (*cs)[dev].reset(new ChainCombiner());
+  return *(*cs)[dev];
+}
+
+void run_chain_calls(int dev, std::vector<ChainCall*>& calls) {
+  // group by (rhs, n): one batch per group, strings in arrival order
+  std::stable_sort(calls.begin(), calls.end(), [](const ChainCall* x, const ChainCall* y) {
+    return std::make_pair(x->rhs.get(), x->n) < std::make_pair(y->rhs.get(), y->n);
+  });
+  for (size_t g0 = 0; g0 < calls.size();) {
+    size_t g1 = g0 + 1;
+    while (g1 < calls.size() && calls[g1]->rhs == calls[g0]->rhs && calls[g1]->n == calls[g0]->n)
+      ++g1;
+    const uint32_t num = (uint32_t)(g1 - g0);
+    std::vector<uint64_t> offs(num + 1, 0);
+    for (uint32_t i = 0; i < num; ++i) offs[i + 1] = offs[i] + calls[g0 + i]->labels->size();
+    std::vector<uint32_t> labels(offs[num]);
+    for (uint32_t i = 0; i < num; ++i)
+      std::copy(calls[g0 + i]->labels->begin(), calls[g0 + i]->labels->end(),
+                labels.begin() + offs[i]);
+    HostPaths h;
+    FstError e = FST_INVALID_ARG;
+    {
+      DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+      if (E)
+        e = run_chain_batch_host(E, *calls[g0]->rhs, labels.data(), offs.data(), num,
+                                 calls[g0]->n, FST_SEM_LAZY, &h);
+    }
+    for (uint32_t i = 0; i < num; ++i) {
+      ChainCall* c = calls[g0 + i];
+      c->err = e;
+      c->stats = t_last_stats;
+      if (e != FST_OK) continue;
+      c->status = h.status[i];
+      if (c->status != kPathOk) continue;
+      c->fin = h.fin[i];
+      c->arcs.resize(h.len[i]);
+      for (uint32_t k = 0; k < h.len[i]; ++k) {
+        const uint64_t o = h.off[i] + k;
+        c->arcs[k] = Arc{h.il[o], h.ol[o], h.w[o], k + 1};
+      }
+    }
+    g0 = g1;
+  }
+}
+
+FstError coalesced_chain_call(int dev, ChainCall* c) {
+  if (dev < 0) return FST_INVALID_ARG;
+  static const bool on = [] {
+    const char* e = std::getenv("FSTAMD_COALESCE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (!on) {
+    std::vector<ChainCall*> one{c};
+    run_chain_calls(dev, one);
+    return c->err;
+  }
+  ChainCombiner& C = chain_combiner(dev);
+  std::unique_lock<std::mutex> lk(C.mu);
+  C.q.push_back(c);
+  while (!c->done) {
+    if (C.leaders < kChainLeaders && !C.q.empty()) {
+      ++C.leaders;
+      const size_t take = std::min(C.q.size(), kChainMaxBatch);
+      std::vector<ChainCall*> batch(C.q.begin(), C.q.begin() + take);
+      C.q.erase(C.q.begin(), C.q.begin() + take);
+      lk.unlock();
+      run_chain_calls(dev, batch);
+      lk.lock();
+      for (ChainCall* x : batch) x->done = true;
+      --C.leaders;
+      C.cv.notify_all();
+    } else {
+      C.cv.wait(lk);
+    }
+  }
+  return c->err;
 }
 
 }  // namespace
@@ -944,23 +1070,28 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
     double kms = 0;
     int rc = -1;
     std::vector<uint32_t> chain;
-    if (as_chain(*a, &chain)) {  // the batch engines on one string
-      const uint64_t offs[2] = {0, chain.size()};
-      HostPaths h;
-      HostProf prof;  // FSTAMD_HOST_PROF=1: where the call's time goes
-      t_prof = &prof;
-      const FstError e = run_chain_batch_host(*b, chain.data(), offs, 1, n, FST_SEM_LAZY, -1, &h);
-      t_prof = nullptr;
-      prof.print("fst_compose_frozen_shortest_path");
+    if (as_chain(*a, &chain)) {  // the batch engines on one string, coalesced with the
+                                 // chain calls of other threads (ChainCombiner)
+      ChainCall c;
+      c.rhs = b;
+      c.n = n;
+      c.labels = &chain;
+      const FstError e = coalesced_chain_call(current_device(), &c);
       if (e == FST_OK) {
-        const int32_t st = h.status[0];
-        if (st == kPathOk || st == kPathEmpty) {
-          result = chain_result(h, 0);
+        if (c.status == kPathOk) {
+          const uint32_t P = (uint32_t)c.arcs.size();
+          result.add_states(P + 1);
+          result.set_start(0);
+          result.set_final(P, c.fin);
+          for (uint32_t k = 0; k < P; ++k) result.add_arc(k, c.arcs[k]);
           rc = 0;
-        } else if (st == kPathCycle) {
+        } else if (c.status == kPathEmpty) {
+          rc = 0;  // the empty FST
+        } else if (c.status == kPathCycle) {
           rc = 3;  // as the general path: the reference would not terminate
         }
-        kms = t_last_stats.kernel_ms;
+        t_last_stats = c.stats;
+        kms = c.stats.kernel_ms;
       }
     }
     // anything else (a general lhs; a string the batch engines handed back): one general lhs
@@ -1005,16 +1136,18 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
   DeviceFst* D = dev >= 0 ? b->device(dev) : nullptr;
   if (!D) return kInvalid;
   const bool hprof = std::getenv("FSTAMD_HOST_PROF") != nullptr;
-  const double t_up0 = us();
-  GraphUpload up(*a);
-  if (!up.ok) return kInvalid;
-  const double t_up1 = us();
   HostLattice lat;
   LaunchStats st;
+  double t_up0 = 0, t_up1 = 0;
   {
-    DeviceEngine& E = DeviceEngine::get(dev);
-    std::lock_guard<std::mutex> lk(E.mutex());
-    if (E.compose_lattice(*D, up.g, &lat, &st) != hipSuccess || lat.status != kPathOk) {
+    DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+    if (!E) return kInvalid;
+    const hipStream_t stream = E.stream();
+    t_up0 = us();
+    GraphUpload up(*a, stream);
+    if (!up.ok) return kInvalid;
+    t_up1 = us();
+    if (E->compose_lattice(*D, up.g, &lat, &st, stream) != hipSuccess || lat.status != kPathOk) {
       trace("compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(),
             st.kernel_ms);
       return kInvalid;
@@ -1082,7 +1215,10 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
     if (!gpu_available()) return kInvalid;
     const int dev = current_device();
     if (dev < 0) return kInvalid;
-    GraphUpload up(*m);
+    DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+    if (!E) return kInvalid;
+    const hipStream_t stream = E.stream();
+    GraphUpload up(*m, stream);
     m.reset();
     const double t_up = ms();
     // Non-negative weights: the parallel fixpoint (eager_bfs.hpp); a negative weight:
@@ -1094,12 +1230,9 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
     if (!out.ok()) return kInvalid;
     LaunchStats st;
     HostPaths hp;
-    {
-      DeviceEngine& E = DeviceEngine::get(dev);
-      std::lock_guard<std::mutex> lk(E.mutex());
-      if (E.shortest_path_graph(up.g, n, out.v, &st, up.nonneg) != hipSuccess) return kInvalid;
-      if (!out.download(1, &hp)) return kInvalid;
-    }
+    if (E->shortest_path_graph(up.g, n, out.v, &st, stream, up.nonneg) != hipSuccess)
+      return kInvalid;
+    if (!out.download(1, &hp, stream)) return kInvalid;
     t_last_stats = st;
     if (hp.status[0] == kPathCycle || hp.status[0] == kPathInternal ||
         hp.status[0] == kPathOutputFull)
@@ -1181,11 +1314,12 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   } prof_scope;
   HostPaths h;
   std::unique_ptr<DevOut> keep;
-  FstError e =
-      run_chain_batch_host(*b, labels, offsets, num_strings, n, semantics, dev, &h, &keep);
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return FST_INVALID_ARG;
+  FstError e = run_chain_batch_host(E, *b, labels, offsets, num_strings, n, semantics, &h, &keep);
   if (e != FST_OK) return e;
   if (!keep) return FST_OOM;
-  e = download_batch_result(dev, *keep, num_strings, nullptr, out);
+  e = download_batch_result(E, *keep, num_strings, nullptr, out);
   if (e != FST_OK) {
     fst_batch_result_free(out);
     return e;
@@ -1218,10 +1352,11 @@ FstError fst_device_project_output(const FstDeviceBatch* o, uint32_t num_strings
                 o->olabels, o->weights, o->arc_capacity,
                 (unsigned long long*)o->arc_cursor, o->work};
   uint32_t ml = 0;
-  DeviceEngine& E = DeviceEngine::get(dev);
-  std::lock_guard<std::mutex> lk(E.mutex());
-  if (E.project_output(v, num_strings, d_next_labels, d_next_offsets, d_proj_status, &ml,
-                       (hipStream_t)stream) != hipSuccess)
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return FST_INVALID_ARG;
+  const hipStream_t s = E.use((hipStream_t)stream);
+  if (E->project_output(v, num_strings, d_next_labels, d_next_offsets, d_proj_status, &ml, s) !=
+      hipSuccess)
     return FST_OOM;
   if (max_len) *max_len = ml;
   return FST_OK;
@@ -1251,6 +1386,9 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
   struct ProfScope {
     ~ProfScope() { t_prof = nullptr; }
   } prof_scope;
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return FST_INVALID_ARG;
+  const hipStream_t stream = E.stream();
   // stage-1 inputs
   const uint64_t total = num_strings ? offsets[num_strings] - offsets[0] : 0;
   uint32_t max_len = 0;
@@ -1260,12 +1398,15 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
     max_len = std::max<uint32_t>(max_len, (uint32_t)(rebased[i + 1] - rebased[i]));
   auto lab = std::make_unique<DevBuf>(total * 4), off = std::make_unique<DevBuf>((num_strings + 1ull) * 8);
   if (!lab->p || !off->p) return FST_OOM;
-  if (total && hipMemcpy(lab->p, labels + offsets[0], total * 4, hipMemcpyHostToDevice) != hipSuccess)
+  if (total && hipMemcpyAsync(lab->p, labels + offsets[0], total * 4, hipMemcpyHostToDevice,
+                              stream) != hipSuccess)
     return FST_OOM;
-  if (hipMemcpy(off->p, rebased.data(), (num_strings + 1ull) * 8, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpyAsync(off->p, rebased.data(), (num_strings + 1ull) * 8, hipMemcpyHostToDevice,
+                     stream) != hipSuccess)
     return FST_OOM;
   DevBuf fail(num_strings * 4ull);  // first failing stage's status, per string (device)
-  if (!fail.p || hipMemset(fail.p, 0, num_strings * 4ull) != hipSuccess) return FST_OOM;
+  if (!fail.p || hipMemsetAsync(fail.p, 0, num_strings * 4ull, stream) != hipSuccess)
+    return FST_OOM;
   uint64_t in_total = total;
   HostPaths h;
   std::unique_ptr<DevOut> keep;
@@ -1275,35 +1416,35 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
     if (!D) return FST_OOM;
     ChainInput in{(const uint32_t*)lab->p, (const uint64_t*)off->p, num_strings, max_len};
     keep.reset();
-    FstError e = run_chain_batch_dev(*D, in, in_total, n, semantics, dev, &h, &keep);
+    FstError e = run_chain_batch_dev(E, *D, in, in_total, n, semantics, &h, &keep);
     if (e != FST_OK) return e;
     if (!keep) return FST_OOM;  // run_chain_batch_dev sets it on FST_OK; never dereference null
     if (k + 1 == num_stages) break;
     // project this stage's outputs into the next stage's inputs, on the device
     unsigned long long used = 0;
-    if (hipMemcpy(&used, keep->v.cursor, 8, hipMemcpyDeviceToHost) != hipSuccess) return FST_OOM;
+    if (hipMemcpyAsync(&used, keep->v.cursor, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return FST_OOM;
     auto nlab = std::make_unique<DevBuf>((used + num_strings) * 4);
     auto noff = std::make_unique<DevBuf>((num_strings + 1ull) * 8);
     DevBuf pst(num_strings * 4ull);
     if (!nlab->p || !noff->p || !pst.p) return FST_OOM;
-    {
-      DeviceEngine& E = DeviceEngine::get(dev);
-      std::lock_guard<std::mutex> lk(E.mutex());
-      if (E.project_output(keep->v, num_strings, (uint32_t*)nlab->p, (uint64_t*)noff->p,
-                           (int32_t*)pst.p, &max_len, nullptr) != hipSuccess ||
-          E.merge_status((int32_t*)fail.p, (const int32_t*)pst.p, num_strings, nullptr) !=
-              hipSuccess)
-        return FST_OOM;
-    }
+    if (E->project_output(keep->v, num_strings, (uint32_t*)nlab->p, (uint64_t*)noff->p,
+                          (int32_t*)pst.p, &max_len, stream) != hipSuccess ||
+        E->merge_status((int32_t*)fail.p, (const int32_t*)pst.p, num_strings, stream) !=
+            hipSuccess)
+      return FST_OOM;
     uint64_t nt = 0;  // (synchronises: pst may go back to the pool)
-    if (hipMemcpy(&nt, (uint64_t*)noff->p + num_strings, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpyAsync(&nt, (uint64_t*)noff->p + num_strings, 8, hipMemcpyDeviceToHost,
+                       stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
       return FST_OOM;
     in_total = nt;
     lab = std::move(nlab);
     off = std::move(noff);
     prof.lap(4);
   }
-  FstError e = download_batch_result(dev, *keep, num_strings, (const int32_t*)fail.p, out);
+  FstError e = download_batch_result(E, *keep, num_strings, (const int32_t*)fail.p, out);
   if (e != FST_OK) {
     fst_batch_result_free(out);
     return e;
@@ -1334,11 +1475,12 @@ FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_
                 o->olabels, o->weights, o->arc_capacity,
                 (unsigned long long*)o->arc_cursor, o->work};
   ChainInput in{d_labels, d_offsets, num_strings, max_len};
-  DeviceEngine& E = DeviceEngine::get(dev);
-  std::lock_guard<std::mutex> lk(E.mutex());
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return FST_INVALID_ARG;
+  const hipStream_t s = E.use((hipStream_t)stream);
   LaunchStats st;
   const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
-  if (E.run_chain(*D, in, n, semantics, v, (hipStream_t)stream, &st) != hipSuccess) return FST_OOM;
+  if (E->run_chain(*D, in, n, semantics, v, s, &st) != hipSuccess) return FST_OOM;
   t_last_stats = st;
   return FST_OK;
 }

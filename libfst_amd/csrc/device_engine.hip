@@ -6,7 +6,9 @@
 #include <cstring>
 #include <chrono>
 #include <cstdlib>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include <hipcub/hipcub.hpp>
@@ -101,8 +103,8 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
                                                                 d->final_w, d->il, d->rec,
                                                                 d->sspan);
   }
-  if (hipDeviceSynchronize() != hipSuccess) {
-    DeviceFst::destroy(d);
+  if (hipStreamSynchronize(nullptr) != hipSuccess) {  // the null stream only: other calls'
+    DeviceFst::destroy(d);                            // engines run on their own streams
     return nullptr;
   }
   uint32_t max_span = 0, jb = 0, jf = 0;
@@ -123,7 +125,9 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   d->nan = f.has_nan_weight();
   d->finite = f.arc_weights_finite();
   d->weight_type = f.weight_type();
-  if (!build_reverse_mirror(d, f)) {  // pull tier (eager_pull.hip); false = device OOM
+  // pull tier (eager_pull.hip); false = device OOM.  Its uploads go to the null stream:
+  // wait for them before engines on their own streams read the mirror
+  if (!build_reverse_mirror(d, f) || hipStreamSynchronize(nullptr) != hipSuccess) {
     DeviceFst::destroy(d);
     return nullptr;
   }
@@ -326,13 +330,78 @@ uint32_t next_pow2(uint64_t x) {
 }
 }  // namespace
 
-DeviceEngine& DeviceEngine::get(int dev) {
+namespace {
+// The engines of one device: created on demand up to max_engines(), leased LIFO (a single
+// caller keeps reusing the same warm engine).
+struct EnginePool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::unique_ptr<DeviceEngine>> all;
+  std::vector<DeviceEngine*> idle;
+  std::mutex heavy;  // dense-replay plans sized from free HBM: query + allocate one at a time
+};
+EnginePool& engine_pool(int dev) {
   static std::mutex mu;
-  static std::vector<std::unique_ptr<DeviceEngine>> engines;
+  static std::vector<std::unique_ptr<EnginePool>>* pools =
+      new std::vector<std::unique_ptr<EnginePool>>();  // never destroyed (static teardown)
   std::lock_guard<std::mutex> g(mu);
-  if ((int)engines.size() <= dev) engines.resize(dev + 1);
-  if (!engines[dev]) engines[dev].reset(new DeviceEngine(dev));
-  return *engines[dev];
+  if ((int)pools->size() <= dev) pools->resize(dev + 1);
+  if (!(*pools)[dev]) (*pools)[dev].reset(new EnginePool());
+  return *(*pools)[dev];
+}
+size_t max_engines() {
+  static const size_t k = [] {
+    const char* e = std::getenv("FSTAMD_ENGINES");
+    const int v = e ? std::atoi(e) : 4;
+    return (size_t)std::max(1, std::min(v, 64));
+  }();
+  return k;
+}
+}  // namespace
+
+DeviceEngine::Lease DeviceEngine::acquire(int dev) {
+  if (dev < 0) return Lease();
+  EnginePool& P = engine_pool(dev);
+  std::unique_lock<std::mutex> lk(P.mu);
+  for (;;) {
+    if (!P.idle.empty()) {
+      DeviceEngine* e = P.idle.back();
+      P.idle.pop_back();
+      return Lease(e);
+    }
+    if (P.all.size() < max_engines()) {
+      P.all.emplace_back(new DeviceEngine(dev));
+      return Lease(P.all.back().get());
+    }
+    P.cv.wait(lk);
+  }
+}
+
+hipStream_t DeviceEngine::Lease::own_stream() const { return e_ ? e_->stream_ : nullptr; }
+
+hipStream_t DeviceEngine::Lease::use(hipStream_t s) {
+  if (!e_) return s;
+  (void)hipSetDevice(e_->dev_);
+  // work of the engine's previous user on another stream finishes before ours starts
+  if (e_->done_valid_ && e_->done_stream_ != s) (void)hipStreamWaitEvent(s, e_->done_, 0);
+  s_ = s;
+  used_ = true;
+  return s;
+}
+
+DeviceEngine::Lease::~Lease() {
+  if (!e_) return;
+  if (used_) {
+    (void)hipSetDevice(e_->dev_);
+    e_->done_valid_ = hipEventRecord(e_->done_, s_) == hipSuccess;
+    e_->done_stream_ = s_;
+  }
+  EnginePool& P = engine_pool(e_->dev_);
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    P.idle.push_back(e_);
+  }
+  P.cv.notify_one();
 }
 
 DeviceEngine::DeviceEngine(int dev) : dev_(dev) {
@@ -344,6 +413,10 @@ DeviceEngine::DeviceEngine(int dev) : dev_(dev) {
   sizes_.assign(kNumScratch, 0);
   (void)hipEventCreate(&ev0_);
   (void)hipEventCreate(&ev1_);
+  (void)hipEventCreateWithFlags(&done_, hipEventDisableTiming);
+  // non-blocking: the legacy null stream (other libraries, torch's default) never
+  // serialises with it, and calls on other engines run concurrently
+  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) stream_ = nullptr;
 }
 
 void* DeviceEngine::scratch(size_t idx, size_t bytes) {
@@ -358,6 +431,15 @@ void* DeviceEngine::scratch(size_t idx, size_t bytes) {
   }
   sizes_[idx] = bytes;
   return bufs_[idx];
+}
+
+// A synchronous copy ordered with the engine's work on `stream` (the legacy synchronous
+// hipMemcpy goes to the null stream, which a non-blocking engine stream does not wait for).
+static hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind,
+                            hipStream_t stream) {
+  if (bytes == 0) return hipSuccess;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, kind, stream));
+  return hipStreamSynchronize(stream);
 }
 
 static hipError_t finish_stats(hipEvent_t e0, hipEvent_t e1, LaunchStats* stats) {
@@ -970,7 +1052,11 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     budget = (uint64_t)std::max(1, std::atoi(be)) << 30;
     budget_known = true;
   }
+  // plans that ask the runtime for free HBM are made (and their arrays allocated) one at a
+  // time per device: two concurrent calls would otherwise both size themselves to it
+  std::unique_lock<std::mutex> heavy(engine_pool(dev_).heavy, std::defer_lock);
   auto query_budget = [&] {
+    if (!heavy.owns_lock()) heavy.lock();
     device_pool_release(dev_);  // idle pooled blocks count as free HBM
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
@@ -1270,7 +1356,8 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
 }
 
 hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput& lhs,
-                                         HostLattice* lat, LaunchStats* stats) {
+                                         HostLattice* lat, LaunchStats* stats,
+                                         hipStream_t stream) {
   HIP_TRY(hipSetDevice(dev_));
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!ctr) return hipErrorOutOfMemory;
@@ -1306,25 +1393,25 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
     ws.lcap = c.lcap;
     ws.wd_ticks = watchdog_ticks();
     ws.lattice_only = 1;
-    HIP_TRY(hipMemset(ctr, 0, 64));
-    if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
+    HIP_TRY(hipMemsetAsync(ctr, 0, 64, stream));
+    if (stats) HIP_TRY(hipEventRecord(ev0_, stream));
     ChainInput none{};
     if (wg1k)
-      eager_bfs_kernel<1024, true><<<1, 1024, 0, nullptr>>>(rhs.view, none, lhs, 1, ctr, nullptr,
+      eager_bfs_kernel<1024, true><<<1, 1024, 0, stream>>>(rhs.view, none, lhs, 1, ctr, nullptr,
                                                             nullptr, 1, ws, none_out);
     else
-      eager_bfs_kernel<kBfsWG, true><<<1, kBfsWG, 0, nullptr>>>(rhs.view, none, lhs, 1, ctr,
+      eager_bfs_kernel<kBfsWG, true><<<1, kBfsWG, 0, stream>>>(rhs.view, none, lhs, 1, ctr,
                                                                 nullptr, nullptr, 1, ws, none_out);
     HIP_TRY(hipGetLastError());
     if (stats) {
-      HIP_TRY(hipEventRecord(ev1_, nullptr));
+      HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
       stats->engine = 2;
       stats->grid = 1;
       stats->launches = tier - tier0 + 1;
     }
     uint32_t hdr[8];
-    HIP_TRY(hipMemcpy(hdr, ws.hdr, sizeof(hdr), hipMemcpyDeviceToHost));
+    HIP_TRY(copy_sync(hdr, ws.hdr, sizeof(hdr), hipMemcpyDeviceToHost, stream));
     lat->status = (int32_t)hdr[3];
     if (lat->status == kPathOverflow) continue;
     lat->n_nodes = hdr[0];
@@ -1351,32 +1438,36 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
                  o_nfin = o_nback + r((size_t)c.ncap * 8), o_anext = o_nfin + r((size_t)c.ncap * 8),
                  o_ail = o_anext + r((size_t)c.acap * 4), o_aol = o_ail + r((size_t)c.acap * 4),
                  o_aw = o_aol + r((size_t)c.acap * 4);
-    HIP_TRY(hipMemcpy(lat->aoff.data(), p + o_aoff, (N + 1) * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(lat->nfin.data(), p + o_nfin, N * 8, hipMemcpyDeviceToHost));
+    // pinned host arrays: asynchronous DMAs, one synchronisation
+    const auto d2h = [&](void* dst, const void* src, size_t b) {
+      return hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, stream);
+    };
+    HIP_TRY(d2h(lat->aoff.data(), p + o_aoff, (N + 1) * 4));
+    HIP_TRY(d2h(lat->nfin.data(), p + o_nfin, N * 8));
     if (A) {
-      HIP_TRY(hipMemcpy(lat->anext.data(), p + o_anext, A * 4, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(lat->ail.data(), p + o_ail, A * 4, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(lat->aol.data(), p + o_aol, A * 4, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(lat->aw.data(), p + o_aw, A * 8, hipMemcpyDeviceToHost));
+      HIP_TRY(d2h(lat->anext.data(), p + o_anext, A * 4));
+      HIP_TRY(d2h(lat->ail.data(), p + o_ail, A * 4));
+      HIP_TRY(d2h(lat->aol.data(), p + o_aol, A * 4));
+      HIP_TRY(d2h(lat->aw.data(), p + o_aw, A * 8));
     }
-    return hipSuccess;
+    return hipStreamSynchronize(stream);
   }
 }
 
 hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
                                              const BatchOutDev& out, LaunchStats* stats,
-                                             bool nonneg) {
+                                             hipStream_t stream, bool nonneg) {
   HIP_TRY(hipSetDevice(dev_));
   const uint32_t N = g.num_states;
   if (!nonneg) {  // negative weights: exact replay of the heap order, one lane
     uint32_t A = 0;
-    if (N) HIP_TRY(hipMemcpy(&A, g.state_off + N, 4, hipMemcpyDeviceToHost));
+    if (N) HIP_TRY(copy_sync(&A, g.state_off + N, 4, hipMemcpyDeviceToHost, stream));
     const uint64_t hcap = (uint64_t)A + 1;
     const size_t nd_b = ((size_t)N * 16 + 255) & ~(size_t)255;
     const size_t st_b = ((size_t)N + 255) & ~(size_t)255;
     uint8_t* w = (uint8_t*)scratch(kBfsSlab, nd_b + st_b + hcap * sizeof(SpHeapEnt));
     if (!w) return hipErrorOutOfMemory;
-    HIP_TRY(hipMemset(out.cursor, 0, 8));
+    HIP_TRY(hipMemsetAsync(out.cursor, 0, 8, stream));
     BfsTables T{};
     T.aoff = const_cast<uint32_t*>(g.state_off);
     T.anext = const_cast<uint32_t*>(g.arc_next);
@@ -1386,36 +1477,36 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
     T.nfin = const_cast<double*>(g.final_w);
     T.nd = (unsigned long long*)w;
     T.nback = (unsigned long long*)(w + (size_t)N * 8);
-    if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
-    sp_replay_kernel<<<1, 64, 0, nullptr>>>(T, N, g.start, n, (SpHeapEnt*)(w + nd_b + st_b),
+    if (stats) HIP_TRY(hipEventRecord(ev0_, stream));
+    sp_replay_kernel<<<1, 64, 0, stream>>>(T, N, g.start, n, (SpHeapEnt*)(w + nd_b + st_b),
                                             hcap, w + nd_b, out, watchdog_ticks());
     HIP_TRY(hipGetLastError());
     if (stats) {
-      HIP_TRY(hipEventRecord(ev1_, nullptr));
+      HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
       stats->engine = 6;
       stats->grid = 1;
       stats->launches = 1;
     }
-    return hipDeviceSynchronize();
+    return hipStreamSynchronize(stream);
   }
   // work arrays: distances, back-pointers, stamps, settled flags, two frontiers, the
   // pending list (one entry per arc at most); the one "level" [0, N) and the distance
   // kernels' flags in the header
   const size_t n_b = ((size_t)N * 4 + 255) & ~(size_t)255;
   uint32_t A = 0;
-  if (N) HIP_TRY(hipMemcpy(&A, g.state_off + N, 4, hipMemcpyDeviceToHost));
+  if (N) HIP_TRY(copy_sync(&A, g.state_off + N, 4, hipMemcpyDeviceToHost, stream));
   uint8_t* w = (uint8_t*)scratch(kBfsSlab, (size_t)N * 16 + 256 + 4 * n_b + ((size_t)A + 64) * 4);
   uint32_t* lv = (uint32_t*)scratch(kBfsHdr, 32);
   if (!w || !lv) return hipErrorOutOfMemory;
   const uint32_t lvh[8] = {0, N, 0, 0, 0, 0, 0, 0};  // [2..3]: have_dist, expired; [4..5] prof
-  HIP_TRY(hipMemcpy(lv, lvh, 32, hipMemcpyHostToDevice));
+  HIP_TRY(copy_sync(lv, lvh, 32, hipMemcpyHostToDevice, stream));
   uint32_t* mark = (uint32_t*)(w + (((size_t)N * 16 + 255) & ~(size_t)255));
   uint32_t* fa = (uint32_t*)((uint8_t*)mark + n_b);
   uint32_t* fb = (uint32_t*)((uint8_t*)fa + n_b);
   uint32_t* stl = (uint32_t*)((uint8_t*)fb + n_b);
   uint32_t* pend = (uint32_t*)((uint8_t*)stl + n_b);
-  HIP_TRY(hipMemset(out.cursor, 0, 8));
+  HIP_TRY(hipMemsetAsync(out.cursor, 0, 8, stream));
   BfsTables T{};
   T.aoff = const_cast<uint32_t*>(g.state_off);
   T.anext = const_cast<uint32_t*>(g.arc_next);
@@ -1426,14 +1517,14 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
   T.lvl = lv;
   T.nd = (unsigned long long*)w;
   T.nback = (unsigned long long*)(w + (size_t)N * 8);
-  if (stats) HIP_TRY(hipEventRecord(ev0_, nullptr));
+  if (stats) HIP_TRY(hipEventRecord(ev0_, stream));
   // FSTAMD_SP_SWEEP=1: the Gauss-Seidel sweeps over every arc instead of the frontier
   const bool sweep = std::getenv("FSTAMD_SP_SWEEP") != nullptr;
   const bool hprof = std::getenv("FSTAMD_HOST_PROF") != nullptr;
   hipEvent_t em = nullptr;
   if (hprof) {
     HIP_TRY(hipEventCreate(&em));
-    HIP_TRY(hipEventRecord(ev0_, nullptr));
+    HIP_TRY(hipEventRecord(ev0_, stream));
   }
   // distances: settled in distance order (sp_settle_kernel); after more than
   // FSTAMD_SP_MAX_ADV (256) distinct distances, label correcting (sp_frontier_kernel)
@@ -1441,23 +1532,23 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
   if (!sweep && g.start < N && n == 1) {
     const char* ma = std::getenv("FSTAMD_SP_MAX_ADV");
     const uint32_t max_adv = ma ? (uint32_t)std::strtoul(ma, nullptr, 10) : 256u;
-    sp_settle_kernel<1024><<<1, 1024, 0, nullptr>>>(T, N, g.start, mark, stl, fa, fb, pend,
+    sp_settle_kernel<1024><<<1, 1024, 0, stream>>>(T, N, g.start, mark, stl, fa, fb, pend,
                                                     lv + 4, max_adv, watchdog_ticks());
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpy(sf, lv + 4, 16, hipMemcpyDeviceToHost));
+    HIP_TRY(copy_sync(sf, lv + 4, 16, hipMemcpyDeviceToHost, stream));
     if (sf[1]) {  // its watchdog fired: the path reports INTERNAL
       const uint32_t one = 1;
-      HIP_TRY(hipMemcpy(lv + 3, &one, 4, hipMemcpyHostToDevice));
+      HIP_TRY(copy_sync(lv + 3, &one, 4, hipMemcpyHostToDevice, stream));
     } else if (sf[0]) {
-      sp_frontier_kernel<1024><<<1, 1024, 0, nullptr>>>(T, N, g.start, mark, fa, fb, lv + 3,
+      sp_frontier_kernel<1024><<<1, 1024, 0, stream>>>(T, N, g.start, mark, fa, fb, lv + 3,
                                                         watchdog_ticks());
     }
   }
-  if (hprof) HIP_TRY(hipEventRecord(em, nullptr));
-  sp_graph_kernel<1024><<<1, 1024, 0, nullptr>>>(
+  if (hprof) HIP_TRY(hipEventRecord(em, stream));
+  sp_graph_kernel<1024><<<1, 1024, 0, stream>>>(
       T, N, g.start, n, out, watchdog_ticks(), sweep || g.start >= N || n != 1 ? nullptr : lv + 2);
   if (hprof) {
-    HIP_TRY(hipEventRecord(ev1_, nullptr));
+    HIP_TRY(hipEventRecord(ev1_, stream));
     HIP_TRY(hipEventSynchronize(ev1_));
     float a = 0.f, b = 0.f;
     HIP_TRY(hipEventElapsedTime(&a, ev0_, em));
@@ -1469,13 +1560,13 @@ hipError_t DeviceEngine::shortest_path_graph(const GraphInput& g, uint32_t n,
   }
   HIP_TRY(hipGetLastError());
   if (stats) {
-    HIP_TRY(hipEventRecord(ev1_, nullptr));
+    HIP_TRY(hipEventRecord(ev1_, stream));
     HIP_TRY(finish_stats(ev0_, ev1_, stats));
     stats->engine = 2;
     stats->grid = 1;
     stats->launches = 1;
   }
-  return hipDeviceSynchronize();
+  return hipStreamSynchronize(stream);
 }
 
 // ---------------------------------------------------------------------------------

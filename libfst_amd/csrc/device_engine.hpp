@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
 #include <mutex>
 #include <new>
@@ -202,11 +203,40 @@ hipError_t launch_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t
                             unsigned int* next_item, const EagerLaunch& lp,
                             const BatchOutDev& out, uint32_t grid, hipStream_t stream);
 
-// Per-device engine state: persistent workspaces (grown on demand) and a lock,
-// since the C ABI may be called from several threads.
+// Per-device engine state: persistent workspaces (grown on demand), its own non-blocking
+// HIP stream and events.  A device has a small pool of engines (FSTAMD_ENGINES, default
+// 4): concurrent C-ABI calls each lease one, so they run side by side on separate streams
+// and synchronise only their own stream (src/c-api.zig:776-787 runs compute outside its
+// lock; include/fst.h:11-26).
 class DeviceEngine {
  public:
-  static DeviceEngine& get(int dev);
+  // Exclusive use of one engine of `dev` for the lifetime of the lease.  use(s) binds the
+  // stream the call's work goes on (the engine's own stream for synchronous entries, the
+  // caller's for the async device entries): a stream other than the previous user's first
+  // waits for that user's work (an event), and the lease records the event when it ends,
+  // so an engine's workspaces are never reused while earlier work on them still runs.
+  class Lease {
+   public:
+    Lease() = default;
+    Lease(Lease&& o) noexcept : e_(o.e_), s_(o.s_), used_(o.used_) { o.e_ = nullptr; }
+    Lease& operator=(Lease&&) = delete;
+    ~Lease();
+    DeviceEngine* operator->() const { return e_; }
+    DeviceEngine& operator*() const { return *e_; }
+    explicit operator bool() const { return e_ != nullptr; }
+    hipStream_t use(hipStream_t s);
+    hipStream_t stream() { return used_ ? s_ : use(own_stream()); }
+
+   private:
+    friend class DeviceEngine;
+    explicit Lease(DeviceEngine* e) : e_(e) {}
+    hipStream_t own_stream() const;
+    DeviceEngine* e_ = nullptr;
+    hipStream_t s_ = nullptr;
+    bool used_ = false;
+  };
+  // Blocks while every engine of the device is leased.  An empty lease on failure.
+  static Lease acquire(int dev);
 
   // All launches are asynchronous on `stream`; stats are filled when `stats` is
   // non-null (this synchronises on the stream's end event).
@@ -214,9 +244,10 @@ class DeviceEngine {
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
   hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
-  // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp).
+  // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp), on
+  // `stream` (synchronised: the lattice is downloaded).
   hipError_t compose_lattice(const DeviceFst& rhs, const GraphInput& lhs, HostLattice* lat,
-                             LaunchStats* stats);
+                             LaunchStats* stats, hipStream_t stream);
   // Output tape of each path of a finished stage as the next stage's chain inputs
   // (printOutputString + compileString on device): next_labels = the path's non-epsilon
   // olabels.  A string whose status is not OK, or whose output has a label > 256, gets
@@ -239,14 +270,19 @@ class DeviceEngine {
   // fst_shortest_path on an explicit graph; `g` holds the FST itself (CSR, arcs in
   // insertion order).  nonneg: every weight >= +0 (parallel fixpoint); otherwise the exact
   // one-lane replay of the reference's heap order (sp_replay_kernel).  No NaN weights.
+  // Runs on `stream` and synchronises it.
   hipError_t shortest_path_graph(const GraphInput& g, uint32_t n, const BatchOutDev& out,
-                                 LaunchStats* stats, bool nonneg = true);
+                                 LaunchStats* stats, hipStream_t stream, bool nonneg = true);
 
   int dev() const { return dev_; }
-  std::mutex& mutex() { return mu_; }
+  int num_cus() const { return num_cus_; }
 
  private:
   explicit DeviceEngine(int dev);
+  hipStream_t stream_ = nullptr;   // the engine's own stream (non-blocking)
+  hipEvent_t done_ = nullptr;      // recorded when a lease ends (on the stream it used)
+  hipStream_t done_stream_ = nullptr;
+  bool done_valid_ = false;
   // General engine (kernels/eager_bfs.hpp) over the strings of `in` whose status is
   // UNSUPPORTED or OVERFLOW after the layered tiers (all strings when `all`); eager
   // shortestPath or, with `lazy`, composeShortestPath semantics (finite weights >= 0).
@@ -273,7 +309,6 @@ class DeviceEngine {
   void* scratch(size_t idx, size_t bytes);
   int dev_;
   int num_cus_ = 0;
-  std::mutex mu_;
   std::vector<void*> bufs_;
   std::vector<size_t> sizes_;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

@@ -1,0 +1,129 @@
+"""Concurrent C-ABI calls (include/fst.h:11-26: the reference computes outside its lock,
+src/c-api.zig:744-811, so N threads may call at once and fst_free may race a call).
+
+Every result is bit-compared with the oracle.  The engines are leased per call (one of a
+small pool per device, each with its own stream), and concurrent chain calls of
+fst_compose_frozen_shortest_path are coalesced into shared batch launches.
+"""
+import json
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+import libfst_amd as F
+import oracle_ffi as O
+from test_gpu_parity import bits, load_blob, random_rhs, to_product
+
+pytestmark = pytest.mark.gpu
+
+TOOL = os.path.join(os.path.dirname(F.fst.LIB_PATH), "concurrent_calls")
+
+
+def norm(start, finals, arcs):
+    return (start, [int(bits([x])[0]) for x in finals],
+            [[(a, b, int(bits([w])[0]), d) for (a, b, w, d) in al] for al in arcs])
+
+
+def oracle_single(lhs: O.Fst, blob):
+    rc, ref = O.compose_shortest_path(lhs, blob, 1)
+    if rc != O.OR_OK:
+        return None
+    return norm(ref.start, ref.finals, ref.arcs)
+
+
+def run_threads(n, fn):
+    errs = []
+
+    def wrap(t):
+        try:
+            fn(t)
+        except BaseException as e:  # noqa: BLE001 (reported below)
+            errs.append((t, repr(e)))
+    th = [threading.Thread(target=wrap, args=(t,)) for t in range(n)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:3]
+
+
+def test_threads_single_chain_calls():
+    blob = O.freeze(O.gen("ambiguous", 512, 12))
+    rhs = load_blob(blob)
+    rng = np.random.default_rng(77)
+    texts = [bytes(np.where(rng.random(int(L)) < 0.95, 0, 1).astype(np.uint8).tolist())
+             for L in rng.integers(0, 48, 40)]
+    expect = [oracle_single(O.compile_string(t), blob) for t in texts]
+
+    def work(t):
+        for i in range(30):
+            k = (t * 13 + i) % len(texts)
+            got = F.compose_frozen_shortest_path(F.MutableFst.compile_string(texts[k]), rhs, 1)
+            g = None if got is None else norm(*got.to_lists())
+            assert g == expect[k], (t, i, k)
+    run_threads(32, work)
+
+
+def test_threads_mixed_entries():
+    # chain calls, general-lhs calls, fst_compose_frozen, fst_shortest_path and batch calls
+    # at the same time, each against the oracle
+    rng = np.random.default_rng(78)
+    eps_blob = O.freeze(O.gen("eps_dense", 64, 6))
+    eps = load_blob(eps_blob)
+    rnd = random_rhs(rng, 12, 50, 3, eps=True)
+    rnd_blob = O.freeze(rnd)
+    rnd_rhs = load_blob(rnd_blob)
+    lhs_graphs = [random_rhs(np.random.default_rng(900 + i), 5, 14, 3, eps=True) for i in range(8)]
+    exp_general = [oracle_single(g, rnd_blob) for g in lhs_graphs]
+    chains = [O.compile_string(bytes([0] * L)) for L in (0, 3, 9, 17)]
+    exp_chain = [oracle_single(c, eps_blob) for c in chains]
+    comp = [O.compose(c, eps_blob) for c in chains]
+    seqs = [[1] * int(L) for L in rng.integers(0, 30, 64)]
+    lab = np.concatenate([np.asarray(s, np.uint32) for s in seqs])
+    off = np.concatenate([[0], np.cumsum([len(s) for s in seqs])]).astype(np.uint64)
+    ref_b = O.batch_run(eps_blob, lab, off, 0, 1)
+
+    def work(t):
+        for i in range(8):
+            kind = (t + i) % 4
+            if kind == 0:
+                k = (t + i) % len(chains)
+                got = F.compose_frozen_shortest_path(to_product(chains[k]), eps, 1)
+                assert (None if got is None else norm(*got.to_lists())) == exp_chain[k]
+            elif kind == 1:
+                k = (t + i) % len(lhs_graphs)
+                got = F.compose_frozen_shortest_path(to_product(lhs_graphs[k]), rnd_rhs, 1)
+                assert (None if got is None else norm(*got.to_lists())) == exp_general[k]
+            elif kind == 2:
+                k = (t + i) % len(chains)
+                rc, ref = comp[k]
+                got = F.compose_frozen(to_product(chains[k]), eps)
+                assert norm(*got.to_lists()) == norm(ref.start, ref.finals, ref.arcs)
+            else:
+                got = F.compose_frozen_shortest_path_batch(eps, lab, off, 1, F.FST_SEM_LAZY)
+                assert np.array_equal(got.offsets, ref_b.offsets)
+                assert np.array_equal(got.olabels, ref_b.olabels)
+                assert np.array_equal(bits(got.weights), bits(ref_b.weights))
+    run_threads(16, work)
+
+
+def run_tool(*args):
+    r = subprocess.run([TOOL, *args], capture_output=True, text=True, timeout=300)
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    return r.returncode, line
+
+
+def test_tool_32_threads_1000_calls():
+    rc, line = run_tool("--threads", "32", "--calls", "1000")
+    assert rc == 0 and line["mismatches"] == 0, line
+    print(json.dumps(line))
+
+
+def test_tool_varied_with_free_midway():
+    rc, line = run_tool("--threads", "32", "--calls", "300", "--varied", "--free-midway",
+                        "--len", "48", "--transducer-len", "512")
+    assert rc == 0 and line["mismatches"] == 0, line
+    print(json.dumps(line))
