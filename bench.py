@@ -268,8 +268,15 @@ def timed(batch, rhs, sem, dev_index, steps, warmup, world):
 
 
 def nproc():
-    """What `nproc` prints: the CPUs this process may run on (its affinity mask).  On the GPU
-    box that is the box's CPU share (16), while os.cpu_count() reports the whole host."""
+    """What GNU `nproc` prints: OMP_NUM_THREADS when set, else the CPUs of this process's
+    affinity mask.  On the GPU box that is its CPU share (16: OMP_NUM_THREADS, and the cgroup
+    quota cpu.max), while the affinity mask and os.cpu_count() show the whole host (256)."""
+    try:
+        v = int(os.environ.get("OMP_NUM_THREADS", "0"))
+        if v > 0:
+            return v
+    except ValueError:
+        pass
     try:
         return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):

@@ -57,10 +57,30 @@ typedef struct {
     uint64_t total_arcs;
 } FstBatchResult;
 
+/* Multi-GPU batches inside the library: with FST_BATCH_DEVICES in flags the
+ * host entries (fst_compose_frozen_shortest_path_batch, fst_pipeline_batch) split the
+ * strings into contiguous shards balanced by estimated work (sum over the string's input
+ * positions of the rhs states a layer can hold) and run one shard per device of
+ * device_mask (bit d = HIP device d), each on its own host thread, with the frozen rhs
+ * replicated to every device on first use (one DMA from its pinned host copy).  Results
+ * are gathered into one FstBatchResult in input order, identical to a one-device run.
+ * num_shards > popcount(device_mask) runs several shards per device (round robin) on
+ * separate engines and streams; 0 = one per device.  No collective runs on the data path. */
+#define FST_BATCH_DEVICES 1u
+
+/* The work estimate the shard planner uses for one chain string of `len` labels against
+ * rhs b (product tuples: the sum over input positions of the rhs states a layer can hold),
+ * for callers that shard batches over processes themselves (one rank per GPU); < 0 for an
+ * invalid handle. */
+double fst_chain_cost(FstHandle b, uint64_t len);
+
 typedef struct {
-    int32_t device;           /* HIP device ordinal (-1: current device) */
+    int32_t device;           /* HIP device ordinal (-1: current device); without
+                                 FST_BATCH_DEVICES the whole batch runs there */
     uint32_t semantics;       /* FstSemantics */
-    uint32_t flags;           /* reserved, 0 */
+    uint32_t flags;           /* FST_BATCH_DEVICES or 0 */
+    uint32_t num_shards;      /* with FST_BATCH_DEVICES: shards (0 = one per device) */
+    uint64_t device_mask;     /* with FST_BATCH_DEVICES: the devices (0 = `device` only) */
 } FstBatchOptions;
 
 /* Host arrays in, host result out (H2D, kernels, D2H).  Returns FST_INVALID_ARG for an

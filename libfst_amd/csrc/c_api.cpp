@@ -17,10 +17,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -80,7 +83,9 @@ class HandleTable {  // src/c-api.zig:132-271
   std::vector<uint32_t> free_;
 };
 
-std::mutex g_api_mu;
+// Handle tables (src/c-api.zig:132-271): one lock, shared by read-only queries (the
+// result readback of many concurrent calls), exclusive for inserts, removes and edits.
+std::shared_mutex g_api_mu;
 HandleTable<MutableFst> g_mut;
 HandleTable<FrozenFst> g_fst;
 
@@ -596,27 +601,49 @@ FstError run_chain_batch_host(DeviceEngine::Lease& E, FrozenFst& b, const uint32
   return run_chain_batch_dev(E, *D, in, total, n, semantics, h, keep);
 }
 
-// The batch result straight from the device outputs: compacted to CSR on the device
-// (DeviceEngine::compact_paths), then one copy per array into the caller's result.
-// `fail` (device, optional): a pipeline's first failing stage per string.
-FstError download_batch_result(DeviceEngine::Lease& E, const DevOut& o, uint32_t num,
-                               const int32_t* fail, FstBatchResult* out) {
-  const hipStream_t stream = E.stream();
+// ---- Host batches in shards (one device, or several: FST_BATCH_DEVICES) ---------------
+// A shard is strings [s0, s1) of the caller's arrays on one device: computed on an engine
+// lease (its device outputs kept), compacted to CSR on the device (count, scan, gather:
+// DeviceEngine::compact_paths), then downloaded straight into the caller's result at the
+// shard's string and arc offsets.
+struct Shard {
+  int dev = 0;
+  uint32_t s0 = 0, s1 = 0;
+  DeviceEngine::Lease E;
+  std::unique_ptr<DevOut> keep;
+  std::unique_ptr<DevBuf> fail;  // pipelines: the first failing stage per string
+  std::unique_ptr<DevBuf> st, off, fin, il, ol, w;
+  uint64_t tot = 0;
+  FstError err = FST_OK;
+  LaunchStats stats;
+};
+
+FstError shard_compact(Shard& S) {
+  const uint32_t num = S.s1 - S.s0;
+  const hipStream_t stream = S.E.stream();
+  const DevOut& o = *S.keep;
   unsigned long long used = 0;
   if (hipMemcpyAsync(&used, o.cursor.p, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return FST_OOM;
   used = std::min<unsigned long long>(used, o.v.arc_cap);
-  DevBuf st(num * 4ull), off((num + 1ull) * 8), fin(num * 8ull), il(used * 4), ol(used * 4),
-      w(used * 8);
-  if (!st.p || !off.p || !fin.p || !il.p || !ol.p || !w.p) return FST_OOM;
-  uint64_t tot = 0;
-  if (E->compact_paths(o.v, num, fail, (int32_t*)st.p, (uint64_t*)off.p, (uint32_t*)il.p,
-                       (uint32_t*)ol.p, (double*)w.p, (double*)fin.p, used, &tot,
-                       stream) != hipSuccess)
+  S.st = std::make_unique<DevBuf>(num * 4ull);
+  S.off = std::make_unique<DevBuf>((num + 1ull) * 8);
+  S.fin = std::make_unique<DevBuf>(num * 8ull);
+  S.il = std::make_unique<DevBuf>(used * 4);
+  S.ol = std::make_unique<DevBuf>(used * 4);
+  S.w = std::make_unique<DevBuf>(used * 8);
+  if (!S.st->p || !S.off->p || !S.fin->p || !S.il->p || !S.ol->p || !S.w->p) return FST_OOM;
+  if (S.E->compact_paths(o.v, num, S.fail ? (const int32_t*)S.fail->p : nullptr,
+                         (int32_t*)S.st->p, (uint64_t*)S.off->p, (uint32_t*)S.il->p,
+                         (uint32_t*)S.ol->p, (double*)S.w->p, (double*)S.fin->p, used, &S.tot,
+                         stream) != hipSuccess)
     return FST_OOM;
-  if (tot > used) return FST_OOM;  // an engine bug (the gather wrote nothing past `used`)
-  if (t_prof) t_prof->lap(4);
+  if (S.tot > used) return FST_OOM;  // an engine bug (the gather wrote nothing past `used`)
+  return FST_OK;
+}
+
+bool alloc_result(FstBatchResult* out, uint32_t num, uint64_t tot) {
   out->num_strings = num;
   out->total_arcs = tot;
   out->status = (int32_t*)pin_alloc(std::max<size_t>(num, 1) * 4);
@@ -625,19 +652,147 @@ FstError download_batch_result(DeviceEngine::Lease& E, const DevOut& o, uint32_t
   out->ilabels = (uint32_t*)pin_alloc(std::max<uint64_t>(tot, 1) * 4);
   out->olabels = (uint32_t*)pin_alloc(std::max<uint64_t>(tot, 1) * 4);
   out->weights = (double*)pin_alloc(std::max<uint64_t>(tot, 1) * 8);
-  if (!out->status || !out->path_offsets || !out->final_weights || !out->ilabels ||
-      !out->olabels || !out->weights)
-    return FST_OOM;
-  // pinned destinations: asynchronous DMAs on the call's stream, one synchronisation
+  return out->status && out->path_offsets && out->final_weights && out->ilabels &&
+         out->olabels && out->weights;
+}
+
+// D2H of a compacted shard into the (pinned) result: asynchronous DMAs on the shard's
+// stream, one synchronisation, then its path offsets moved by the shard's first arc.
+FstError shard_download(Shard& S, FstBatchResult* out, uint64_t arc_base) {
+  const uint32_t num = S.s1 - S.s0;
+  const hipStream_t stream = S.E.stream();
   const auto d2h = [stream](void* dst, const void* src, size_t b) {
     return b == 0 || hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, stream) == hipSuccess;
   };
-  if (!(d2h(out->status, st.p, num * 4ull) && d2h(out->final_weights, fin.p, num * 8ull) &&
-        d2h(out->path_offsets, off.p, (num + 1ull) * 8) && d2h(out->ilabels, il.p, tot * 4) &&
-        d2h(out->olabels, ol.p, tot * 4) && d2h(out->weights, w.p, tot * 8)) ||
+  if (!(d2h(out->status + S.s0, S.st->p, num * 4ull) &&
+        d2h(out->final_weights + S.s0, S.fin->p, num * 8ull) &&
+        d2h(out->path_offsets + S.s0, S.off->p, num * 8ull) &&
+        d2h(out->ilabels + arc_base, S.il->p, S.tot * 4) &&
+        d2h(out->olabels + arc_base, S.ol->p, S.tot * 4) &&
+        d2h(out->weights + arc_base, S.w->p, S.tot * 8)) ||
       hipStreamSynchronize(stream) != hipSuccess)
     return FST_OOM;
+  if (arc_base)
+    for (uint32_t i = S.s0; i < S.s1; ++i) out->path_offsets[i] += arc_base;
+  return FST_OK;
+}
+
+// Runs `compute` (the engines: it fills S.keep and, for pipelines, S.fail) over the shards
+// of a batch and gathers their results into *out.  Shards are contiguous string ranges of
+// equal estimated cost (cost[i]: the work estimate of string i); shard j runs on
+// devices[j % devices.size()] on a host thread of its own (inline for one shard).
+FstError run_sharded(const std::vector<int>& devices, uint32_t nsh, uint32_t num,
+                     const std::vector<double>& cost,
+                     const std::function<FstError(Shard&)>& compute, FstBatchResult* out) {
+  nsh = std::max<uint32_t>(1, std::min<uint32_t>(nsh, std::max<uint32_t>(num, 1)));
+  std::vector<Shard> sh(nsh);
+  if (nsh == 1) {
+    sh[0].dev = devices[0];
+    sh[0].s0 = 0;
+    sh[0].s1 = num;
+  } else {
+    double total = 0;
+    for (double c : cost) total += c;
+    uint32_t i = 0;
+    double acc = 0;
+    for (uint32_t j = 0; j < nsh; ++j) {
+      sh[j].dev = devices[j % devices.size()];
+      sh[j].s0 = i;
+      const double goal = total * (j + 1) / nsh;
+      // leave at least one string for each later shard
+      while (i < num && (j + 1 == nsh || (acc + cost[i] <= goal && num - i > nsh - 1 - j))) {
+        acc += cost[i];
+        ++i;
+      }
+      if (j + 1 < nsh && i == sh[j].s0 && i < num) acc += cost[i++];  // never empty
+      sh[j].s1 = (j + 1 == nsh) ? num : i;
+    }
+  }
+  if (std::getenv("FSTAMD_SHARD_LOG"))  // tests: the shard plan
+    for (uint32_t j = 0; j < nsh; ++j) {
+      double c = 0;
+      for (uint32_t i = sh[j].s0; i < sh[j].s1 && i < cost.size(); ++i) c += cost[i];
+      std::fprintf(stderr, "[libfst_amd shard] %u dev %d strings %u..%u cost %.6g\n", j,
+                   sh[j].dev, sh[j].s0, sh[j].s1, c);
+    }
+  auto phase1 = [&](Shard& S) {
+    if (hipSetDevice(S.dev) != hipSuccess) {
+      S.err = FST_INVALID_ARG;
+      return;
+    }
+    S.E = DeviceEngine::acquire(S.dev);
+    if (!S.E) {
+      S.err = FST_INVALID_ARG;
+      return;
+    }
+    S.err = compute(S);
+    S.stats = t_last_stats;
+    if (S.err == FST_OK && !S.keep) S.err = FST_OOM;
+    if (S.err == FST_OK) S.err = shard_compact(S);
+    // no lease is held between the phases: a shard waiting for an engine never holds one
+    // (two sharded calls on one device cannot deadlock)
+    S.E = DeviceEngine::Lease();
+  };
+  auto phase2 = [&](Shard& S, uint64_t base) {
+    if (hipSetDevice(S.dev) != hipSuccess) {
+      S.err = FST_OOM;
+      return;
+    }
+    S.E = DeviceEngine::acquire(S.dev);
+    S.err = S.E ? shard_download(S, out, base) : FST_OOM;
+    S.E = DeviceEngine::Lease();
+  };
+  auto each = [&](const std::function<void(uint32_t)>& f) {
+    if (nsh == 1) return f(0);
+    std::vector<std::thread> th;
+    for (uint32_t j = 1; j < nsh; ++j) th.emplace_back(f, j);
+    f(0);
+    for (auto& x : th) x.join();
+  };
+  each([&](uint32_t j) { phase1(sh[j]); });
+  uint64_t tot = 0;
+  for (Shard& S : sh) {
+    if (S.err != FST_OK) return S.err;
+    tot += S.tot;
+  }
+  if (t_prof) t_prof->lap(4);
+  if (!alloc_result(out, num, tot)) return FST_OOM;
+  std::vector<uint64_t> base(nsh, 0);
+  for (uint32_t j = 1; j < nsh; ++j) base[j] = base[j - 1] + sh[j - 1].tot;
+  each([&](uint32_t j) { phase2(sh[j], base[j]); });
+  out->path_offsets[num] = tot;
+  LaunchStats agg = sh[0].stats;  // the slowest shard's kernel time, launches summed
+  for (uint32_t j = 1; j < nsh; ++j) {
+    agg.kernel_ms = std::max(agg.kernel_ms, sh[j].stats.kernel_ms);
+    agg.launches += sh[j].stats.launches;
+  }
+  t_last_stats = agg;
+  for (Shard& S : sh)
+    if (S.err != FST_OK) return S.err;
   if (t_prof) t_prof->lap(3);
+  return FST_OK;
+}
+
+// The devices and shard count of a host batch call (FstBatchOptions, fst_batch.h).
+FstError batch_devices(const FstBatchOptions* opts, std::vector<int>* devices, uint32_t* nsh) {
+  devices->clear();
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return FST_INVALID_ARG;
+  if (opts && (opts->flags & FST_BATCH_DEVICES) && opts->device_mask) {
+    for (int d = 0; d < 64; ++d)
+      if (opts->device_mask >> d & 1) {
+        if (d >= count) return FST_INVALID_ARG;
+        devices->push_back(d);
+      }
+  } else {
+    int dev = opts ? opts->device : -1;
+    if (dev < 0) dev = current_device();
+    if (dev < 0 || dev >= count) return FST_INVALID_ARG;
+    devices->push_back(dev);
+  }
+  *nsh = (uint32_t)devices->size();
+  if (opts && (opts->flags & FST_BATCH_DEVICES) && opts->num_shards)
+    *nsh = std::max<uint32_t>(opts->num_shards, 1);
   return FST_OK;
 }
 
@@ -726,13 +881,16 @@ struct ChainCall {
   std::vector<Arc> arcs;
   double fin = 0;
   LaunchStats stats;
+  // combiner hand-off (under ChainCombiner::mu): each waiter sleeps on its own condition,
+  // so a finished batch wakes exactly its callers and one queued caller to lead next
+  std::condition_variable cv;
   bool done = false;
+  bool lead = false;
 };
 
 struct ChainCombiner {
   std::mutex mu;
-  std::condition_variable cv;
-  std::vector<ChainCall*> q;
+  std::deque<ChainCall*> q;
   int leaders = 0;
 };
 constexpr int kChainLeaders = 2;
@@ -803,23 +961,34 @@ FstError coalesced_chain_call(int dev, ChainCall* c) {
   ChainCombiner& C = chain_combiner(dev);
   std::unique_lock<std::mutex> lk(C.mu);
   C.q.push_back(c);
-  while (!c->done) {
-    if (C.leaders < kChainLeaders && !C.q.empty()) {
-      ++C.leaders;
-      const size_t take = std::min(C.q.size(), kChainMaxBatch);
-      std::vector<ChainCall*> batch(C.q.begin(), C.q.begin() + take);
-      C.q.erase(C.q.begin(), C.q.begin() + take);
-      lk.unlock();
-      run_chain_calls(dev, batch);
-      lk.lock();
-      for (ChainCall* x : batch) x->done = true;
-      --C.leaders;
-      C.cv.notify_all();
-    } else {
-      C.cv.wait(lk);
-    }
+  if (C.leaders < kChainLeaders) {
+    c->lead = true;
+    ++C.leaders;
   }
-  return c->err;
+  for (;;) {
+    c->cv.wait(lk, [c] { return c->done || c->lead; });
+    if (c->done) return c->err;
+    // leading: take the queue (this call is in it: a leader is picked from the queue)
+    c->lead = false;
+    const size_t take = std::min(C.q.size(), kChainMaxBatch);
+    std::vector<ChainCall*> batch(C.q.begin(), C.q.begin() + take);
+    C.q.erase(C.q.begin(), C.q.begin() + take);
+    lk.unlock();
+    run_chain_calls(dev, batch);
+    lk.lock();
+    for (ChainCall* x : batch) {
+      x->done = true;
+      if (x != c) x->cv.notify_one();
+    }
+    // hand the lead to the oldest queued caller, or retire
+    if (!C.q.empty()) {
+      C.q.front()->lead = true;
+      C.q.front()->cv.notify_one();
+    } else {
+      --C.leaders;
+    }
+    if (c->done) return c->err;
+  }
 }
 
 }  // namespace
@@ -835,31 +1004,31 @@ extern "C" {
 // ---- MutableFst lifecycle -----------------------------------------------------------
 
 FstMutableHandle fst_mutable_new(void) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>());
 }
 
 FstMutableHandle fst_mutable_clone(FstMutableHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m) return kInvalid;
   return g_mut.insert(std::make_shared<MutableFst>(*m));
 }
 
 void fst_mutable_free(FstMutableHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   g_mut.remove(handle);
 }
 
 uint32_t fst_mutable_add_state(FstMutableHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m) return FST_NO_STATE;
   return m->add_state();
 }
 
 FstError fst_mutable_set_start(FstMutableHandle handle, uint32_t state) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m) return FST_INVALID_ARG;
   if (state >= m->num_states()) return FST_INVALID_STATE;
@@ -868,7 +1037,7 @@ FstError fst_mutable_set_start(FstMutableHandle handle, uint32_t state) {
 }
 
 FstError fst_mutable_set_final(FstMutableHandle handle, uint32_t state, double weight) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m) return FST_INVALID_ARG;
   if (state >= m->num_states()) return FST_INVALID_STATE;
@@ -878,7 +1047,7 @@ FstError fst_mutable_set_final(FstMutableHandle handle, uint32_t state, double w
 
 FstError fst_mutable_add_arc(FstMutableHandle handle, uint32_t src, uint32_t ilabel,
                              uint32_t olabel, double weight, uint32_t nextstate) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m) return FST_INVALID_ARG;
   if (src >= m->num_states()) return FST_INVALID_STATE;
@@ -888,26 +1057,26 @@ FstError fst_mutable_add_arc(FstMutableHandle handle, uint32_t src, uint32_t ila
 }
 
 uint32_t fst_mutable_start(FstMutableHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   return m ? m->start() : FST_NO_STATE;
 }
 
 uint32_t fst_mutable_num_states(FstMutableHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   return m ? (uint32_t)m->num_states() : 0;
 }
 
 uint32_t fst_mutable_num_arcs(FstMutableHandle handle, uint32_t state) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m || state >= m->num_states()) return 0;
   return (uint32_t)m->num_arcs(state);
 }
 
 double fst_mutable_final_weight(FstMutableHandle handle, uint32_t state) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m || state >= m->num_states()) return w_zero();
   return m->final_weight(state);
@@ -915,7 +1084,7 @@ double fst_mutable_final_weight(FstMutableHandle handle, uint32_t state) {
 
 uint32_t fst_mutable_get_arcs(FstMutableHandle handle, uint32_t state, FstArc* buf,
                               uint32_t buf_len) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m || state >= m->num_states()) return 0;
   const auto& arcs = m->arcs(state);
@@ -931,49 +1100,49 @@ uint32_t fst_mutable_get_arcs(FstMutableHandle handle, uint32_t state, FstArc* b
 FstHandle fst_freeze(FstMutableHandle mutable_handle) {
   std::shared_ptr<MutableFst> snap;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     auto m = g_mut.get(mutable_handle);
     if (!m) return kInvalid;
     snap = std::make_shared<MutableFst>(*m);  // clone under the lock (c-api.zig:507-517)
   }
   auto f = FrozenFst::from_mutable(*snap, kWeightTropical);
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
 void fst_free(FstHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   g_fst.remove(handle);
 }
 
 uint32_t fst_start(FstHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   return f ? f->start() : FST_NO_STATE;
 }
 
 uint32_t fst_num_states(FstHandle handle) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   return f ? f->num_states() : 0;
 }
 
 uint32_t fst_num_arcs(FstHandle handle, uint32_t state) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   if (!f || state >= f->num_states()) return 0;
   return f->num_arcs(state);
 }
 
 double fst_final_weight(FstHandle handle, uint32_t state) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   if (!f || state >= f->num_states()) return w_zero();
   return f->final_weight(state);
 }
 
 uint32_t fst_get_arcs(FstHandle handle, uint32_t state, FstArc* buf, uint32_t buf_len) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   if (!f || state >= f->num_states()) return 0;
   const StateEntry& e = f->states()[state];
@@ -992,7 +1161,7 @@ FstHandle fst_load(const char* path) {
   if (!path) return kInvalid;
   auto f = FrozenFst::load_file(path, kWeightTropical, nullptr);  // binary.zig:16-36
   if (!f) return kInvalid;
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -1015,7 +1184,7 @@ FstMutableHandle fst_read_text(const char* path) {
   if (!ok) return kInvalid;
   auto m = std::make_shared<MutableFst>();
   if (!MutableFst::read_text(data.data(), data.size(), m.get())) return kInvalid;
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::move(m));
 }
 
@@ -1023,7 +1192,7 @@ FstError fst_save(FstHandle handle, const char* path) {
   if (!path) return FST_INVALID_ARG;
   std::shared_ptr<FrozenFst> f;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     f = g_fst.get(handle);
     if (!f) return FST_INVALID_ARG;
   }
@@ -1045,7 +1214,7 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
   std::shared_ptr<MutableFst> a;
   std::shared_ptr<FrozenFst> b;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     auto ha = g_mut.get(a_handle);
     if (!ha) {
       trace("sp_invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
@@ -1104,7 +1273,7 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
   }
   trace("sp_ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
         result.total_arcs(), us(), t_last_stats.kernel_ms);
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
@@ -1118,7 +1287,7 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
   std::shared_ptr<MutableFst> a;
   std::shared_ptr<FrozenFst> b;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     auto ha = g_mut.get(a_handle);
     if (!ha) {
       trace("invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
@@ -1187,7 +1356,7 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
                  (us() - t_gpu) / 1e3);
   trace("ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
         result.total_arcs(), us(), st.kernel_ms);
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
@@ -1200,7 +1369,7 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
   };
   std::unique_ptr<HostGraph> m;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     auto h = g_mut.get(handle);
     if (!h) return kInvalid;
     m = std::make_unique<HostGraph>(*h);  // snapshot, flattened to CSR under the lock
@@ -1243,21 +1412,21 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
                    "[libfst_amd host] fst_shortest_path call: snapshot %.2f upload %.2f engine + "
                    "result %.2f ms\n", t_snap, t_up - t_snap, ms() - t_up);
   }
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
 // ---- Strings ------------------------------------------------------------------------
 
 FstMutableHandle fst_compile_string(const uint8_t* input, uint32_t len) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   if (!input) return kInvalid;
   return g_mut.insert(
       std::make_shared<MutableFst>(MutableFst::compile_string(input, len, input, len)));
 }
 
 static int32_t print_impl(FstMutableHandle handle, uint8_t* buf, uint32_t buf_len, bool out_tape) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto m = g_mut.get(handle);
   if (!m) return -1;
   std::vector<uint8_t> s;
@@ -1277,7 +1446,7 @@ int32_t fst_print_output_string(FstMutableHandle handle, uint8_t* buf, uint32_t 
 
 void fst_teardown(void) {
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::unique_lock<std::shared_mutex> g(g_api_mu);
     g_mut.clear();
     g_fst.clear();
   }
@@ -1296,30 +1465,33 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   std::memset(out, 0, sizeof(*out));
   for (uint32_t i = 0; i < num_strings; ++i)
     if (offsets[i + 1] < offsets[i]) return FST_INVALID_ARG;
+  if (opts && (opts->flags & ~FST_BATCH_DEVICES)) return FST_INVALID_ARG;
   std::shared_ptr<FrozenFst> b;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     b = g_fst.get(b_handle);
   }
   if (!b) return FST_INVALID_ARG;
   if (!gpu_available()) return FST_INVALID_ARG;
   const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
-  int dev = opts ? opts->device : -1;
-  if (dev < 0) dev = current_device();
-  if (dev < 0 || hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  std::vector<int> devices;
+  uint32_t nsh = 1;
+  if (FstError e = batch_devices(opts, &devices, &nsh); e != FST_OK) return e;
   HostProf prof;
   t_prof = &prof;
   struct ProfScope {
     ~ProfScope() { t_prof = nullptr; }
   } prof_scope;
-  HostPaths h;
-  std::unique_ptr<DevOut> keep;
-  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
-  if (!E) return FST_INVALID_ARG;
-  FstError e = run_chain_batch_host(E, *b, labels, offsets, num_strings, n, semantics, &h, &keep);
-  if (e != FST_OK) return e;
-  if (!keep) return FST_OOM;
-  e = download_batch_result(E, *keep, num_strings, nullptr, out);
+  std::vector<double> cost(nsh > 1 ? num_strings : 0);
+  for (size_t i = 0; i < cost.size(); ++i) cost[i] = b->chain_cost(offsets[i + 1] - offsets[i]);
+  const FstError e = run_sharded(
+      devices, nsh, num_strings, cost,
+      [&](Shard& S) {
+        HostPaths h;
+        return run_chain_batch_host(S.E, *b, labels, offsets + S.s0, S.s1 - S.s0, n, semantics,
+                                    &h, &S.keep);
+      },
+      out);
   if (e != FST_OK) {
     fst_batch_result_free(out);
     return e;
@@ -1362,32 +1534,16 @@ FstError fst_device_project_output(const FstDeviceBatch* o, uint32_t num_strings
   return FST_OK;
 }
 
-FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const uint32_t* labels,
-                            const uint64_t* offsets, uint32_t num_strings, uint32_t n,
-                            const FstBatchOptions* opts, FstBatchResult* out) {
-  if (!out || !stages || num_stages == 0 || !offsets ||
-      (!labels && num_strings && offsets[num_strings] != offsets[0]))
-    return FST_INVALID_ARG;
-  std::memset(out, 0, sizeof(*out));
-  for (uint32_t i = 0; i < num_strings; ++i)
-    if (offsets[i + 1] < offsets[i]) return FST_INVALID_ARG;
-  std::vector<std::shared_ptr<FrozenFst>> fs(num_stages);
-  {
-    std::lock_guard<std::mutex> g(g_api_mu);
-    for (uint32_t k = 0; k < num_stages; ++k)
-      if (!(fs[k] = g_fst.get(stages[k]))) return FST_INVALID_ARG;
-  }
-  if (!gpu_available()) return FST_INVALID_ARG;
-  const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
-  int dev = opts && opts->device >= 0 ? opts->device : current_device();
-  if (dev < 0 || hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
-  HostProf prof;
-  t_prof = &prof;
-  struct ProfScope {
-    ~ProfScope() { t_prof = nullptr; }
-  } prof_scope;
-  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
-  if (!E) return FST_INVALID_ARG;
+namespace {
+// One shard of a pipeline: every stage on the shard's device, each stage's 1-best output tape
+// projected into the next stage's inputs on the device; S.keep = the last stage's outputs,
+// S.fail = the first failing stage per string.
+FstError run_pipeline_shard(Shard& S, const std::vector<std::shared_ptr<FrozenFst>>& fs,
+                            const uint32_t* labels, const uint64_t* offsets, uint32_t n,
+                            int semantics) {
+  DeviceEngine::Lease& E = S.E;
+  const int dev = S.dev;
+  const uint32_t num_strings = S.s1 - S.s0;
   const hipStream_t stream = E.stream();
   // stage-1 inputs
   const uint64_t total = num_strings ? offsets[num_strings] - offsets[0] : 0;
@@ -1404,34 +1560,33 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
   if (hipMemcpyAsync(off->p, rebased.data(), (num_strings + 1ull) * 8, hipMemcpyHostToDevice,
                      stream) != hipSuccess)
     return FST_OOM;
-  DevBuf fail(num_strings * 4ull);  // first failing stage's status, per string (device)
-  if (!fail.p || hipMemsetAsync(fail.p, 0, num_strings * 4ull, stream) != hipSuccess)
+  S.fail = std::make_unique<DevBuf>(num_strings * 4ull);  // first failing stage per string
+  if (!S.fail->p || hipMemsetAsync(S.fail->p, 0, num_strings * 4ull, stream) != hipSuccess)
     return FST_OOM;
   uint64_t in_total = total;
   HostPaths h;
-  std::unique_ptr<DevOut> keep;
-  prof.lap(0);
-  for (uint32_t k = 0; k < num_stages; ++k) {
+  if (t_prof) t_prof->lap(0);
+  for (size_t k = 0; k < fs.size(); ++k) {
     DeviceFst* D = fs[k]->device(dev);
     if (!D) return FST_OOM;
     ChainInput in{(const uint32_t*)lab->p, (const uint64_t*)off->p, num_strings, max_len};
-    keep.reset();
-    FstError e = run_chain_batch_dev(E, *D, in, in_total, n, semantics, &h, &keep);
+    S.keep.reset();
+    FstError e = run_chain_batch_dev(E, *D, in, in_total, n, semantics, &h, &S.keep);
     if (e != FST_OK) return e;
-    if (!keep) return FST_OOM;  // run_chain_batch_dev sets it on FST_OK; never dereference null
-    if (k + 1 == num_stages) break;
+    if (!S.keep) return FST_OOM;  // run_chain_batch_dev sets it on FST_OK
+    if (k + 1 == fs.size()) break;
     // project this stage's outputs into the next stage's inputs, on the device
     unsigned long long used = 0;
-    if (hipMemcpyAsync(&used, keep->v.cursor, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+    if (hipMemcpyAsync(&used, S.keep->v.cursor, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
       return FST_OOM;
     auto nlab = std::make_unique<DevBuf>((used + num_strings) * 4);
     auto noff = std::make_unique<DevBuf>((num_strings + 1ull) * 8);
     DevBuf pst(num_strings * 4ull);
     if (!nlab->p || !noff->p || !pst.p) return FST_OOM;
-    if (E->project_output(keep->v, num_strings, (uint32_t*)nlab->p, (uint64_t*)noff->p,
+    if (E->project_output(S.keep->v, num_strings, (uint32_t*)nlab->p, (uint64_t*)noff->p,
                           (int32_t*)pst.p, &max_len, stream) != hipSuccess ||
-        E->merge_status((int32_t*)fail.p, (const int32_t*)pst.p, num_strings, stream) !=
+        E->merge_status((int32_t*)S.fail->p, (const int32_t*)pst.p, num_strings, stream) !=
             hipSuccess)
       return FST_OOM;
     uint64_t nt = 0;  // (synchronises: pst may go back to the pool)
@@ -1442,9 +1597,47 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
     in_total = nt;
     lab = std::move(nlab);
     off = std::move(noff);
-    prof.lap(4);
+    if (t_prof) t_prof->lap(4);
   }
-  FstError e = download_batch_result(E, *keep, num_strings, (const int32_t*)fail.p, out);
+  return FST_OK;
+}
+}  // namespace
+
+FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const uint32_t* labels,
+                            const uint64_t* offsets, uint32_t num_strings, uint32_t n,
+                            const FstBatchOptions* opts, FstBatchResult* out) {
+  if (!out || !stages || num_stages == 0 || !offsets ||
+      (!labels && num_strings && offsets[num_strings] != offsets[0]))
+    return FST_INVALID_ARG;
+  std::memset(out, 0, sizeof(*out));
+  for (uint32_t i = 0; i < num_strings; ++i)
+    if (offsets[i + 1] < offsets[i]) return FST_INVALID_ARG;
+  if (opts && (opts->flags & ~FST_BATCH_DEVICES)) return FST_INVALID_ARG;
+  std::vector<std::shared_ptr<FrozenFst>> fs(num_stages);
+  {
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
+    for (uint32_t k = 0; k < num_stages; ++k)
+      if (!(fs[k] = g_fst.get(stages[k]))) return FST_INVALID_ARG;
+  }
+  if (!gpu_available()) return FST_INVALID_ARG;
+  const int semantics = opts ? (int)opts->semantics : FST_SEM_LAZY;
+  std::vector<int> devices;
+  uint32_t nsh = 1;
+  if (FstError e = batch_devices(opts, &devices, &nsh); e != FST_OK) return e;
+  HostProf prof;
+  t_prof = &prof;
+  struct ProfScope {
+    ~ProfScope() { t_prof = nullptr; }
+  } prof_scope;
+  // shards balanced by the first stage's work (later stages' inputs are not known yet)
+  std::vector<double> cost(nsh > 1 ? num_strings : 0);
+  for (size_t i = 0; i < cost.size(); ++i) cost[i] = fs[0]->chain_cost(offsets[i + 1] - offsets[i]);
+  const FstError e = run_sharded(
+      devices, nsh, num_strings, cost,
+      [&](Shard& S) {
+        return run_pipeline_shard(S, fs, labels, offsets + S.s0, n, semantics);
+      },
+      out);
   if (e != FST_OK) {
     fst_batch_result_free(out);
     return e;
@@ -1462,7 +1655,7 @@ FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_
   if (!o || !d_offsets) return FST_INVALID_ARG;
   std::shared_ptr<FrozenFst> b;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     b = g_fst.get(b_handle);
   }
   if (!b) return FST_INVALID_ARG;
@@ -1488,7 +1681,7 @@ FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_
 FstError fst_device_prepare(FstHandle b_handle, int32_t device) {
   std::shared_ptr<FrozenFst> b;
   {
-    std::lock_guard<std::mutex> g(g_api_mu);
+    std::shared_lock<std::shared_mutex> g(g_api_mu);
     b = g_fst.get(b_handle);
   }
   if (!b) return FST_INVALID_ARG;
@@ -1516,7 +1709,7 @@ FstHandle fst_device_adopt_blob(const void* d_blob, uint64_t len, int32_t device
   DeviceFst* D = DeviceFst::adopt(d_blob, *f, dev);
   if (!D) return kInvalid;
   f->adopt_device(dev, D);
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -1536,7 +1729,7 @@ FstHandle fst_batch_load_bytes(const void* bytes, uint64_t len) {
   if (h.weight_type != kWeightTropical && h.weight_type != kWeightLog) return kInvalid;
   auto f = FrozenFst::from_bytes((const uint8_t*)bytes, len, h.weight_type, nullptr);
   if (!f) return kInvalid;
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -1544,7 +1737,7 @@ FstHandle fst_batch_load(const char* path) {
   if (!path) return kInvalid;
   auto f = FrozenFst::load_file(path, FrozenFst::kAnyWeightType, nullptr);
   if (!f) return kInvalid;
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -1567,12 +1760,18 @@ FstHandle fst_load_att(const char* path, uint32_t flags) {
   if (!MutableFst::read_text(data.data(), data.size(), &m)) return kInvalid;
   if (flags & FST_ATT_SHIFT_BYTE_LABELS) m.shift_labels();
   auto f = FrozenFst::from_mutable(m, kWeightTropical);
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
+double fst_chain_cost(FstHandle b, uint64_t len) {
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
+  auto f = g_fst.get(b);
+  return f ? f->chain_cost(len) : -1.0;
+}
+
 int32_t fst_weight_type(FstHandle b) {
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(b);
   return f ? (int32_t)f->weight_type() : -1;
 }
@@ -1618,7 +1817,7 @@ FstHandle fst_bench_transducer_wt(uint32_t kind, uint32_t T, uint32_t B, uint32_
     return kInvalid;
   }
   auto f = FrozenFst::from_mutable(m, (uint8_t)weight_type);
-  std::lock_guard<std::mutex> g(g_api_mu);
+  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 

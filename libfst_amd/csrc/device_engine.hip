@@ -389,7 +389,7 @@ hipStream_t DeviceEngine::Lease::use(hipStream_t s) {
   return s;
 }
 
-DeviceEngine::Lease::~Lease() {
+void DeviceEngine::Lease::release() {
   if (!e_) return;
   if (used_) {
     (void)hipSetDevice(e_->dev_);
@@ -402,6 +402,8 @@ DeviceEngine::Lease::~Lease() {
     P.idle.push_back(e_);
   }
   P.cv.notify_one();
+  e_ = nullptr;
+  used_ = false;
 }
 
 DeviceEngine::DeviceEngine(int dev) : dev_(dev) {

@@ -219,8 +219,17 @@ class DeviceEngine {
    public:
     Lease() = default;
     Lease(Lease&& o) noexcept : e_(o.e_), s_(o.s_), used_(o.used_) { o.e_ = nullptr; }
-    Lease& operator=(Lease&&) = delete;
-    ~Lease();
+    Lease& operator=(Lease&& o) noexcept {
+      if (this != &o) {
+        release();
+        e_ = o.e_;
+        s_ = o.s_;
+        used_ = o.used_;
+        o.e_ = nullptr;
+      }
+      return *this;
+    }
+    ~Lease() { release(); }
     DeviceEngine* operator->() const { return e_; }
     DeviceEngine& operator*() const { return *e_; }
     explicit operator bool() const { return e_ != nullptr; }
@@ -230,6 +239,7 @@ class DeviceEngine {
    private:
     friend class DeviceEngine;
     explicit Lease(DeviceEngine* e) : e_(e) {}
+    void release();  // records the end event, returns the engine to its pool
     hipStream_t own_stream() const;
     DeviceEngine* e_ = nullptr;
     hipStream_t s_ = nullptr;

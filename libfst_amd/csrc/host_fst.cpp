@@ -366,11 +366,30 @@ void FrozenFst::analyze() {
     if (!std::isfinite(w)) finite_ = false;
   }
   const StateEntry* s = states();
+  jump_fwd_ = jump_back_ = 0;
   for (uint32_t i = 0; i < h.num_states; ++i) {
     const double w = s[i].final_weight;
     if (!(w >= 0.0) || std::signbit(w)) nonneg_ = false;
     if (std::isnan(w)) nan_ = true;
+    for (uint32_t k = s[i].arc_offset; k < s[i].arc_offset + s[i].num_arcs; ++k) {
+      const uint32_t t = a[k].nextstate;
+      if (t >= i) jump_fwd_ = std::max(jump_fwd_, t - i);
+      else jump_back_ = std::max(jump_back_, i - t);
+    }
   }
+}
+
+double FrozenFst::chain_cost(uint64_t L) const {
+  // sum over input positions k = 0..L of the rhs states layer k can hold: min(NS, 1 + k J),
+  // J = the widest forward + backward jump of one arc; an rhs with input epsilons can
+  // spread a layer over every state (config 3: ~2 (T + 1) tuples per layer)
+  const double ns = std::max<uint32_t>(num_states(), 1);
+  if (has_eps_) return (double)(L + 1) * ns;
+  const double J = std::max<uint32_t>(jump_fwd_ + jump_back_, 1);
+  const double K = std::ceil((ns - 1) / J);  // layers below the cap
+  const double l1 = (double)L + 1;
+  if (l1 <= K) return l1 + J * (double)L * l1 / 2;
+  return K + J * (K - 1) * K / 2 + (l1 - K) * ns;
 }
 
 void FrozenFst::arcs_by_ilabel(StateId s, Label label, uint32_t* lo_out, uint32_t* hi_out) const {

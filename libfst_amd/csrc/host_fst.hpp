@@ -111,6 +111,11 @@ class FrozenFst {
   bool weights_nonnegative() const { return nonneg_; }
   bool has_nan_weight() const { return nan_; }
   bool arc_weights_finite() const { return finite_; }
+  // Widest forward / backward state jump of one arc, and the estimated work of one chain
+  // string of length L against this rhs (product tuples), for cost-balanced shards.
+  uint32_t jump_fwd() const { return jump_fwd_; }
+  uint32_t jump_back() const { return jump_back_; }
+  double chain_cost(uint64_t L) const;
 
   // Lazily uploaded per-device copy (blob + SoA mirror); thread safe.
   DeviceFst* device(int dev);
@@ -133,6 +138,7 @@ class FrozenFst {
   bool nonneg_ = true;
   bool nan_ = false;
   bool finite_ = true;
+  uint32_t jump_fwd_ = 0, jump_back_ = 0;
   std::mutex dev_mu_;
   std::vector<DeviceFst*> dev_;
 };

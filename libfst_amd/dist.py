@@ -23,6 +23,32 @@ def shard_range(num: int, rank: int, world: int):
     return begin, begin + base + (1 if rank < rem else 0)
 
 
+def cost_shard_range(lengths, rhs: "F.Fst", rank: int, world: int):
+    """Contiguous [begin, end) of the strings for `rank`, balanced by the library's work
+    estimate (fst_chain_cost: product tuples per string) instead of by count -- config 3's
+    lengths 11..251 differ 20x in cost.  Shards tile the batch; every shard is non-empty
+    when there are at least `world` strings."""
+    import numpy as np
+    lengths = np.asarray(lengths, dtype=np.int64)
+    num = len(lengths)
+    if num == 0:
+        return 0, 0
+    L = F.lib()
+    # one call per distinct length
+    uniq, inv = np.unique(lengths, return_inverse=True)
+    cost = np.array([L.fst_chain_cost(rhs.h, int(u)) for u in uniq])[inv]
+    cum = np.concatenate([[0.0], np.cumsum(cost)])
+
+    def cut(j):  # first string of shard j
+        if j <= 0:
+            return 0
+        if j >= world:
+            return num
+        i = int(np.searchsorted(cum, cum[-1] * j / world, side="left"))
+        return min(max(i, j if num >= world else 0), num - (world - j) if num >= world else num)
+    return cut(rank), cut(rank + 1)
+
+
 def blob_bytes(fst: "F.Fst") -> bytes:
     """The frozen blob of an Fst handle (fst_save, src/io/binary.zig:9-13)."""
     fd, path = tempfile.mkstemp(suffix=".fst")

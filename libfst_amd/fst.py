@@ -43,8 +43,24 @@ class FstBatchResult(C.Structure):
                 ("final_weights", C.POINTER(C.c_double)), ("total_arcs", C.c_uint64)]
 
 
+FST_BATCH_DEVICES = 1
+
+
 class FstBatchOptions(C.Structure):
-    _fields_ = [("device", C.c_int32), ("semantics", C.c_uint32), ("flags", C.c_uint32)]
+    _fields_ = [("device", C.c_int32), ("semantics", C.c_uint32), ("flags", C.c_uint32),
+                ("num_shards", C.c_uint32), ("device_mask", C.c_uint64)]
+
+
+def batch_options(device=-1, semantics=FST_SEM_LAZY, devices=None, shards=0) -> FstBatchOptions:
+    """FstBatchOptions; `devices` (a list of HIP ordinals) shards the batch over them
+    (FST_BATCH_DEVICES), `shards` > len(devices) runs several shards per device."""
+    if devices is None and not shards:
+        return FstBatchOptions(device, semantics, 0, 0, 0)
+    devs = list(devices) if devices is not None else [max(device, 0)]
+    mask = 0
+    for d in devs:
+        mask |= 1 << int(d)
+    return FstBatchOptions(device, semantics, FST_BATCH_DEVICES, int(shards), mask)
 
 
 class FstDeviceBatch(C.Structure):
@@ -105,6 +121,7 @@ SIGNATURES = {
     "fst_batch_load_bytes": (_u64, [C.c_void_p, C.c_uint64]),
     "fst_weight_type": (C.c_int32, [_u64]),
     "fst_read_text": (_u64, [C.c_char_p]),
+    "fst_chain_cost": (_f64, [_u64, _u64]),
     "fst_load_att": (_u64, [C.c_char_p, _u32]),
     "fst_device_project_output": (C.c_int, [C.c_void_p, _u32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(_u32), C.c_void_p]),
@@ -326,14 +343,15 @@ class BatchResult:
 
 
 def compose_frozen_shortest_path_batch(b: Fst, labels, offsets, n: int = 1,
-                                       semantics: int = FST_SEM_LAZY, device: int = -1
-                                       ) -> BatchResult:
-    """Batched 1-best of many chain acceptors against one frozen rhs (fst_batch.h)."""
+                                       semantics: int = FST_SEM_LAZY, device: int = -1,
+                                       devices=None, shards: int = 0) -> BatchResult:
+    """Batched 1-best of many chain acceptors against one frozen rhs (fst_batch.h);
+    `devices` / `shards`: cost-balanced shards over several GPUs (FST_BATCH_DEVICES)."""
     L = lib()
     labels = np.ascontiguousarray(labels, dtype=np.uint32)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     num = len(offsets) - 1
-    opts = FstBatchOptions(device, semantics, 0)
+    opts = batch_options(device, semantics, devices, shards)
     res = FstBatchResult()
     rc = L.fst_compose_frozen_shortest_path_batch(b.h, labels.ctypes.data, offsets.ctypes.data,
                                                   num, n, C.byref(opts), C.byref(res))
@@ -343,7 +361,7 @@ def compose_frozen_shortest_path_batch(b: Fst, labels, offsets, n: int = 1,
 
 
 def pipeline_batch(stages, labels, offsets, n: int = 1, semantics: int = FST_SEM_LAZY,
-                   device: int = -1) -> BatchResult:
+                   device: int = -1, devices=None, shards: int = 0) -> BatchResult:
     """Multi-stage batch (tagger -> verbalizer ...): each stage's 1-best output tape is the
     next stage's input, projected on the device (fst_pipeline_batch)."""
     L = lib()
@@ -351,7 +369,7 @@ def pipeline_batch(stages, labels, offsets, n: int = 1, semantics: int = FST_SEM
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     num = len(offsets) - 1
     hs = (C.c_uint64 * len(stages))(*[s.h for s in stages])
-    opts = FstBatchOptions(device, semantics, 0)
+    opts = batch_options(device, semantics, devices, shards)
     res = FstBatchResult()
     rc = L.fst_pipeline_batch(hs, len(stages), labels.ctypes.data, offsets.ctypes.data, num, n,
                               C.byref(opts), C.byref(res))

@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--len", type=int, default=0, help="fixed string length (probes)")
     ap.add_argument("--cpu-n", type=int, default=0,
                     help="also time the CPU port on the first N strings (--cpu-threads)")
-    ap.add_argument("--cpu-threads", type=int, default=len(os.sched_getaffinity(0)))
+    ap.add_argument("--cpu-threads", type=int, default=bench.nproc())
     a = ap.parse_args()
     # a launch at T = 65,536 runs for minutes without returning: say so every 30 s (gpurun
     # takes 3 silent minutes for a hang)

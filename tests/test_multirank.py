@@ -77,3 +77,63 @@ def test_shard_range_tiles(num, world):
     assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
     sizes = [e - b for b, e in parts]
     assert max(sizes) - min(sizes) <= 1
+
+
+def _shard_worker(rank, world, port, q):
+    """Each rank takes its cost-balanced shard (libfst_amd.dist.cost_shard_range, the
+    library's own work estimate), composes it (on a CPU rank: the oracle, the checker;
+    tests/test_gpu_multidevice.py runs the same with the GPU engines) and all ranks
+    gather the per-string results in input order."""
+    import sys
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    sys.path.insert(0, here)
+    import libfst_amd as F
+    from libfst_amd import dist as D
+    import oracle_ffi as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rhs = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, 32, 12)
+        blob = D.blob_bytes(rhs)
+        lens = np.random.default_rng(0x5EED).integers(11, 252, 30)
+        b, e = D.cost_shard_range(lens, rhs, rank, world)
+        mine = lens[b:e]
+        offs = np.concatenate([[0], np.cumsum(mine)]).astype(np.uint64)
+        r = O.batch_run(blob, np.ones(int(mine.sum()), np.uint32), offs, 0, 1)
+        part = (b, e, [(int(r.status[i]), r.olabels[int(r.offsets[i]):int(r.offsets[i + 1])].tolist(),
+                        float(r.finals[i])) for i in range(e - b)])
+        parts = [None] * world
+        dist.all_gather_object(parts, part)
+        if rank == 0:
+            parts.sort(key=lambda p: p[0])
+            got = [x for p in parts for x in p[2]]
+            offs_all = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+            ra = O.batch_run(blob, np.ones(int(lens.sum()), np.uint32), offs_all, 0, 1)
+            exp = [(int(ra.status[i]), ra.olabels[int(ra.offsets[i]):int(ra.offsets[i + 1])].tolist(),
+                    float(ra.finals[i])) for i in range(len(lens))]
+            costs = [sum(F.lib().fst_chain_cost(rhs.h, int(L)) for L in lens[p[0]:p[1]]) for p in parts]
+            q.put((got == exp, [(p[0], p[1]) for p in parts], max(costs) / max(min(costs), 1)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_compose_cost_shards_and_gather(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    same, spans, imbalance = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert same, "gathered shards differ from the whole-batch answer"
+    assert spans[0][0] == 0 and spans[-1][1] == 30
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+    assert imbalance < 1.6
