@@ -444,6 +444,10 @@ static hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyK
   return hipStreamSynchronize(stream);
 }
 
+__global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_count,
+                                    const int32_t* status, int32_t code, uint32_t* list,
+                                    uint32_t* count);
+
 static hipError_t finish_stats(hipEvent_t e0, hipEvent_t e1, LaunchStats* stats) {
   if (!stats) return hipSuccess;
   HIP_TRY(hipEventSynchronize(e1));
@@ -723,13 +727,58 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   if (use_dense) {
     if (stats) {
       stats->engine = 5;
+      stats->launches = 1;
       HIP_TRY(hipEventRecord(ev0_, stream));
     }
-    bool ran = false;
-    HIP_TRY(run_lazy_dense(rhs, in, n, out, stream, &ran));
+    // Small lattices first, whatever the rhs size: the replay with the wave's tables in
+    // LDS at 128, then 256 tuples.  A WeText-scale tagger has 0.4 M states but ~140 tuples
+    // per utterance, while the dense replay's per-wave index is (L + 1) * NS * 2 tuples (1.6
+    // GB per wave there): it takes only what outgrows the LDS.  An rhs whose strings nearly
+    // all outgrow it (config 3's lattices of millions of tuples) skips the LDS pass from
+    // then on (DeviceFst::skip_tiny_lazy); FSTAMD_LAZY_TINY=0 skips it always.
+    const bool small = !force_dense && !(lte && std::strcmp(lte, "0") == 0) &&
+                       rhs.skip_tiny_lazy.load(std::memory_order_relaxed) == 0 &&
+                       in.num_strings > 0;
+    const uint32_t* todo = nullptr;  // the dense replay's strings (nullptr: all)
+    uint32_t todo_n = in.num_strings;
+    if (small) {
+      const uint32_t num = in.num_strings;
+      uint32_t* la = (uint32_t*)scratch(kItems, (size_t)num * 4);
+      uint32_t* lb = (uint32_t*)scratch(kItems2, (size_t)num * 4);
+      if (!la || !lb) return hipErrorOutOfMemory;
+      unsigned int* c = counter + 40;  // [40] items (LDS 128), [41] |la|, [42] items (256), [43] |lb|
+      HIP_TRY(hipMemsetAsync(c, 0, 16, stream));
+      uint32_t g = 0;
+      HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 1, nullptr, num, c, &g));
+      if (stats) stats->grid = g;
+      collect_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(out.status, num, kPathOverflow,
+                                                                  la, c + 1);
+      HIP_TRY(hipGetLastError());
+      uint32_t cnt[2] = {0, 0};
+      HIP_TRY(hipMemcpyAsync(&cnt[0], c + 1, 4, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (cnt[0] > 0) {
+        HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 2, la, cnt[0], c + 2, &g));
+        collect_list_kernel<<<(cnt[0] + 255) / 256, 256, 0, stream>>>(la, c + 1, out.status,
+                                                                      kPathOverflow, lb, c + 3);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&cnt[1], c + 3, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (stats) stats->launches += 1;
+      }
+      if (num >= 64 && (uint64_t)cnt[0] * 10 > (uint64_t)num * 9)
+        rhs.skip_tiny_lazy.store(1, std::memory_order_relaxed);
+      todo = lb;
+      todo_n = cnt[1];
+    }
+    bool ran = true;
+    if (todo_n > 0) {
+      HIP_TRY(run_lazy_dense(rhs, in, n, out, stream, &ran, todo, todo ? todo_n : 0));
+      if (stats) stats->launches += 1;
+    }
     if (stats && !ran) stats->engine = 3;  // too large for the dense engine: rounds only
     if (!std::getenv("FSTAMD_DENSE_NOFALLBACK"))  // debug: leave UNSUPPORTED strings
-      HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !ran, true));
+      HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !ran && !small, true));
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));
       HIP_TRY(finish_stats(ev0_, ev1_, stats));
@@ -837,26 +886,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   }
   uint32_t grid0 = 0;
   const bool tiny_first = tiny_ok;
-  if (tiny_first) {  // LDS tables (kernels/lazy_wave.hpp kLzTiny*): stamps from 1 per launch
-    static const int occ = [] {
-      int o = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &o, (const void*)lazy_wave_kernel<false, true>, 64, 0) != hipSuccess)
-        o = 1;
-      return std::max(o, 1);
-    }();
-    LazyWs ws{};
-    ws.hcap = kLzTinyH;
-    ws.ncap = kLzTinyN;
-    ws.qcap = kLzTinyQ;
-    ws.gcap = 0;
-    ws.stamp_base = 0;
-    ws.max_pops = kLzTinyQ + 1;
-    ws.wd_ticks = watchdog_ticks();
-    grid0 = (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(in.num_strings, 1u));
-    lazy_wave_kernel<false, true><<<grid0, 64, 0, stream>>>(rhs.view, in, none, n, counter,
-                                                            nullptr, in.num_strings, ws, out);
-    HIP_TRY(hipGetLastError());
+  if (tiny_first) {  // LDS tables (kernels/lazy_wave.hpp, 128 tuples)
+    HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 1, nullptr, in.num_strings, counter, &grid0));
   } else {
     HIP_TRY(launch_lazy(want, nullptr, in.num_strings, counter, &grid0));
   }
@@ -1022,6 +1053,47 @@ hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput
   return hipSuccess;
 }
 
+namespace {
+template <int T>
+int lazy_tiny_per_cu() {  // resident LDS-replay waves per CU, asked of the runtime once
+  static const int occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &o, (const void*)lazy_wave_kernel<false, T>, 64, 0) != hipSuccess)
+      o = 1;
+    return std::max(o, 1);
+  }();
+  return occ;
+}
+}  // namespace
+
+hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                       const BatchOutDev& out, hipStream_t stream, int tier,
+                                       const uint32_t* items, uint32_t num_items,
+                                       unsigned int* ctr, uint32_t* grid_out) {
+  LazyWs ws{};
+  ws.hcap = lz_tiny_h(tier);
+  ws.ncap = lz_tiny_n(tier);
+  ws.qcap = lz_tiny_q(tier);
+  ws.gcap = 0;
+  ws.stamp_base = 0;  // stamps from 1 per launch: the LDS table starts zeroed
+  ws.max_pops = ws.qcap + 1;
+  ws.wd_ticks = watchdog_ticks();
+  const int occ = tier == 1 ? lazy_tiny_per_cu<1>() : lazy_tiny_per_cu<2>();
+  const uint32_t grid =
+      (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(num_items, 1u));
+  GraphInput none{};
+  if (tier == 1)
+    lazy_wave_kernel<false, 1><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
+                                                         num_items, ws, out);
+  else
+    lazy_wave_kernel<false, 2><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
+                                                         num_items, ws, out);
+  HIP_TRY(hipGetLastError());
+  if (grid_out) *grid_out = grid;
+  return hipSuccess;
+}
+
 // Dense lazy replay (kernels/lazy_dense.hpp).  Per wave: rec 16 B + back arc 4 B + id map
 // 4 B per dense tuple, the bitmap, and a future list of a quarter of the dense tuples
 // (compacted when full; a string that still overflows goes to the rounds engine).  The
@@ -1031,8 +1103,31 @@ hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput
 constexpr size_t kLdMaxDynLds = 150 * 1024;
 
 hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
-                                        const BatchOutDev& out, hipStream_t stream, bool* ran) {
+                                        const BatchOutDev& out, hipStream_t stream, bool* ran,
+                                        const uint32_t* subset_dev, uint32_t subset_n) {
   *ran = false;
+  // the strings this call takes: all of `in`, or a device list (what the LDS replay of
+  // small lattices handed on); with a list the plan is sized by its own longest string
+  std::vector<uint32_t> subset;
+  std::vector<uint64_t> off;
+  uint32_t num = in.num_strings, max_len = in.max_len;
+  if (subset_dev) {
+    subset.resize(subset_n);
+    off.resize((size_t)in.num_strings + 1);
+    if (subset_n)
+      HIP_TRY(hipMemcpyAsync(subset.data(), subset_dev, subset_n * 4ull, hipMemcpyDeviceToHost,
+                             stream));
+    HIP_TRY(hipMemcpyAsync(off.data(), in.offsets, off.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    num = subset_n;
+    max_len = 0;
+    for (uint32_t i : subset)
+      max_len = std::max<uint32_t>(max_len, (uint32_t)std::min<uint64_t>(off[i + 1] - off[i], in.max_len));
+    if (num == 0) {
+      *ran = true;
+      return hipSuccess;
+    }
+  }
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [33] is ours
   if (!ctr) return hipErrorOutOfMemory;
   // One launch plan: the per-wave dense state is sized by the longest string it takes.
@@ -1097,7 +1192,7 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
     return true;
   };
   Plan whole;
-  if (!make_plan(in.max_len, in.num_strings, whole)) return hipSuccess;
+  if (!make_plan(max_len, num, whole)) return hipSuccess;
   // Length buckets.  When the dense state of the longest string caps the waves in flight
   // (budget / per-wave < max_waves: large rhs, e.g. config 3 at T >= 4096), the strings are
   // launched in buckets of similar length, each sized by its own longest string, so short
@@ -1108,28 +1203,33 @@ hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& 
   // Only for batches that refill every bucket's waves many times over: with fewer strings
   // a bucket runs one string per wave and its tail dominates (T = 4096, 4096 strings:
   // 14.1 s bucketed vs 9.2 s in one launch).
-  uint32_t nb = (whole.grid < max_waves && in.num_strings >= 8ull * max_waves) ? 4u : 1u;
+  uint32_t nb = (whole.grid < max_waves && num >= 8ull * max_waves) ? 4u : 1u;
   if (const char* be = std::getenv("FSTAMD_DENSE_BUCKETS"))
     nb = (uint32_t)std::max(1, std::atoi(be));
-  nb = std::min<uint32_t>(nb, std::max<uint32_t>(in.num_strings, 1));
+  nb = std::min<uint32_t>(nb, std::max<uint32_t>(num, 1));
   // Longest first inside a launch: work items are taken in order, so when a launch has
   // more strings than waves the long strings start first and the short ones fill the
   // tail (list scheduling, longest processing time first).  FSTAMD_DENSE_LPT=0 turns it
   // off (measurements).
-  bool lpt = in.num_strings > whole.grid;
+  bool lpt = num > whole.grid;
   if (const char* le = std::getenv("FSTAMD_DENSE_LPT")) lpt = lpt && std::atoi(le) != 0;
-  if (nb > 1 || lpt) {
-    std::vector<uint64_t> off((size_t)in.num_strings + 1);
-    HIP_TRY(hipMemcpyAsync(off.data(), in.offsets, off.size() * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    order.resize(in.num_strings);
-    for (uint32_t i = 0; i < in.num_strings; ++i) order[i] = i;
+  if (nb > 1 || lpt || subset_dev) {
+    if (!subset_dev) {
+      off.resize((size_t)in.num_strings + 1);
+      HIP_TRY(hipMemcpyAsync(off.data(), in.offsets, off.size() * 8, hipMemcpyDeviceToHost,
+                             stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      order.resize(in.num_strings);
+      for (uint32_t i = 0; i < in.num_strings; ++i) order[i] = i;
+    } else {
+      order = subset;
+    }
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
       return off[a + 1] - off[a] < off[b + 1] - off[b];
     });
     for (uint32_t b = 0; b < nb; ++b) {  // equal-count buckets of the sorted lengths
-      const uint32_t lo = (uint32_t)((uint64_t)in.num_strings * b / nb);
-      const uint32_t hi = (uint32_t)((uint64_t)in.num_strings * (b + 1) / nb);
+      const uint32_t lo = (uint32_t)((uint64_t)num * b / nb);
+      const uint32_t hi = (uint32_t)((uint64_t)num * (b + 1) / nb);
       if (hi == lo) continue;
       const uint32_t last = order[hi - 1];
       // a length above max_len (caller's bound) keeps the whole plan: the kernel passes
@@ -1279,8 +1379,13 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
   // small by the product bound; not for the exact heap replay (negative weights), whose
   // heap lives in HBM.  FSTAMD_BFS_TINY=0 turns it off (A/B runs, tests).
   const char* te = std::getenv("FSTAMD_BFS_TINY");
+  // Small lattices by the product bound always fit; beyond it the tiny tiers are tried too
+  // (a WeText-scale rhs: 0.4 M states, ~140 tuples per utterance) unless an earlier batch
+  // on this rhs handed nearly every string on (DeviceFst::skip_tiny_eager).
   const bool tiny = !replay && !(te && std::strcmp(te, "0") == 0) &&
-                    (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
+                    ((uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384 ||
+                     rhs.skip_tiny_eager.load(std::memory_order_relaxed) == 0);
+  const uint32_t count0 = count;
   // tier -2: the 128-tuple tiny size, tier -1: the 256-tuple one, then the HBM tiers
   for (int tier = tiny ? -2 : 0; count > 0; ++tier) {
     const TinyCaps tc = tiny_caps(tier == -2 ? 1 : 2);
@@ -1353,6 +1458,10 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     HIP_TRY(hipMemcpyAsync(cnt, cnt + 2, 4, hipMemcpyDeviceToDevice, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::swap(list, list2);
+    // the 128-tuple tier handed on nearly every string: skip the tiny tiers on this rhs
+    if (tier == -2 && count0 >= 64 && (uint64_t)count * 10 > (uint64_t)count0 * 9 &&
+        (uint64_t)(in.max_len + 1) * rhs.view.num_states > 16384)
+      rhs.skip_tiny_eager.store(1, std::memory_order_relaxed);
   }
   return hipSuccess;
 }

@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
@@ -97,6 +98,9 @@ struct DeviceFst {
   // within a same-ilabel run, candidate order = olabel order (relax's (id, il, ol) rule
   // then reduces to (id, candidate))
   bool lazy_pull_ok = false;
+  // Routing hints learnt from earlier batches on this rhs: a small-lattice (LDS) tier that
+  // handed on nearly every string is skipped next time (config 3's lattices never fit).
+  mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};
   RevView rev{};
   void* rev_bufs[4] = {nullptr, nullptr, nullptr, nullptr};
 
@@ -314,8 +318,17 @@ class DeviceEngine {
   // composeShortestPath as a dense-indexed exact replay (kernels/lazy_dense.hpp), for rhs
   // with input epsilons; strings it does not take end UNSUPPORTED / OVERFLOW for
   // run_bfs_chain.  *ran = false: it took none (the lattice exceeds its dense index).
+  // subset_dev (device, subset_n entries): only those strings (nullptr: all).
   hipError_t run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
-                            const BatchOutDev& out, hipStream_t stream, bool* ran);
+                            const BatchOutDev& out, hipStream_t stream, bool* ran,
+                            const uint32_t* subset_dev = nullptr, uint32_t subset_n = 0);
+  // composeShortestPath with the wave's tables in LDS (kernels/lazy_wave.hpp, kTiny = tier:
+  // 1 = 128 tuples, 2 = 256) over a device list of strings (nullptr: all); strings whose
+  // lattice outgrows it end OVERFLOW.
+  hipError_t run_lazy_tiny(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                           const BatchOutDev& out, hipStream_t stream, int tier,
+                           const uint32_t* items, uint32_t num_items, unsigned int* ctr,
+                           uint32_t* grid_out);
   void* scratch(size_t idx, size_t bytes);
   int dev_;
   int num_cus_ = 0;

@@ -276,10 +276,16 @@ struct LazyLds {
 // per utterance on average) keep the wave's hash, node arrays and heap in LDS instead of
 // HBM slabs, ~15 KB, 10 waves per CU; strings that outgrow it report OVERFLOW and are rerun
 // in HBM.  The host sets ws.{hcap, ncap, qcap, max_pops} to these caps for that launch.
-constexpr uint32_t kLzTinyN = 128, kLzTinyH = 256, kLzTinyQ = 384;
+// Two LDS sizes: kTiny 1 = 128 tuples (~15 KB, 10 waves per CU), 2 = 256 tuples (~29 KB,
+// 5 per CU) for what outgrows the first (a WeText-scale tagger's utterances: ~140 tuples on
+// average, ~300 at most, libfst_amd/wetext_standin.py).
+constexpr uint32_t lz_tiny_n(int t) { return t == 1 ? 128u : 256u; }
+constexpr uint32_t lz_tiny_h(int t) { return 2 * lz_tiny_n(t); }
+constexpr uint32_t lz_tiny_q(int t) { return 3 * lz_tiny_n(t); }
+constexpr uint32_t kLzTinyN = lz_tiny_n(1), kLzTinyH = lz_tiny_h(1), kLzTinyQ = lz_tiny_q(1);
 
-template <bool kGraph, bool kTiny = false>
-__global__ void __launch_bounds__(64, kTiny ? 3 : FSTAMD_REPLAY_WAVES)
+template <bool kGraph, int kTiny = 0>
+__global__ void __launch_bounds__(64, kTiny == 1 ? 3 : kTiny == 2 ? 1 : FSTAMD_REPLAY_WAVES)
 lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, uint32_t num_items, LazyWs ws,
                  BatchOutDev out) {
@@ -295,14 +301,15 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
   double* qd;
   uint32_t* qid;
   uint4* tbl = nullptr;
-  if constexpr (kTiny) {
-    __shared__ uint4 t_hslot[kLzTinyH];
-    __shared__ unsigned long long t_nkey[kLzTinyN];
-    __shared__ double t_ndist[kLzTinyN];
-    __shared__ uint4 t_nback[kLzTinyN];
-    __shared__ double t_nbw[kLzTinyN];
-    __shared__ double t_qd[kLzTinyQ];
-    __shared__ uint32_t t_qid[kLzTinyQ];
+  if constexpr (kTiny != 0) {
+    constexpr uint32_t TN = lz_tiny_n(kTiny), TH = lz_tiny_h(kTiny), TQ = lz_tiny_q(kTiny);
+    __shared__ uint4 t_hslot[TH];
+    __shared__ unsigned long long t_nkey[TN];
+    __shared__ double t_ndist[TN];
+    __shared__ uint4 t_nback[TN];
+    __shared__ double t_nbw[TN];
+    __shared__ double t_qd[TQ];
+    __shared__ uint32_t t_qid[TQ];
     hslot = t_hslot;
     nkey = t_nkey;
     ndist = t_ndist;
@@ -311,7 +318,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
     qd = t_qd;
     qid = t_qid;
     // stamps start at ws.stamp_base + 1 > 0: a zeroed table is empty for every string
-    for (uint32_t i = lane; i < kLzTinyH; i += 64) t_hslot[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = lane; i < TH; i += 64) t_hslot[i] = make_uint4(0u, 0u, 0u, 0u);
     wave_fence();
   } else {
     hslot = ws.hslot + w * ws.hcap;

@@ -9,6 +9,7 @@ strings, is bench.py's).  One JSON line per config; CPU time of the oracle resta
      T=1,024 here (4,096 strings); the full config (T=65,536, ~17M tuples per string) is
      measured on 512 strings by scripts/config3_scaling.py
   4  two-stage tagger -> verbalizer (synthetic stand-ins, libfst_amd/synthetic.py)
+  4w the same on the WeText-scale stand-in (libfst_amd/wetext_standin.py)
   5  LogWeight ambiguous chain, 256K strings, lengths 1..64, 10 % dead strings
 
 usage: python scripts/bench_configs.py [--configs 1,2,3,4,5] [--out FILE]
@@ -162,7 +163,7 @@ def config4(n=65536):
     texts = SY.utterances(rng, n)
     labels, offsets = SY.to_labels(texts)
     blobs = [D.blob_bytes(f) for f in stages]
-    threads = min(16, os.cpu_count() or 1)
+    threads = bench.nproc()
     ncpu = min(n, 16384)
     out = []
     for sem, name in ((F.FST_SEM_LAZY, "lazy (fst_compose_frozen_shortest_path)"),
@@ -186,6 +187,45 @@ def config4(n=65536):
                     "cpu_kind": f"port, {threads} threads, both stages (projection untimed)",
                     "note": "host API end to end: H2D inputs, 2 stages + device projection, "
                             "D2H results; median of 7 after 3 full-size warm-up calls"})
+    return out
+
+
+def config4w(n=65536):
+    """Config 4 on the WeText-scale stand-in (libfst_amd/wetext_standin.py: 0.43 M-state,
+    1.03 M-arc tagger with byte labels, scattered state ids, epsilon-output chains; a
+    markup-removing verbalizer): the two-stage pipeline end to end on the host API, and
+    the tagger stage alone (which engine took it), beside the CPU port on nproc threads."""
+    from libfst_amd import wetext_standin as W
+    blobs = [W.freeze_blob(W.tagger()), W.freeze_blob(W.verbalizer())]
+    stages = [F.Fst.from_bytes(b) for b in blobs]
+    labels, offsets = W.utterances(np.random.default_rng(44), n)
+    threads = bench.nproc()
+    ncpu = min(n, 16384)
+    out = []
+    for sem, name in ((F.FST_SEM_LAZY, "lazy (fst_compose_frozen_shortest_path)"),
+                      (F.FST_SEM_EAGER, "eager")):
+        for _ in range(2):
+            F.pipeline_batch(stages, labels, offsets, 1, sem)
+        walls = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            r = F.pipeline_batch(stages, labels, offsets, 1, sem)
+            walls.append(time.perf_counter() - t0)
+        wall = float(np.median(walls))
+        t0 = time.perf_counter()
+        r1 = F.compose_frozen_shortest_path_batch(stages[0], labels, offsets, 1, sem)
+        t_tag = time.perf_counter() - t0
+        st = F.last_launch_stats()
+        cpu = cpu_pipeline_rate(blobs, labels[:int(offsets[ncpu])], offsets[:ncpu + 1],
+                                0 if sem == F.FST_SEM_LAZY else 1, threads)
+        out.append({"config": "4w", "workload": f"WeText-scale stand-in tagger (0.43 M states, "
+                                                 f"1.03 M arcs) -> verbalizer, {n} utterances, {name}",
+                    "strings_per_s": n / wall, "ok": int((r.status == 0).sum()), "walls_s": walls,
+                    "tagger_only_strings_per_s": n / t_tag, "tagger_ok": int((r1.status == 0).sum()),
+                    "tagger_engine": st.engine, "tagger_kernel_ms": st.kernel_ms,
+                    "tagger_launches": st.launches,
+                    "cpu_oracle_strings_per_s": cpu, "cpu_sample": ncpu,
+                    "cpu_kind": f"port, {threads} threads (nproc), both stages (projection untimed)"})
     return out
 
 
@@ -219,7 +259,7 @@ def main():
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    fns = {"1": config1, "2": config2, "3": config3, "4": config4, "5": config5}
+    fns = {"1": config1, "2": config2, "3": config3, "4": config4, "4w": config4w, "5": config5}
     lines = []
     for c in args.configs.split(","):
         r = fns[c]()
