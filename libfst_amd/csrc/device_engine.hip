@@ -35,29 +35,32 @@ namespace fstamd {
 // Fst(W) layout) plus an SoA mirror derived from it on the device.
 // ---------------------------------------------------------------------------------
 
-__global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t na, uint2* span,
-                                    double* fin, uint32_t* il, ArcRec* rec, uint4* sspan) {
+// perm (optional): the device's state numbering (old id -> new id, DeviceFst::perm).
+__global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t na,
+                                    const uint32_t* perm, uint2* span, double* fin, uint32_t* il,
+                                    ArcRec* rec, uint4* sspan) {
   const StateEntry* se = reinterpret_cast<const StateEntry*>(blob + sizeof(Header));
   const PackedArc* pa =
       reinterpret_cast<const PackedArc*>(blob + sizeof(Header) + (size_t)ns * sizeof(StateEntry));
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
     const StateEntry e = se[i];
-    span[i] = make_uint2(e.arc_offset, e.num_arcs);
-    fin[i] = e.final_weight;
+    const uint32_t ni = perm ? perm[i] : i;
+    span[ni] = make_uint2(e.arc_offset, e.num_arcs);
+    fin[ni] = e.final_weight;
     // arcs are sorted by ilabel (fst.zig:258-265): first == last <=> one shared ilabel
     uint32_t uniq = kSpanNone;
     if (e.num_arcs > 0) {
       const uint32_t a = pa[e.arc_offset].ilabel, z = pa[e.arc_offset + e.num_arcs - 1].ilabel;
       uniq = a == z ? a : kSpanMixed;
     }
-    sspan[i] = make_uint4(e.arc_offset, e.num_arcs, uniq, 0u);
+    sspan[ni] = make_uint4(e.arc_offset, e.num_arcs, uniq, 0u);
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
     const PackedArc a = pa[i];
     il[i] = a.ilabel;
     ArcRec r;
-    r.next = a.nextstate;
+    r.next = perm ? perm[a.nextstate] : a.nextstate;
     r.olabel = a.olabel;
     r.weight = a.weight;
     rec[i] = r;
@@ -83,9 +86,73 @@ __global__ void mark_status_kernel(uint32_t num, uint32_t n_best, uint32_t rhs_s
   }
 }
 
+// Bandwidth reduction of the device's state numbering.  No kernel orders anything by rhs
+// state id: candidates go in (lattice id, arc position) order, arcs keep their span order
+// (sorted by the ORIGINAL nextstate, fst.zig:160-224), and outputs carry labels and
+// weights only -- so renumbering the device copy changes no result, only locality.  A
+// grammar whose ids are scattered (a WeText asset, or any rhs built without regard to
+// numbering) gets breadth-first ids from the start state when that shrinks the widest
+// arc jump at least 4x: the pull tiers' 320-state windows then hold its layers again
+// (metric rhs with scattered ids: P / LP instead of the hash tiers).  FSTAMD_RENUMBER=0
+// keeps the blob's ids, =1 forces BFS ids.
+static std::vector<uint32_t> bfs_renumbering(const FrozenFst& f, uint32_t* jf_out,
+                                             uint32_t* jb_out) {
+  const uint32_t ns = f.num_states();
+  const StateEntry* se = f.states();
+  const PackedArc* pa = f.arcs();
+  auto band = [&](const uint32_t* perm, uint32_t* jf, uint32_t* jb) {
+    *jf = *jb = 0;
+    for (uint32_t i = 0; i < ns; ++i) {
+      const uint32_t pi = perm ? perm[i] : i;
+      for (uint32_t a = se[i].arc_offset; a < se[i].arc_offset + se[i].num_arcs; ++a) {
+        const uint32_t t = perm ? perm[pa[a].nextstate] : pa[a].nextstate;
+        if (t >= pi) *jf = std::max(*jf, t - pi);
+        else *jb = std::max(*jb, pi - t);
+      }
+    }
+  };
+  band(nullptr, jf_out, jb_out);
+  const char* e = std::getenv("FSTAMD_RENUMBER");
+  const int mode = e ? std::atoi(e) : -1;  // -1 auto, 0 off, 1 force
+  const uint64_t id_band = (uint64_t)*jf_out + *jb_out;
+  if (mode == 0 || ns < 2 || f.start() >= ns || (mode < 0 && id_band <= 64)) return {};
+  std::vector<uint32_t> perm(ns, 0xFFFFFFFFu), queue;
+  queue.reserve(ns);
+  uint32_t next = 0;
+  auto visit = [&](uint32_t s) {
+    if (perm[s] == 0xFFFFFFFFu) {
+      perm[s] = next++;
+      queue.push_back(s);
+    }
+  };
+  visit(f.start());
+  for (size_t q = 0; q < queue.size(); ++q) {
+    const uint32_t s = queue[q];
+    for (uint32_t a = se[s].arc_offset; a < se[s].arc_offset + se[s].num_arcs; ++a)
+      visit(pa[a].nextstate);
+  }
+  for (uint32_t s = 0; s < ns; ++s) visit(s);  // unreachable states last, in id order
+  uint32_t jf = 0, jb = 0;
+  band(perm.data(), &jf, &jb);
+  if (mode < 0 && ((uint64_t)jf + jb) * 4 > id_band) return {};
+  *jf_out = jf;
+  *jb_out = jb;
+  return perm;
+}
+
 static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   const Header& h = f.header();
   const uint32_t ns = h.num_states, na = h.num_arcs;
+  uint32_t jf = 0, jb = 0;
+  d->perm = bfs_renumbering(f, &jf, &jb);
+  uint32_t* d_perm = nullptr;
+  if (!d->perm.empty() &&
+      (hipMalloc(&d_perm, ns * 4ull) != hipSuccess ||
+       hipMemcpy(d_perm, d->perm.data(), ns * 4ull, hipMemcpyHostToDevice) != hipSuccess)) {
+    if (d_perm) (void)hipFree(d_perm);
+    DeviceFst::destroy(d);
+    return nullptr;
+  }
   bool ok = hipMalloc(&d->span, sizeof(uint2) * std::max<uint32_t>(ns, 1)) == hipSuccess &&
             hipMalloc(&d->final_w, sizeof(double) * std::max<uint32_t>(ns, 1)) == hipSuccess &&
             hipMalloc(&d->il, sizeof(uint32_t) * std::max<uint32_t>(na, 1)) == hipSuccess &&
@@ -99,27 +166,23 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   const uint32_t work = std::max(ns, na);
   const uint32_t blocks = std::min<uint32_t>((work + 255) / 256, 4096);
   if (work > 0) {
-    build_mirror_kernel<<<std::max<uint32_t>(blocks, 1), 256>>>(d->blob, ns, na, d->span,
+    build_mirror_kernel<<<std::max<uint32_t>(blocks, 1), 256>>>(d->blob, ns, na, d_perm, d->span,
                                                                 d->final_w, d->il, d->rec,
                                                                 d->sspan);
   }
-  if (hipStreamSynchronize(nullptr) != hipSuccess) {  // the null stream only: other calls'
-    DeviceFst::destroy(d);                            // engines run on their own streams
+  const bool synced = hipStreamSynchronize(nullptr) == hipSuccess;  // the null stream only:
+  if (d_perm) (void)hipFree(d_perm);          // other calls' engines run on their own streams
+  if (!synced) {
+    DeviceFst::destroy(d);
     return nullptr;
   }
-  uint32_t max_span = 0, jb = 0, jf = 0;
+  uint32_t max_span = 0;
   const StateEntry* se = f.states();
-  const PackedArc* pa = f.arcs();
-  for (uint32_t i = 0; i < ns; ++i) {
-    max_span = std::max(max_span, se[i].num_arcs);
-    for (uint32_t a = se[i].arc_offset; a < se[i].arc_offset + se[i].num_arcs; ++a) {
-      const uint32_t t = pa[a].nextstate;
-      if (t >= i) jf = std::max(jf, t - i);
-      else jb = std::max(jb, i - t);
-    }
-  }
-  d->view = RhsView{d->span, d->final_w, d->il,       d->rec,        d->sspan,
-                    ns,      na,         h.start_state, max_span,   jb, jf};
+  for (uint32_t i = 0; i < ns; ++i) max_span = std::max(max_span, se[i].num_arcs);
+  const uint32_t start = (d->perm.empty() || h.start_state >= ns) ? h.start_state
+                                                                  : d->perm[h.start_state];
+  d->view = RhsView{d->span, d->final_w, d->il,       d->rec,     d->sspan,
+                    ns,      na,         start,        max_span,   jb, jf};
   d->has_eps = f.has_epsilon_input();
   d->nonneg = f.weights_nonnegative();
   d->nan = f.has_nan_weight();
@@ -770,6 +833,33 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
         rhs.skip_tiny_lazy.store(1, std::memory_order_relaxed);
       todo = lb;
       todo_n = cnt[1];
+      // The LDS replays took most strings (>= 3/4): the rest are small-lattice outliers,
+      // served by the hashed replay (HBM tables sized by the lattice, x8 per retry) rather
+      // than by the dense index sized by (L + 1) * NS (a WeText-scale tagger: 1.6 GB per
+      // wave).  When they took few (large lattices), the dense replay takes the rest.
+      if (todo_n > 0 && (uint64_t)todo_n * 4 <= num) {
+        uint32_t* cur = lb;
+        unsigned int* cur_cnt = c + 3;
+        uint32_t* nxt = la;
+        unsigned int* nxt_cnt = c + 1;
+        uint64_t want = 4096;
+        for (int t = 0; t < 4 && todo_n > 0; ++t, want *= 8) {
+          HIP_TRY(hipMemsetAsync(c + 4, 0, 4, stream));  // [44] item counter
+          if (launch_lazy_hashed(rhs, in, n, out, stream, want, cur, todo_n, c + 4, &g) !=
+              hipSuccess)
+            break;  // beyond its budget: the strings stay OVERFLOW for the dense replay
+          HIP_TRY(hipMemsetAsync(nxt_cnt, 0, 4, stream));
+          collect_list_kernel<<<(todo_n + 255) / 256, 256, 0, stream>>>(
+              cur, cur_cnt, out.status, kPathOverflow, nxt, nxt_cnt);
+          HIP_TRY(hipGetLastError());
+          HIP_TRY(hipMemcpyAsync(&todo_n, nxt_cnt, 4, hipMemcpyDeviceToHost, stream));
+          HIP_TRY(hipStreamSynchronize(stream));
+          std::swap(cur, nxt);
+          std::swap(cur_cnt, nxt_cnt);
+          if (stats) stats->launches += 1;
+        }
+        todo = cur;
+      }
     }
     bool ran = true;
     if (todo_n > 0) {
@@ -827,56 +917,10 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   // Replay: the per-wave workspace is sized from max_len; strings that outgrow it
   // (OVERFLOW) are re-run from a list with 8x the capacity and fewer waves, until they
   // fit or the budget is exhausted.
-  GraphInput none{};
-  const bool debug = std::getenv("FSTAMD_LAZY_DEBUG") != nullptr;
   auto launch_lazy = [&](uint64_t want_nodes, const uint32_t* items, uint32_t num_items,
                          unsigned int* ctr, uint32_t* grid_out) -> hipError_t {
-    LazyWs ws{};
-    ws.ncap = next_pow2(want_nodes);
-    ws.hcap = ws.ncap * 2;
-    ws.qcap = ws.ncap * 4;
-    ws.gcap = 64;
-    const uint64_t per_wave = (uint64_t)ws.hcap * sizeof(uint4) +
-                              (uint64_t)ws.ncap * (8 + 8 + 16 + 8) +
-                              (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
-    if (per_wave > (24ull << 30)) return hipErrorOutOfMemory;
-    uint32_t grid =
-        (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 4 * FSTAMD_REPLAY_WAVES, num_items);
-    // latency-bound: as many waves in flight as the SIMDs hold (4/SIMD), within 20 GB of
-    // the 288 GB HBM
-    const uint64_t budget = 20ull << 30;
-    while (grid > 1 && (uint64_t)grid * per_wave > budget) grid /= 2;
-    grid = std::max<uint32_t>(grid, 1);
-    ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
-    ws.nkey = (unsigned long long*)scratch(kLzNkey, (size_t)grid * ws.ncap * 8);
-    ws.ndist = (double*)scratch(kLzNdist, (size_t)grid * ws.ncap * 8);
-    ws.nback = (uint4*)scratch(kLzNback, (size_t)grid * ws.ncap * 16);
-    ws.nbw = (double*)scratch(kLzNbw, (size_t)grid * ws.ncap * 8);
-    ws.qd = (double*)scratch(kLzQd, (size_t)grid * ws.qcap * 8);
-    ws.qid = (uint32_t*)scratch(kLzQid, (size_t)grid * ws.qcap * 4);
-    ws.gscratch = (uint4*)scratch(kLzG, (size_t)grid * ws.gcap * sizeof(uint4));
-    if (!ws.hslot || !ws.nkey || !ws.ndist || !ws.nback || !ws.nbw || !ws.qd || !ws.qid ||
-        !ws.gscratch)
-      return hipErrorOutOfMemory;
-    // Stamps: zero the table whenever it was (re)allocated or the stamp would wrap.
-    if (lazy_hash_bytes_ != (size_t)grid * ws.hcap * sizeof(uint4) ||
-        (uint64_t)lazy_stamp_ + num_items + 2 > 0xFFFFFFF0ull) {
-      HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
-      lazy_hash_bytes_ = (size_t)grid * ws.hcap * sizeof(uint4);
-      lazy_stamp_ = 0;
-    }
-    ws.stamp_base = lazy_stamp_;
-    ws.max_pops = ws.qcap + 1;
-    lazy_stamp_ += num_items + 1;
-    ws.wd_ticks = watchdog_ticks();
-    ws.dbg = debug ? (uint32_t*)scratch(kDebug, (size_t)grid * 8 * 4) : nullptr;
-    if (ws.dbg) HIP_TRY(hipMemsetAsync(ws.dbg, 0, (size_t)grid * 8 * 4, stream));
-    lazy_wave_kernel<false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
-                                                     num_items, ws, out);
-    HIP_TRY(hipGetLastError());
-    if (debug) dump_debug(ws.dbg, grid, stream);
-    *grid_out = grid;
-    return hipSuccess;
+    return launch_lazy_hashed(rhs, in, n, out, stream, want_nodes, items, num_items, ctr,
+                              grid_out);
   };
   uint64_t want = std::max<uint64_t>(4096, (uint64_t)256 * (in.max_len + 1));
   if (stats) {
@@ -1050,6 +1094,63 @@ hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput
                  grid, sum[4], sum[0] / 100.0 / it, sum[1] / 100.0 / it, sum[2] / 100.0 / it,
                  sum[3] / 100.0 / it, sum[5] / it);
   }
+  return hipSuccess;
+}
+
+// The hashed exact replay (kernels/lazy_wave.hpp) with per-wave HBM tables sized for
+// want_nodes tuples, over a device list of strings (nullptr: all of `in`).
+hipError_t DeviceEngine::launch_lazy_hashed(const DeviceFst& rhs, const ChainInput& in,
+                                            uint32_t n, const BatchOutDev& out,
+                                            hipStream_t stream, uint64_t want_nodes,
+                                            const uint32_t* items, uint32_t num_items,
+                                            unsigned int* ctr, uint32_t* grid_out) {
+  GraphInput none{};
+  const bool debug = std::getenv("FSTAMD_LAZY_DEBUG") != nullptr;
+  LazyWs ws{};
+  ws.ncap = next_pow2(want_nodes);
+  ws.hcap = ws.ncap * 2;
+  ws.qcap = ws.ncap * 4;
+  ws.gcap = 64;
+  const uint64_t per_wave = (uint64_t)ws.hcap * sizeof(uint4) +
+                            (uint64_t)ws.ncap * (8 + 8 + 16 + 8) +
+                            (uint64_t)ws.qcap * (8 + 4) + (uint64_t)ws.gcap * sizeof(uint4);
+  if (per_wave > (24ull << 30)) return hipErrorOutOfMemory;
+  uint32_t grid =
+      (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * 4 * FSTAMD_REPLAY_WAVES, num_items);
+  // latency-bound: as many waves in flight as the SIMDs hold (4/SIMD), within 20 GB of
+  // the 288 GB HBM
+  const uint64_t budget = 20ull << 30;
+  while (grid > 1 && (uint64_t)grid * per_wave > budget) grid /= 2;
+  grid = std::max<uint32_t>(grid, 1);
+  ws.hslot = (uint4*)scratch(kLzHash, (size_t)grid * ws.hcap * sizeof(uint4));
+  ws.nkey = (unsigned long long*)scratch(kLzNkey, (size_t)grid * ws.ncap * 8);
+  ws.ndist = (double*)scratch(kLzNdist, (size_t)grid * ws.ncap * 8);
+  ws.nback = (uint4*)scratch(kLzNback, (size_t)grid * ws.ncap * 16);
+  ws.nbw = (double*)scratch(kLzNbw, (size_t)grid * ws.ncap * 8);
+  ws.qd = (double*)scratch(kLzQd, (size_t)grid * ws.qcap * 8);
+  ws.qid = (uint32_t*)scratch(kLzQid, (size_t)grid * ws.qcap * 4);
+  ws.gscratch = (uint4*)scratch(kLzG, (size_t)grid * ws.gcap * sizeof(uint4));
+  if (!ws.hslot || !ws.nkey || !ws.ndist || !ws.nback || !ws.nbw || !ws.qd || !ws.qid ||
+      !ws.gscratch)
+    return hipErrorOutOfMemory;
+  // Stamps: zero the table whenever it was (re)allocated or the stamp would wrap.
+  if (lazy_hash_bytes_ != (size_t)grid * ws.hcap * sizeof(uint4) ||
+      (uint64_t)lazy_stamp_ + num_items + 2 > 0xFFFFFFF0ull) {
+    HIP_TRY(hipMemsetAsync(ws.hslot, 0, (size_t)grid * ws.hcap * sizeof(uint4), stream));
+    lazy_hash_bytes_ = (size_t)grid * ws.hcap * sizeof(uint4);
+    lazy_stamp_ = 0;
+  }
+  ws.stamp_base = lazy_stamp_;
+  ws.max_pops = ws.qcap + 1;
+  lazy_stamp_ += num_items + 1;
+  ws.wd_ticks = watchdog_ticks();
+  ws.dbg = debug ? (uint32_t*)scratch(kDebug, (size_t)grid * 8 * 4) : nullptr;
+  if (ws.dbg) HIP_TRY(hipMemsetAsync(ws.dbg, 0, (size_t)grid * 8 * 4, stream));
+  lazy_wave_kernel<false><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
+                                                   num_items, ws, out);
+  HIP_TRY(hipGetLastError());
+  if (debug) dump_debug(ws.dbg, grid, stream);
+  *grid_out = grid;
   return hipSuccess;
 }
 

@@ -103,6 +103,10 @@ struct DeviceFst {
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};
   RevView rev{};
   void* rev_bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+  // The device's state numbering (old id -> new id; empty = the blob's own ids): a
+  // breadth-first renumbering of an rhs with scattered ids (device_engine.hip
+  // bfs_renumbering).  Every device view (RhsView, RevView) uses it; results do not.
+  std::vector<uint32_t> perm;
 
   static DeviceFst* create(const FrozenFst& f, int dev);
   // Blob already in device memory on `dev` (e.g. after an RCCL broadcast).
@@ -325,6 +329,10 @@ class DeviceEngine {
   // composeShortestPath with the wave's tables in LDS (kernels/lazy_wave.hpp, kTiny = tier:
   // 1 = 128 tuples, 2 = 256) over a device list of strings (nullptr: all); strings whose
   // lattice outgrows it end OVERFLOW.
+  hipError_t launch_lazy_hashed(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                const BatchOutDev& out, hipStream_t stream, uint64_t want_nodes,
+                                const uint32_t* items, uint32_t num_items, unsigned int* ctr,
+                                uint32_t* grid_out);
   hipError_t run_lazy_tiny(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                            const BatchOutDev& out, hipStream_t stream, int tier,
                            const uint32_t* items, uint32_t num_items, unsigned int* ctr,

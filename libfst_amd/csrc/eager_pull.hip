@@ -69,6 +69,9 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   if (ns == 0 || ns >= (1u << 27)) return true;  // records hold 8 * state < 2^30
   const StateEntry* se = f.states();
   const PackedArc* pa = f.arcs();
+  // the device numbering (DeviceFst::perm): sources and targets by their device ids
+  const std::vector<uint32_t>& perm = d->perm;
+  auto pid = [&](uint32_t s) { return perm.empty() ? s : perm[s]; };
 
   // j of every arc: its position in the source's run of equal ilabels (spans are sorted
   // by ilabel, fst.zig:258-265).  A run longer than 8 does not fit the key's 3 bits.
@@ -81,8 +84,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       if (a > se[s].arc_offset && pa[a].ilabel != pa[a - 1].ilabel) run = a;
       if (a - run >= 8) return true;
       jpos[a] = (uint8_t)(a - run);
-      src[a] = s;
-      ++indeg[pa[a].nextstate];
+      src[a] = pid(s);
+      ++indeg[pid(pa[a].nextstate)];
     }
   }
   // lazy pull: within a same-ilabel run, arcs into one target must come in olabel order
@@ -99,7 +102,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   std::vector<uint32_t> ioff(ns + 1, 0);
   for (uint32_t t = 0; t < ns; ++t) ioff[t + 1] = ioff[t] + indeg[t];
   std::vector<uint32_t> in(na), fill(ioff.begin(), ioff.end() - 1);
-  for (uint32_t a = 0; a < na; ++a) in[fill[pa[a].nextstate]++] = a;
+  for (uint32_t a = 0; a < na; ++a) in[fill[pid(pa[a].nextstate)]++] = a;
   for (uint32_t t = 0; t < ns; ++t)
     std::sort(in.begin() + ioff[t], in.begin() + ioff[t + 1], [&](uint32_t x, uint32_t y) {
       if (pa[x].ilabel != pa[y].ilabel) return pa[x].ilabel < pa[y].ilabel;

@@ -229,6 +229,42 @@ def config4w(n=65536):
     return out
 
 
+def config2p(n=262144, L=64):
+    """The metric workload on a non-banded rhs: the ambiguous chain T=4096 with its state ids
+    scattered by a random permutation (same language, same answers up to state names).  The
+    pull tier P needs a banded rhs (a layer's targets within 320 consecutive ids), so this
+    measures the tiers that take such grammars (A0 -> A hash -> B -> C -> general)."""
+    from libfst_amd import wetext_standin as W
+    f = O.gen("ambiguous", 4096, 12)
+    src, il, ol, w, dst = [], [], [], [], []
+    for s_, al in enumerate(f.arcs):
+        for (a, b, ww, d) in al:
+            src.append(s_); il.append(a); ol.append(b); w.append(ww); dst.append(d)
+    ns = f.num_states
+    perm = np.random.default_rng(7).permutation(ns).astype(np.uint32)
+    fin = np.empty(ns)
+    fin[perm] = np.asarray(f.finals)
+    g = W.Graph(ns, int(perm[f.start]), fin, perm[np.asarray(src, np.uint32)],
+                np.asarray(il, np.uint32), np.asarray(ol, np.uint32), np.asarray(w),
+                perm[np.asarray(dst, np.uint32)])
+    blob = W.freeze_blob(g)
+    rhs = D.adopt_on_device(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to("cuda:0"), 0)
+    out = []
+    for sem, name in ((F.FST_SEM_EAGER, "eager"), (F.FST_SEM_LAZY, "lazy")):
+        b = bench.DeviceBatch(np.full(n, L, np.int64), lambda t: torch.ones(t, dtype=torch.int32),
+                              "cuda:0")
+        wall, kms = timed_device(b, rhs, sem, steps=3)
+        st = F.last_launch_stats()
+        assert np.all(b.status.cpu().numpy() == 0)
+        checked = bench.check_sample(b, blob, sem, n=64, threads=bench.nproc())
+        out.append({"config": "2p", "workload": f"ambiguous T=4096 B=12 with scattered state ids, "
+                                                  f"{n} x 1^64, {name}",
+                    "strings_per_s": n / wall, "kernel_ms": kms, "engine": st.engine,
+                    "launches": st.launches, "checked_vs_oracle": checked})
+        del b
+    return out
+
+
 def config5(n=262144):
     fz = F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, 4096, 12, weight_type=1)
     assert fz.weight_type == 1
@@ -259,7 +295,7 @@ def main():
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    fns = {"1": config1, "2": config2, "3": config3, "4": config4, "4w": config4w, "5": config5}
+    fns = {"1": config1, "2": config2, "3": config3, "4": config4, "4w": config4w, "2p": config2p, "5": config5}
     lines = []
     for c in args.configs.split(","):
         r = fns[c]()

@@ -288,3 +288,32 @@ def test_single_call_chain_route(rhs_kind):
             a = near.arcs[0][0]
             near.arcs[0] = [(a[0], a[1] + 1, a[2], a[3])]
             compare_single(near, blob)
+
+
+# ---------------------------------------------------------------------------------------
+# an rhs with scattered state ids (device renumbering, device_engine.hip bfs_renumbering)
+# ---------------------------------------------------------------------------------------
+
+def scattered(f: O.Fst, seed) -> O.Fst:
+    perm = np.random.default_rng(seed).permutation(f.num_states)
+    g = O.Fst(start=int(perm[f.start]), finals=[0.0] * f.num_states,
+              arcs=[[] for _ in range(f.num_states)])
+    for s, fw in enumerate(f.finals):
+        g.finals[int(perm[s])] = fw
+    for s, al in enumerate(f.arcs):
+        g.arcs[int(perm[s])] = [(a, b, w, int(perm[d])) for (a, b, w, d) in al]
+    return g
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_scattered_state_ids_take_the_pull_tiers(sem):
+    blob = O.freeze(scattered(O.gen("ambiguous", 2048, 12), 5))
+    rhs = load_blob(blob)
+    rng = np.random.default_rng(12)
+    seqs = [[1] * int(L) for L in rng.integers(0, 97, 200)]
+    check(blob, *csr(seqs), sem, rhs=rhs)
+    # renumbered breadth-first on the device, the banded pull tiers take every string
+    labels, offsets = csr([[1] * 64] * 64)
+    F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+    st = F.last_launch_stats()
+    assert st.engine == (7 if sem == LAZY else 0)
