@@ -860,6 +860,11 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
         }
         todo = cur;
       }
+      if (std::getenv("FSTAMD_ROUTE_LOG"))
+        std::fprintf(stderr,
+                     "[libfst_amd route] lazy: %u strings, LDS-128 handed on %u, LDS-256 %u, "
+                     "to the dense replay %u\n",
+                     num, cnt[0], cnt[1], todo_n);
     }
     bool ran = true;
     if (todo_n > 0) {
