@@ -16,6 +16,7 @@
 #include "host_fst.hpp"
 #include "kernels/eager_bfs.hpp"
 #include "kernels/lazy_dense.hpp"
+#include "kernels/lazy_band.hpp"
 #include "kernels/lazy_layered.hpp"
 #include "kernels/eager_layered.hpp"
 #include "kernels/eager_wave.hpp"
@@ -310,6 +311,11 @@ enum Scratch : size_t {
   kLdLeaf,
   kLdFut,
   kLdItems,
+  kLbWin,
+  kLbBack,
+  kLbIdr,
+  kLbFut,
+  kLbItems,
   kBfsHeap,
   kPullBack,
   kItems4,
@@ -868,6 +874,27 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     }
     bool ran = true;
     if (todo_n > 0) {
+      // the band replay first (rhs whose arcs all go forward: config 3), the dense replay
+      // for what it hands on
+      bool band = false;
+      HIP_TRY(run_lazy_band(rhs, in, n, out, stream, &band, todo, todo ? todo_n : 0));
+      if (band) {
+        if (stats) stats->launches += 1;
+        uint32_t* la = (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4);
+        if (!la) return hipErrorOutOfMemory;
+        unsigned int* c = counter + 46;  // [46] |la|
+        HIP_TRY(hipMemsetAsync(c, 0, 4, stream));
+        collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
+            out.status, in.num_strings, kPathOverflow, la, c);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&todo_n, c, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        todo = la;
+        if (std::getenv("FSTAMD_ROUTE_LOG"))
+          std::fprintf(stderr, "[libfst_amd route] lazy: band replay handed on %u\n", todo_n);
+      }
+    }
+    if (todo_n > 0) {
       HIP_TRY(run_lazy_dense(rhs, in, n, out, stream, &ran, todo, todo ? todo_n : 0));
       if (stats) stats->launches += 1;
     }
@@ -1200,13 +1227,205 @@ hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& i
   return hipSuccess;
 }
 
+constexpr size_t kLdMaxDynLds = 150 * 1024;
+
+// Band replay (kernels/lazy_band.hpp): the dense replay over a sliding window of rhs
+// states, for an rhs whose arcs all go forward (jump_back == 0).  Per wave: the window's
+// records (16 B x ws x (L + 1) x 2), 8 B per possible id, a 16K-id ring, a 64K-entry
+// future list.  Strings it hands on end OVERFLOW / UNSUPPORTED (the dense replay, then
+// the rounds engine, take them).  subset_dev: the strings to run (nullptr: all).
+hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                                       const BatchOutDev& out, hipStream_t stream, bool* ran,
+                                       const uint32_t* subset_dev, uint32_t subset_n) {
+  *ran = false;
+  if (rhs.view.jump_back != 0 || std::getenv("FSTAMD_NO_BAND")) return hipSuccess;
+  unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [36] is ours
+  if (!ctr) return hipErrorOutOfMemory;
+  // the strings and their lengths on the host (plans, buckets, longest first)
+  std::vector<uint64_t> off((size_t)in.num_strings + 1);
+  HIP_TRY(hipMemcpyAsync(off.data(), in.offsets, off.size() * 8, hipMemcpyDeviceToHost, stream));
+  std::vector<uint32_t> order;
+  if (subset_dev) {
+    order.resize(subset_n);
+    if (subset_n)
+      HIP_TRY(hipMemcpyAsync(order.data(), subset_dev, subset_n * 4ull, hipMemcpyDeviceToHost,
+                             stream));
+  } else {
+    order.resize(in.num_strings);
+    for (uint32_t i = 0; i < in.num_strings; ++i) order[i] = i;
+  }
+  HIP_TRY(hipStreamSynchronize(stream));
+  const uint32_t num = (uint32_t)order.size();
+  if (num == 0) {
+    *ran = true;
+    return hipSuccess;
+  }
+  auto len = [&](uint32_t i) { return (uint32_t)std::min<uint64_t>(off[i + 1] - off[i], in.max_len); };
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len(a) < len(b); });
+  const uint32_t NS = rhs.view.num_states;
+  constexpr uint32_t kRing = 16384, kFcap = 65536;
+  struct Plan {
+    uint32_t lcap, wstates, grid, first, count;
+    uint64_t wn, idcap;
+    size_t lds;
+  };
+  // every launch's memory from one budget: free HBM (pooled blocks released first) less a
+  // 24 GB reserve, 90 % of it; the plans are made one at a time per device (EnginePool::heavy)
+  std::unique_lock<std::mutex> heavy(engine_pool(dev_).heavy);
+  device_pool_release(dev_);
+  uint64_t budget = 128ull << 30;
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
+      uint64_t avail = fr;
+      for (size_t b : {kLbWin, kLbBack, kLbIdr, kLbFut}) avail += sizes_[b];
+      const uint64_t reserve = 24ull << 30;
+      budget = avail > 2 * reserve ? (avail - reserve) / 10 * 9 : avail / 2;
+    }
+    if (const char* be = std::getenv("FSTAMD_DENSE_BUDGET_GB"))
+      budget = (uint64_t)std::max(1, std::atoi(be)) << 30;
+  }
+  const uint32_t max_waves = (uint32_t)num_cus_ * 16;
+  const char* ge = std::getenv("FSTAMD_DENSE_GRID");
+  auto make_plan = [&](uint32_t max_len, uint32_t count, Plan& p) -> bool {
+    p.lcap = std::max<uint32_t>(max_len, 1);
+    if (p.lcap > 4095) return false;
+    uint32_t w = 64;
+    const uint64_t want = 2ull * (p.lcap + 1) + 2ull * (rhs.view.jump_fwd + 1);
+    while (w < want) w <<= 1;
+    p.wstates = w;
+    p.wn = (uint64_t)w * (p.lcap + 1) * 2;
+    p.idcap = (uint64_t)(p.lcap + 1) * NS * 2 + 64;
+    if (p.idcap > kLdDenseMax) return false;
+    p.lds = kRing / 8 + (size_t)w * 4 + (size_t)p.lcap * 4;
+    if (p.lds > kLdMaxDynLds) return false;
+    const uint64_t per_wave = p.wn * 16 + p.idcap * 8 + (uint64_t)kRing * 4 + (uint64_t)kFcap * 16;
+    p.grid = (uint32_t)std::min<uint64_t>(
+        {(uint64_t)max_waves, (uint64_t)count, std::max<uint64_t>(1, budget / per_wave)});
+    if (ge) p.grid = std::min<uint32_t>(p.grid, (uint32_t)std::max(1, std::atoi(ge)));
+    p.grid = std::max<uint32_t>(p.grid, 1);
+    p.count = count;
+    p.first = 0;
+    return true;
+  };
+  Plan whole;
+  if (!make_plan(len(order.back()), num, whole)) return hipSuccess;
+  // length buckets (as the dense replay) when the longest string's footprint caps the
+  // waves and the batch refills them many times; longest first inside each launch
+  uint32_t nb = (whole.grid < max_waves && num >= 8ull * max_waves) ? 4u : 1u;
+  if (const char* be = std::getenv("FSTAMD_DENSE_BUCKETS")) nb = (uint32_t)std::max(1, std::atoi(be));
+  nb = std::min<uint32_t>(nb, num);
+  std::vector<Plan> plans;
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t lo = (uint32_t)((uint64_t)num * b / nb), hi = (uint32_t)((uint64_t)num * (b + 1) / nb);
+    if (hi == lo) continue;
+    Plan p;
+    if (nb == 1 || !make_plan(len(order[hi - 1]), hi - lo, p)) p = whole;
+    p.first = lo;
+    p.count = hi - lo;
+    std::reverse(order.begin() + lo, order.begin() + hi);
+    plans.push_back(p);
+  }
+  uint64_t need_win = 0, need_back = 0;
+  uint32_t gmax = 0;
+  for (const Plan& p : plans) {
+    need_win = std::max<uint64_t>(need_win, (uint64_t)p.grid * p.wn);
+    need_back = std::max<uint64_t>(need_back, (uint64_t)p.grid * p.idcap);
+    gmax = std::max(gmax, p.grid);
+  }
+  LbWs ws{};
+  ws.win = (uint4*)scratch(kLbWin, need_win * 16);
+  ws.back = (uint2*)scratch(kLbBack, need_back * 8);
+  ws.idr = (uint32_t*)scratch(kLbIdr, (size_t)gmax * kRing * 4);
+  ws.fut = (uint4*)scratch(kLbFut, (size_t)gmax * kFcap * 16);
+  uint32_t* d_order = (uint32_t*)scratch(kLbItems, (size_t)num * 4);
+  if (!ws.win || !ws.back || !ws.idr || !ws.fut || !d_order) return hipErrorOutOfMemory;
+  if (lb_clean_ != bufs_[kLbWin] || lb_clean_bytes_ != sizes_[kLbWin]) {  // new allocation
+    HIP_TRY(hipMemsetAsync(ws.win, 0xFF, sizes_[kLbWin], stream));
+    lb_clean_ = bufs_[kLbWin];
+    lb_clean_bytes_ = sizes_[kLbWin];
+  }
+  HIP_TRY(hipMemcpyAsync(d_order, order.data(), (size_t)num * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipStreamSynchronize(stream));  // `order` is pageable and goes away
+  heavy.unlock();  // the arrays are allocated: a concurrent plan sees the HBM they took
+  const bool prof = std::getenv("FSTAMD_BFS_PROF") != nullptr;
+  ws.prof = prof ? (unsigned long long*)scratch(kDebug, (size_t)gmax * kLbProf * 8) : nullptr;
+  if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)gmax * kLbProf * 8, stream));
+  ws.ring = kRing;
+  ws.fcap = kFcap;
+  for (const Plan& p : plans) {
+    ws.lcap = p.lcap;
+    ws.ws = p.wstates;
+    ws.wn = p.wn;
+    ws.idcap = p.idcap;
+    ws.wd_ticks = watchdog_ticks();
+    ws.wd_tuple_ticks = std::getenv("FSTAMD_WATCHDOG_MS") ? 0ull : 1000ull;
+    ws.items = d_order + p.first;
+    ws.num_items = p.count;
+    HIP_TRY(hipMemsetAsync(ctr + 36, 0, 4, stream));
+    if (p.lds > 64 * 1024)
+      HIP_TRY(hipFuncSetAttribute((const void*)lazy_band_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
+    lazy_band_kernel<<<p.grid, 64, p.lds, stream>>>(rhs.view, in, n, ctr + 36, ws, out);
+    HIP_TRY(hipGetLastError());
+  }
+  *ran = true;
+  if (ws.prof) {
+    std::vector<unsigned long long> h((size_t)gmax * kLbProf);
+    HIP_TRY(hipMemcpyAsync(h.data(), ws.prof, h.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    unsigned long long sum[8] = {};
+    for (size_t w = 0; w < gmax; ++w)
+      for (int j = 0; j < 8; ++j) sum[j] += h[w * kLbProf + j];
+    const double it = (double)std::max(1ull, sum[3]);
+    std::fprintf(stderr, "[lazy-band prof] grid %u items %llu | per item: pops %.0f advances "
+                 "%.1f slides %.1f | overflows: window %llu ids %llu future %llu ring %llu\n",
+                 gmax, sum[3], sum[0] / it, sum[1] / it, sum[2] / it, sum[4], sum[5], sum[6],
+                 sum[7]);
+    if (kLbProf > 306) {
+      unsigned long long tt[6] = {};
+      for (size_t w = 0; w < gmax; ++w)
+        for (int j = 0; j < 6; ++j) tt[j] += h[w * kLbProf + 300 + j];
+      const double tp = (double)std::max(1ull, sum[0]);
+      std::fprintf(stderr, "[lazy-band prof] s_memtime ticks per pop: find %.1f pop %.1f "
+                   "cand %.1f slide %.1f relax %.1f loop %.1f\n", tt[0] / tp, tt[1] / tp,
+                   tt[2] / tp, tt[3] / tp, tt[4] / tp, tt[5] / tp);
+    }
+    int shown = 0;
+    for (size_t w = 0; w < gmax && shown < 4; ++w) {
+      const unsigned long long* q = &h[w * kLbProf];
+      if (!q[9]) continue;
+      if (kLbProf > 16 && shown == 0)
+        for (uint32_t e = 0; e < (kLbProf - 16) / 2 && q[16 + 2 * e]; ++e)
+          std::fprintf(stderr, "[lazy-band ev] tag %llu id %llu pop %llu word %016llx\n",
+                       q[16 + 2 * e] >> 56, (q[16 + 2 * e] >> 24) & 0xFFFFFFFFull,
+                       q[16 + 2 * e] & 0xFFFFFFull, q[17 + 2 * e]);
+      ++shown;
+      std::fprintf(stderr, "[lazy-band prof]   wave %zu: site %llu at pop %llu s %llu aux %llu "
+                   "slo %llu nn %llu fn %llu L %llu | %llx %llu %llu %llx\n", w, q[9], q[8], q[10], q[11],
+                   q[12], q[13], q[14], q[15], q[4], q[5], q[6], q[7]);
+    }
+  }
+  uint64_t held = 0;
+  for (size_t b : {kLbWin, kLbBack, kLbIdr, kLbFut}) held += sizes_[b];
+  if (held > (64ull << 30)) {  // give large arrays back after the call
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (size_t b : {kLbWin, kLbBack, kLbIdr, kLbFut}) {
+      (void)hipFree(bufs_[b]);
+      bufs_[b] = nullptr;
+      sizes_[b] = 0;
+    }
+    lb_clean_ = nullptr;
+  }
+  return hipSuccess;
+}
+
 // Dense lazy replay (kernels/lazy_dense.hpp).  Per wave: rec 16 B + back arc 4 B + id map
 // 4 B per dense tuple, the bitmap, and a future list of a quarter of the dense tuples
 // (compacted when full; a string that still overflows goes to the rounds engine).  The
 // dense arrays are left clean by every string, so they are initialised only when
 // (re)allocated.  *ran = false when the lattice is too large for the engine at all.
 // LDS of a gfx950 workgroup is 160 KB; the kernel's static LdLds takes ~4.6 KB of it.
-constexpr size_t kLdMaxDynLds = 150 * 1024;
 
 hipError_t DeviceEngine::run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                         const BatchOutDev& out, hipStream_t stream, bool* ran,

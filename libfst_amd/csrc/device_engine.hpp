@@ -329,6 +329,11 @@ class DeviceEngine {
   // composeShortestPath with the wave's tables in LDS (kernels/lazy_wave.hpp, kTiny = tier:
   // 1 = 128 tuples, 2 = 256) over a device list of strings (nullptr: all); strings whose
   // lattice outgrows it end OVERFLOW.
+  // The band replay (kernels/lazy_band.hpp); *ran = false when the rhs or the batch is not
+  // its (arcs going backwards, lengths > 4095); strings it hands on end OVERFLOW.
+  hipError_t run_lazy_band(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                           const BatchOutDev& out, hipStream_t stream, bool* ran,
+                           const uint32_t* subset_dev = nullptr, uint32_t subset_n = 0);
   hipError_t launch_lazy_hashed(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                 const BatchOutDev& out, hipStream_t stream, uint64_t want_nodes,
                                 const uint32_t* items, uint32_t num_items, unsigned int* ctr,
@@ -351,6 +356,8 @@ class DeviceEngine {
   size_t ld_clean_bytes_ = 0;
   void* ld_leaf_ = nullptr;
   size_t ld_leaf_bytes_ = 0;
+  void* lb_clean_ = nullptr;     // band-replay window initialised for this allocation
+  size_t lb_clean_bytes_ = 0;
 };
 
 }  // namespace fstamd

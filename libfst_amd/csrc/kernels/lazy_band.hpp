@@ -1,0 +1,705 @@
+// lazy_band.hpp -- composeShortestPath (FST_SEM_LAZY) as an exact pop-by-pop replay over a
+// sliding window of rhs states, one wavefront per string (gfx950 / CDNA4).
+//
+// Same replay as lazy_dense.hpp (the reference's pops of src/ops/compose-shortest-path.zig:
+// 26-401 one by one, heap split by distance, candidates read lane-parallel and folded in
+// relax order), for the same domain, with a per-wave footprint ~3.5x smaller so that
+// ~4x as many strings run at once.  The dense replay is latency-bound: its throughput
+// scales with the waves in flight (T = 16,384, L = 87: 20 / 40 / 78 / 142 strings/s at
+// 128 / 256 / 512 / 1,024 waves, profiles/r03/dense_waves.log), and at config 3's full size
+// its 28 B per dense tuple (0.93 GB per wave at L = 251) cap them near 250.
+//
+// What lives where (per wave):
+//   * the tuple records {dist, id | settled, back source id} (16 B) only for rhs states in
+//     a window [slo, slo + Ws): index ((s mod Ws) (L + 1) + k) 2 + f.  With every rhs arc
+//     going forward (t >= s, RhsView::jump_back == 0), a pop at state s only touches states
+//     >= s, so a tuple whose state lies below every open tuple's can never be touched or
+//     relaxed again (its record is final): the window slides up to the lowest state with an
+//     open tuple (a count per window state in LDS) when a target falls beyond its end.  On
+//     epsilon-dense lattices the open tuples span L + 2 states (a diagonal across the input
+//     positions, tests/lazy_model.py), so Ws = 2 (L + 1) rounded up to a power of two;
+//   * per id, written through on every take: {back source id, rhs arc} (8 B) -- all the
+//     backtrace (:368-400) needs;
+//   * the open-at-dcur set as a bitmap over the newest R ids (LDS): the open tuples' ids lie
+//     within ~12 L of the newest (2,997 at L = 251, T = 1,024); an id falling R behind
+//     while open, or a window overflow, hands the string to the dense replay (OVERFLOW);
+//   * id -> window index for the newest R ids (HBM ring, the newest 512 also in LDS).
+#pragma once
+
+#include "lazy_dense.hpp"
+
+namespace fstamd {
+
+// FSTAMD_BAND_TIMING (debug builds): cycles per phase into prof[300 + i]
+#ifdef FSTAMD_BAND_TIMING
+#define LB_T(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    tacc[i] += t_ - tlast; tlast = t_; } while (0)
+#else
+#define LB_T(i) do { } while (0)
+#endif
+#ifdef FSTAMD_BAND_DEBUG
+constexpr uint32_t kLbProf = 512;  // per-wave profile words (+ the debug event log)
+#else
+constexpr uint32_t kLbProf = 16;
+#endif
+
+struct LbWs {
+  uint4* win;                 // [grid * wn] window records (lazy_dense.hpp ld_rec layout)
+  uint2* back;                // [grid * idcap] per id {back source id, rhs arc}
+  uint32_t* idr;              // [grid * ring] id -> window index (id mod ring)
+  uint4* fut;                 // [grid * fcap] {dist lo, dist hi, window index, id}
+  unsigned long long wn;      // window records per wave = ws * (lcap + 1) * 2
+  unsigned long long idcap;   // ids per wave (every tuple the string can create)
+  uint32_t ws;                // window states (power of two)
+  uint32_t ring;              // ids kept (power of two, multiple of 4096)
+  uint32_t fcap, lcap;
+  unsigned long long wd_ticks, wd_tuple_ticks;
+  unsigned long long* prof;   // [grid * 16] (FSTAMD_BFS_PROF): pops, advances, slides, items,
+                              // overflows by site (4..7), the wave's last overflow (8..15)
+  const uint32_t* items;      // this launch's strings, or nullptr = all
+  uint32_t num_items;
+};
+
+__device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const ChainInput& in,
+                                                 const LbWs& ws, const BatchOutDev& out,
+                                                 uint4* R, uint2* back, uint32_t* idr, uint4* fut,
+                                                 unsigned long long* bm, uint32_t* cnt,
+                                                 const uint32_t* lab, LdLds& S,
+                                                 unsigned long long* prof, uint32_t si,
+                                                 uint32_t L) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t* Rw = (uint32_t*)R;
+  const uint32_t NS = rhs.num_states;
+  const uint32_t LC = L + 1;
+  const uint32_t WS = ws.ws, wmask = WS - 1;
+  const uint32_t RING = ws.ring, rmask = RING - 1;
+  const uint32_t nbw = RING / 64;  // bitmap words
+  // open ids stay within the newest LS = RING - 64 (an older one hands the string on):
+  // then a scan over [nn - LS, nn) never meets one physical bitmap word twice, and the
+  // ring slot of an open id is never reused
+  const uint32_t LS = RING - 64;
+  auto wix = [&](uint32_t k_, uint32_t s_) { return (s_ & wmask) * LC + k_; };  // x 2 + f
+  if (prof && lane == 0) prof[3] += 1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long wd = ws.wd_ticks + (uint64_t)LC * 2 * NS * ws.wd_tuple_ticks;
+
+  uint32_t slo = rhs.start;  // window: states [slo, slo + WS)
+  const uint32_t x0 = 2 * wix(0, rhs.start);
+  if (lane == 0) {
+    R[x0] = ld_rec(w_one(), 0u, kLdNoPrev);
+    back[0] = make_uint2(kLdNoPrev, 0u);
+    idr[0] = x0;
+    S.ring[0] = x0;
+    bm[0] = 1ull;
+    cnt[rhs.start & wmask] = 1;
+  }
+  wave_lds_sync();
+  uint32_t nn = 1, fn = 0, pops = 0, advances = 0, slides = 0;
+  uint32_t lowp = 0;                 // every open id at dcur is >= lowp
+  uint32_t cur_base = 0;             // cached word: ids [cur_base, cur_base + 64)
+  unsigned long long cur_bits = 1ull;
+  bool cache = true;
+  double dcur = w_one();
+  uint32_t best_id = kNoState;
+  double best_fw = w_zero(), best_total = w_zero();
+  int32_t fail = kPathOk;
+  uint32_t site = 0;  // INTERNAL / OVERFLOW: where it stopped (FSTAMD_BFS_PROF)
+  uint32_t dbg_s = 0, dbg_t = 0;
+#ifdef FSTAMD_BAND_DEBUG
+  uint32_t dbg_ins = 0;
+  unsigned long long dbg_w0 = 0, dbg_w1 = 0, dbg_w2 = 0, dbg_w3 = 0;
+  uint32_t nev = 0;  // events on bitmap word 1 -> prof[16 + 2 e], prof[17 + 2 e]
+  auto ev = [&](uint32_t tag, uint32_t a, unsigned long long v) {
+    if (prof && lane == 0 && nev < 240) {
+      prof[16 + 2 * nev] = ((unsigned long long)tag << 56) | ((unsigned long long)a << 24) | pops;
+      prof[17 + 2 * nev] = v;
+    }
+    ++nev;
+  };
+#endif
+  uint64_t relax = 0;
+
+  // open-at-dcur insert of lane-held ids: LDS bitmap bits, the cached word, lowp.  The
+  // bitmap is the wave's own: each word the lanes hit is OR-reduced across the wave and
+  // written by one lane (no same-word atomics from many lanes in one instruction)
+  auto bucket_insert = [&](bool ins, uint32_t id) {
+    unsigned long long pend = __ballot(ins);
+    while (pend) {
+      const uint32_t wl = lane_read(id, (uint32_t)__ffsll((long long)pend) - 1) & ~63u;
+      const bool mine = ins && (id & ~63u) == wl;
+      const unsigned long long bits = uni64(wave_or_u64(mine ? 1ull << (id & 63) : 0ull));
+      pend &= ~__ballot(mine);
+      if (lane == 0) bm[(wl & rmask) >> 6] |= bits;
+      if (wl == cur_base) cur_bits = uni64(cur_bits | bits);
+#ifdef FSTAMD_BAND_DEBUG
+      wave_lds_sync();
+      const unsigned long long chk = uni64(bm[(wl & rmask) >> 6]);
+      if (((wl & rmask) >> 6) == 1) ev(1, wl, chk);
+      if ((chk & bits) != bits && dbg_ins == 0) {
+        dbg_ins = 1;
+        dbg_w0 = bits;
+        dbg_w1 = chk;
+        dbg_w2 = __ballot(1);
+        dbg_w3 = wl;
+      }
+#endif
+    }
+    if (__ballot(ins && id < cur_base)) cache = false;
+    if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
+  };
+
+#ifdef FSTAMD_BAND_TIMING
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+  for (;;) {
+    LB_T(5);
+    // ---- the lowest open id at dcur: the cached word, else a scan of the bitmap over
+    // ids [lowp, nn) ----
+    bool have = uni(cache && cur_bits != 0ull ? 1u : 0u) != 0u;
+    if (cache && !have) lowp = max(lowp, cur_base + 64);  // the lowest word is exhausted
+    if (!have) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > wd) {
+        fail = kPathInternal;
+        site = 1;
+        break;
+      }
+      uint32_t found = kNoState;
+      unsigned long long fw = 0ull;
+      const uint32_t lo = max(lowp, nn > LS ? nn - LS : 0u);
+      for (uint32_t b0 = lo & ~63u; b0 < nn; b0 += 64 * 64) {
+        const uint32_t id0 = b0 + lane * 64;
+        const unsigned long long v = id0 < nn ? bm[(id0 & rmask) >> 6] : 0ull;
+        const unsigned long long nz = __ballot(v != 0ull);
+        if (nz) {
+          const uint32_t l = (uint32_t)__ffsll((long long)nz) - 1;
+          fw = lane_read64(v, l);
+          found = b0 + l * 64;
+          break;
+        }
+      }
+      found = uni(found);
+#ifdef FSTAMD_BAND_DEBUG
+      ev(3, found, uni64(fw));
+#endif
+      if (found != kNoState) {
+        cur_base = found;
+        cur_bits = uni64(fw);
+        lowp = found;
+        cache = true;
+        have = true;
+      } else {
+        lowp = nn;
+      }
+    }
+    if (!have) {
+      // ---- advance: smallest live distance in the future list (:159-163) ----
+      ++advances;
+      double dmin = w_zero();
+      bool any = false;
+      uint32_t wpos = 0;
+      for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        const bool v = e < fn;
+        const uint4 en = v ? fut[e] : make_uint4(0, 0, 0, 0);
+        const uint4 rv = v ? R[en.z] : make_uint4(0, 0, kLdUntouched, 0);
+        const double ed = __hiloint2double((int)en.y, (int)en.x);
+        // live: the window slot still holds this id, unsettled, at this distance
+        const bool live = v && rv.z == en.w && ld_dist(rv) == ed;
+        if (live) {
+          any = true;
+          dmin = ed < dmin ? ed : dmin;
+        }
+        const unsigned long long lm = __ballot(live);
+        if (live) fut[wpos + (uint32_t)__popcll(lm & lanemask_lt())] = en;
+        wpos += (uint32_t)__popcll(lm);
+      }
+      wave_fence();
+      fn = wpos;
+      if (!__ballot(any)) break;  // the queue is empty: done
+      dcur = uni_f64(wave_min_f64(dmin));
+      wpos = 0;
+      cache = false;
+      bool old = false;
+      for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        const bool v = e < fn;
+        const uint4 en = v ? fut[e] : make_uint4(0, 0, 0, 0);
+        const double ed = __hiloint2double((int)en.y, (int)en.x);
+        const bool hit = v && ed == dcur;
+        old |= hit && en.w + LS <= nn;  // fell out of the id ring
+        const bool keep = v && !hit;
+        const unsigned long long km = __ballot(keep);
+        if (keep) fut[wpos + (uint32_t)__popcll(km & lanemask_lt())] = en;
+        wpos += (uint32_t)__popcll(km);
+        bucket_insert(hit, en.w);
+      }
+      fn = wpos;
+      wave_fence();
+      wave_lds_sync();
+      if (__ballot(old)) {
+        fail = kPathOverflow;
+        site = 7;
+        break;
+      }
+      continue;
+    }
+
+    LB_T(0);  // finding the next id (scans, advances)
+    // ---- pop (:159-163) ----
+    const uint32_t pid = uni(cur_base + (uint32_t)__ffsll((long long)cur_bits) - 1);
+    cur_bits = uni64(cur_bits & (cur_bits - 1));
+    const uint32_t x = uni(pid + kLdRing >= nn ? S.ring[pid & (kLdRing - 1)] : idr[pid & rmask]);
+    const uint32_t sslot = (x >> 1) / LC;
+    const uint32_t k = (x >> 1) - sslot * LC;
+    const uint32_t s = slo + ((sslot - slo) & wmask);
+#ifdef FSTAMD_BAND_DEBUG
+    {
+      const unsigned long long wbits = uni64(bm[(pid & rmask) >> 6]);
+      const uint32_t zz = uni(Rw[4 * (size_t)x + 2]);
+      if (!((wbits >> (pid & 63)) & 1ull) || zz != pid) {
+        fail = kPathInternal;
+        site = ((wbits >> (pid & 63)) & 1ull) ? 9 : 8;
+        dbg_s = zz;
+        dbg_t = pid;
+        if (prof && lane == 0) {
+          prof[4] = dbg_ins ? dbg_w0 : cur_base;
+          prof[5] = dbg_ins ? dbg_w1 : cur_bits;
+          prof[6] = dbg_ins ? dbg_w2 : wbits;
+          prof[7] = dbg_ins ? dbg_w3 : 0xC0000000ull + (cache ? 1 : 0);
+        }
+        break;
+      }
+    }
+#endif
+    if (lane == 0) {
+      bm[(pid & rmask) >> 6] &= ~(1ull << (pid & 63));
+      Rw[4 * (size_t)x + 2] = pid | kLdSettled;
+      cnt[s & wmask] -= 1u;
+    }
+#ifdef FSTAMD_BAND_DEBUG
+    wave_lds_sync();
+    if (((pid & rmask) >> 6) == 1) ev(2, pid, uni64(bm[1]));
+#endif
+    ++pops;
+    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > wd) {
+      fail = kPathInternal;
+      site = 2;
+      break;
+    }
+    if (k > L || s >= NS || pid >= nn) {  // invariant guard: never walk on garbage
+      fail = kPathInternal;
+      site = 3;
+      dbg_s = s;
+      dbg_t = pid;
+      break;
+    }
+
+    // ---- best final (:165-179): lhs final only at k == L ----
+    if (k == L) {
+      const double fw2 = rhs.final_w[s];
+      if (!w_is_zero(fw2)) {
+        const double fw = w_times(w_one(), fw2);
+        const double total = w_times(dcur, fw);
+        if (best_id == kNoState || total < best_total || (total == best_total && pid < best_id)) {
+          best_id = pid;
+          best_fw = fw;
+          best_total = total;
+        }
+      }
+    }
+
+    LB_T(1);  // pop bookkeeping, best final
+    // ---- candidates: phase 1 (labels[k] arcs) then phase 3 (epsilon arcs) ----
+    const bool has1 = k < L;
+    const uint32_t label = has1 ? lab[k] : 0u;
+    const uint2 sp = rhs.span[s];
+    const uint32_t aoff = sp.x, na = sp.y;
+    uint32_t C = 0, lo1 = 0, n1 = 0, lo3 = 0, tmax = s;
+    const bool small = na <= 64;
+    if (small) {
+      const bool v = lane < na;
+      const uint32_t il = v ? rhs.il[aoff + lane] : 0xFFFFFFFFu;
+      const ArcRec r = v ? rhs.rec[aoff + lane] : ArcRec{0u, 0u, 0.0};
+      const bool p1 = v && has1 && il == label;
+      const bool p3 = v && il == kEpsilon;
+      const unsigned long long m1 = __ballot(p1), m3 = __ballot(p3);
+      n1 = (uint32_t)__popcll(m1);
+      C = n1 + (uint32_t)__popcll(m3);
+      tmax = max(tmax, __ockl_wfred_max_u32((p1 || p3) ? r.next : 0u));
+      if (p1 || p3) {  // (a window index does not depend on slo: valid after any slide)
+        const uint32_t rank = p1 ? (uint32_t)__popcll(m1 & lanemask_lt())
+                                 : n1 + (uint32_t)__popcll(m3 & lanemask_lt());
+        S.x[rank] = p1 ? 2 * wix(k + 1, r.next) : 2 * wix(k, r.next) + 1;
+        S.a[rank] = aoff + lane;
+        S.il[rank] = il;
+        S.ol[rank] = r.olabel;
+        S.w[rank] = p1 ? w_times(w_one(), r.weight) : r.weight;
+      }
+      wave_lds_sync();
+    } else {
+      uint32_t hi;
+      if (has1) {
+        span_by_ilabel(rhs, s, label, lo1, hi);
+        n1 = hi - lo1;
+      }
+      span_by_ilabel(rhs, s, kEpsilon, lo3, hi);
+      C = n1 + (hi - lo3);
+      for (uint32_t c = lane; c < C; c += 64) {
+        const uint32_t a = c < n1 ? lo1 + c : lo3 + (c - n1);
+        tmax = max(tmax, rhs.rec[a].next);
+      }
+      tmax = __ockl_wfred_max_u32(tmax);
+    }
+    tmax = uni(tmax);
+    relax += C;
+
+    LB_T(2);  // candidates
+    // ---- the window must hold every target: slide it up to the lowest state with an
+    // open tuple (a pop at state s only ever touches states >= s) ----
+    if (tmax >= slo + WS) {
+      ++slides;
+      // lowest state >= slo with an open tuple (cnt > 0); none: the popped state s
+      uint32_t smin = s;
+      for (uint32_t b = 0; b < WS; b += 64) {
+        const uint32_t st = slo + b + lane;
+        const bool v = b + lane < WS && st < s && cnt[st & wmask] != 0;
+        const unsigned long long m = __ballot(v);
+        if (m) {
+          smin = slo + b + (uint32_t)__ffsll((long long)m) - 1;
+          break;
+        }
+      }
+      smin = uni(smin);
+      if (tmax >= smin + WS) {  // the open tuples span more than the window
+        fail = kPathOverflow;
+        site = 4;
+        dbg_s = s;
+        dbg_t = smin;
+#ifdef FSTAMD_BAND_DEBUG
+        if (prof) {  // the open records at state smin: (k, f, id, dist) of the first, count
+          uint32_t first = ~0u, nopen = 0;
+          for (uint32_t r0 = 0; r0 < LC * 2; r0 += 64) {
+            const uint32_t r = r0 + lane;
+            const uint32_t ix = 2 * ((smin & wmask) * LC) + r;
+            const uint32_t z = r < LC * 2 ? Rw[4 * (size_t)ix + 2] : kLdUntouched;
+            const bool op = z != kLdUntouched && !(z & kLdSettled);
+            const unsigned long long m = __ballot(op);
+            nopen += (uint32_t)__popcll(m);
+            if (m && first == ~0u) first = r0 + (uint32_t)__ffsll((long long)m) - 1;
+          }
+          first = uni(first);
+          if (lane == 0) {
+            prof[5] = nopen;
+            prof[6] = cnt[smin & wmask];
+            if (first != ~0u) {
+              const uint4 rr = R[2 * ((smin & wmask) * LC) + first];
+              prof[4] = first;  // (k << 1) | f
+              prof[7] = ((unsigned long long)rr.z << 32) | (uint32_t)ld_dist(rr);
+            }
+          }
+        }
+#endif
+        break;
+      }
+      // clear the leaving states' records (every tuple there is final)
+      const uint32_t nclear = (smin - slo) * LC * 2;
+      for (uint32_t i = lane; i < nclear; i += 64) {
+        const uint32_t st = slo + i / (LC * 2);
+        const uint32_t r = i - (st - slo) * (LC * 2);
+        Rw[4 * (size_t)(2 * ((st & wmask) * LC) + r) + 2] = kLdUntouched;
+      }
+      wave_fence();
+      slo = smin;
+    }
+
+    LB_T(3);  // slides
+    for (uint32_t cb = 0; cb < C; cb += 64) {
+      const uint32_t cnt_c = min(64u, C - cb);
+      if (!small) {  // this chunk's candidates into LDS, in relax order
+        const uint32_t c = cb + lane;
+        if (lane < cnt_c) {
+          const bool p1 = c < n1;
+          const uint32_t a = p1 ? lo1 + c : lo3 + (c - n1);
+          const ArcRec r = rhs.rec[a];
+          S.x[lane] = p1 ? 2 * wix(k + 1, r.next) : 2 * wix(k, r.next) + 1;
+          S.a[lane] = a;
+          S.il[lane] = p1 ? label : kEpsilon;
+          S.ol[lane] = r.olabel;
+          S.w[lane] = p1 ? w_times(w_one(), r.weight) : r.weight;
+        }
+        wave_lds_sync();
+      }
+      // room for this chunk's future entries: compact the list first if needed
+      if (fn + 64 > ws.fcap) {
+        uint32_t wpos = 0;
+        for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
+          const uint32_t e = e0 + lane;
+          const bool v = e < fn;
+          const uint4 en = v ? fut[e] : make_uint4(0, 0, 0, 0);
+          const uint4 rv = v ? R[en.z] : make_uint4(0, 0, kLdUntouched, 0);
+          const double ed = __hiloint2double((int)en.y, (int)en.x);
+          const bool live = v && rv.z == en.w && ld_dist(rv) == ed;
+          const unsigned long long lm = __ballot(live);
+          if (live) fut[wpos + (uint32_t)__popcll(lm & lanemask_lt())] = en;
+          wpos += (uint32_t)__popcll(lm);
+        }
+        wave_fence();
+        fn = wpos;
+        if (fn + 64 > ws.fcap) {
+          fail = kPathOverflow;
+          site = 6;
+          break;
+        }
+      }
+      const bool act = lane < cnt_c;
+      const uint32_t tx = act ? S.x[lane] : 0u;
+      const double nd = act ? w_times(dcur, S.w[lane]) : 0.0;
+      S.nd[lane] = nd;
+      const uint4 rv = act ? R[tx] : make_uint4(0, 0, kLdUntouched, 0);
+      // group candidates by target: the group's first lane folds it in order
+      unsigned long long gmask = 0;
+      {
+        unsigned long long pend = __ballot(act);
+        while (pend) {
+          const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
+          const uint32_t xl = lane_read(tx, l);
+          const unsigned long long m = __ballot(act && tx == xl);
+          if (lane == l) gmask = m;
+          pend &= ~m;
+        }
+      }
+      wave_lds_sync();
+      const bool leader = gmask != 0ull;
+      const bool untouched = rv.z == kLdUntouched;
+      const double od = untouched ? w_zero() : ld_dist(rv);
+      double cd = od;
+      uint32_t bprev = untouched ? kLdNoPrev : rv.w;
+      uint32_t bil = 0, bol = 0, ba = 0;
+      bool took = false;
+      if (leader) {
+        if (!untouched && bprev == pid) {  // back set earlier in this pop: its labels
+          const uint32_t a0 = back[(rv.z & ~kLdSettled)].y;
+          bil = rhs.il[a0];
+          bol = rhs.rec[a0].olabel;
+        }
+        unsigned long long m = gmask;
+        while (m) {  // relax (:99-141) in candidate order
+          const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
+          m &= m - 1;
+          const double cnd = S.nd[i];
+          const uint32_t cil = S.il[i], col = S.ol[i];
+          bool take = w_is_zero(cd) || cnd < cd;
+          if (!take && cnd == cd)
+            take = pid < bprev || (pid == bprev && (cil < bil || (cil == bil && col < bol)));
+          if (take) {
+            cd = cnd;
+            bprev = pid;
+            bil = cil;
+            bol = col;
+            ba = S.a[i];
+            took = true;
+          }
+        }
+      }
+      // getOrCreate: new tuples numbered by first occurrence (leaders in lane order)
+      const bool fresh = leader && untouched;
+      const unsigned long long fm = __ballot(fresh);
+      const uint32_t id = fresh ? nn + (uint32_t)__popcll(fm & lanemask_lt()) : (rv.z & ~kLdSettled);
+      nn += (uint32_t)__popcll(fm);
+      // a new id pushes id - LS out of the live span: that id must not be open at dcur
+      // (one open above dcur is checked when it joins the bitmap), nor may a tie re-open
+      // an id outside the span
+      const uint32_t oid = id - LS;
+      bool clash = fresh && id >= LS && ((bm[(oid & rmask) >> 6] >> (oid & 63)) & 1ull);
+      const bool settled = !untouched && (rv.z & kLdSettled);
+      if (took) {
+        R[tx] = ld_rec(cd, untouched ? id : rv.z, pid);
+        back[id] = make_uint2(pid, ba);
+        if (fresh) {
+          idr[id & rmask] = tx;
+          S.ring[id & (kLdRing - 1)] = tx;
+        }
+      }
+      {  // open tuples per window state: one add per distinct state slot
+        const uint32_t ts = (tx >> 1) / LC;
+        unsigned long long pend = fm;
+        while (pend) {
+          const uint32_t sl = lane_read(ts, (uint32_t)__ffsll((long long)pend) - 1);
+          const unsigned long long m = __ballot(fresh && ts == sl);
+          pend &= ~m;
+          if (lane == 0) cnt[sl] += (uint32_t)__popcll(m);
+        }
+      }
+      // push (:136-140): open at dcur -> bitmap, above -> future list.  An equal-dist
+      // take (a tie) is already queued at that distance.
+      const bool q = took && !settled && (untouched || cd < od);
+      const bool tob = q && cd == dcur;
+      const bool tof = q && !tob;
+      clash |= tob && !fresh && id + LS <= nn;
+      const unsigned long long fmk = __ballot(tof);
+      if (tof) fut[fn + (uint32_t)__popcll(fmk & lanemask_lt())] = ld_rec(cd, tx, id);
+      fn += (uint32_t)__popcll(fmk);
+      bucket_insert(tob, id);
+      wave_fence();
+      wave_lds_sync();
+      if (__ballot(clash) || (uint64_t)nn >= ws.idcap) {
+        fail = kPathOverflow;
+        site = 5;
+        dbg_s = s;
+        dbg_t = uni(wave_min_u32d(clash ? id : ~0u));
+        break;
+      }
+    }
+    LB_T(4);  // relax
+    if (fail != kPathOk) break;
+  }
+#ifdef FSTAMD_BAND_TIMING
+  if (prof && lane == 0)
+    for (int i = 0; i < 6; ++i) prof[300 + i] += tacc[i];
+#endif
+
+  // ---- result (:368-400): the back chain by id ----
+  ld_drain();
+  uint32_t P = 0;
+  unsigned long long o = 0;
+  double fin = w_zero();
+  int32_t st = fail;
+  if (lane == 0) {
+    if (st == kPathOk) {
+      if (best_id == kNoState) {
+        st = kPathEmpty;
+      } else {
+        uint32_t cur = best_id;
+        while (cur != 0) {  // init_id == 0
+          const uint32_t prev = back[cur].x;
+          if (prev == kLdNoPrev) {
+            st = kPathEmpty;
+            break;
+          }
+          if (++P > nn) {
+            st = kPathCycle;
+            break;
+          }
+          cur = prev;
+        }
+        if (st == kPathOk) {
+          o = atomicAdd(out.cursor, (unsigned long long)P);
+          if (o + P > out.arc_cap) {
+            st = kPathOutputFull;
+          } else {
+            uint32_t kk = P;
+            cur = best_id;
+            while (cur != 0 && kk > 0) {
+              const uint2 b = back[cur];
+              const uint32_t il = rhs.il[b.y];
+              const ArcRec r = rhs.rec[b.y];
+              --kk;
+              out.out_il[o + kk] = il;
+              out.out_ol[o + kk] = r.olabel;
+              out.out_w[o + kk] = il == kEpsilon ? r.weight : w_times(w_one(), r.weight);
+              cur = b.x;
+            }
+            fin = best_fw;
+          }
+        }
+      }
+    }
+    if (st != kPathOk) {
+      P = 0;
+      o = 0;
+      fin = w_zero();
+    }
+    out.status[si] = st;
+    out.path_len[si] = st == kPathInternal ? pops : P;
+    out.path_off[si] = st == kPathInternal ? site : o;
+    out.final_w[si] = fin;
+    if (out.work) {
+      out.work[2 * si] = nn;
+      out.work[2 * si + 1] = (uint32_t)relax;
+    }
+    if (prof) {
+      prof[0] += pops;
+      prof[1] += advances;
+      prof[2] += slides;
+      if (fail != kPathOk && site != 0) {
+        if (site >= 4) prof[site] += 1;
+        prof[8] = pops;  // the last failure of this wave
+        prof[9] = site;
+        prof[10] = dbg_s;
+        prof[11] = dbg_t;
+        prof[12] = slo;
+        prof[13] = nn;
+        prof[14] = fn;
+        prof[15] = L;
+      }
+    }
+  }
+  // ---- leave the window, the bitmap and the counts clean ----
+  wave_fence();
+  for (uint32_t i = lane; i < WS * LC * 2; i += 64) Rw[4 * (size_t)i + 2] = kLdUntouched;
+  for (uint32_t i = lane; i < nbw; i += 64) bm[i] = 0ull;
+  for (uint32_t i = lane; i < WS; i += 64) cnt[i] = 0u;
+  wave_fence();
+  wave_lds_sync();
+}
+
+__global__ void __launch_bounds__(64)
+lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item, LbWs ws,
+                 BatchOutDev out) {
+  extern __shared__ unsigned long long lb_dyn[];
+  __shared__ LdLds S;
+  unsigned long long* bm = lb_dyn;                        // [ring / 64] open-at-dcur bitmap
+  uint32_t* cnt = (uint32_t*)(lb_dyn + ws.ring / 64);     // [ws] open tuples per window state
+  uint32_t* lab = cnt + ws.ws;                            // [lcap] the string's labels
+  const uint32_t lane = threadIdx.x;
+  const size_t w = blockIdx.x;
+  uint4* R = ws.win + w * ws.wn;
+  uint2* back = ws.back + w * ws.idcap;
+  uint32_t* idr = ws.idr + w * (size_t)ws.ring;
+  uint4* fut = ws.fut + w * (size_t)ws.fcap;
+  unsigned long long* prof = ws.prof ? ws.prof + w * kLbProf : nullptr;
+
+  for (uint32_t i = lane; i < ws.ring / 64; i += 64) bm[i] = 0ull;
+  for (uint32_t i = lane; i < ws.ws; i += 64) cnt[i] = 0u;
+  wave_lds_sync();
+
+  const uint32_t num_items = ws.items ? ws.num_items : in.num_strings;
+  uint32_t passes = 0;
+  for (;;) {
+    // one fresh item per pass, fetched by the first active lane (lazy_dense.hpp's loop)
+    if (++passes > num_items + 1) return;
+    uint32_t item = 0;
+    const uint32_t first = (uint32_t)__ffsll((long long)__ballot(1)) - 1;
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == first)
+      item = atomicAdd(next_item, 1u);
+    item = __builtin_amdgcn_readlane(item, first);
+    if (item >= num_items) break;
+    const uint32_t si = ws.items ? uni(ws.items[item]) : item;
+    const uint64_t off = in.offsets[si];
+    const uint32_t L = uni((uint32_t)(in.offsets[si + 1] - off));
+    int32_t pre = kPathOk;
+    if (rhs.start == kNoState || n_best != 1)  // compose-shortest-path.zig:30-33
+      pre = (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN;
+    else if (L > ws.lcap)
+      pre = kPathUnsupported;
+    if (pre == kPathOk) {
+      bool zero_label = false;
+      for (uint32_t i = lane; i < L; i += 64) {
+        const uint32_t x = in.labels[off + i];
+        lab[i] = x;
+        zero_label |= x == kEpsilon;
+      }
+      if (__ballot(zero_label) != 0ull) pre = kPathUnsupported;  // lhs epsilon phases
+      wave_lds_sync();
+    }
+    pre = (int32_t)uni((uint32_t)pre);
+    if (pre != kPathOk) {
+      if (lane == 0) write_status(out, si, pre, 0, 0);
+    } else {
+      lazy_band_string(rhs, in, ws, out, R, back, idr, fut, bm, cnt, lab, S, prof, si, L);
+    }
+  }
+}
+
+}  // namespace fstamd

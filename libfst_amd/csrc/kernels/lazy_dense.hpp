@@ -105,9 +105,12 @@ __device__ __forceinline__ uint32_t wave_min_u32d(uint32_t v) { return __ockl_wf
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) {  // l uniform
   return __builtin_amdgcn_readlane(v, l);
 }
+// (readlane returns int: both halves go through uint32_t, or a low half with bit 31 set
+// would sign-extend over the high half)
 __device__ __forceinline__ unsigned long long lane_read64(unsigned long long v, uint32_t l) {
-  return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
-         __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+  return ((unsigned long long)hi << 32) | lo;
 }
 // Leaf words are updated with L2 atomics (several lanes may set bits of one word in one
 // instruction), so they are read with agent-scope loads, which skip the vector L1.

@@ -142,7 +142,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint2* const back = slabs + (size_t)njobs * lp.back_cap;
     const uint64_t off0 = in.offsets[si];
     const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
-                         __builtin_amdgcn_readfirstlane((uint32_t)off0);
+                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)off0);  // (no sign ext.)
     const uint32_t L = __builtin_amdgcn_readfirstlane((uint32_t)(in.offsets[si + 1] - off));
 
     if (rhs.start == kNoState || n_best != 1) {  // compose-shortest-path.zig:30-33
@@ -472,7 +472,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         } else {
           const unsigned long long dv = __ockl_wfred_or_u64(diff);
           vary = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(dv >> 32)) << 32) |
-                 __builtin_amdgcn_readfirstlane((uint32_t)dv);
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)dv);
         }
         if (counting) {
           // stable counting sort, 64 ids at a time in id order: the lanes holding key b
@@ -626,7 +626,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     unsigned long long o = 0;
     if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
     o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
-        __builtin_amdgcn_readfirstlane((uint32_t)o);
+        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)o);
     if (o + L > out.arc_cap) {
       if (lane == 0) write_status(out, si, kPathOutputFull, tuples, relax);
       continue;
