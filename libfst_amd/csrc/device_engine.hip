@@ -312,7 +312,7 @@ enum Scratch : size_t {
   kLdFut,
   kLdItems,
   kLbWin,
-  kLbBack,
+  kLbBk,
   kLbIdr,
   kLbFut,
   kLbItems,
@@ -1263,12 +1263,21 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   auto len = [&](uint32_t i) { return (uint32_t)std::min<uint64_t>(off[i + 1] - off[i], in.max_len); };
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len(a) < len(b); });
   const uint32_t NS = rhs.view.num_states;
-  constexpr uint32_t kRing = 16384, kFcap = 65536;
+  constexpr uint32_t kRing = 4096, kFcap = 65536;
   struct Plan {
     uint32_t lcap, wstates, grid, first, count;
-    uint64_t wn, idcap;
+    uint64_t wn, tn;
     size_t lds;
   };
+  // back pointer width: f_src (1 bit) | state distance (dbits) | arc index within the source
+  // state; 1, 2 or 4 B as that fits (config 3's rhs: 1 + 3 + 4 bits), else not this engine's
+  uint32_t dbits = 1;
+  while ((1ull << dbits) <= rhs.view.jump_fwd) ++dbits;
+  uint32_t abits = 1;
+  while ((1ull << abits) < rhs.view.max_span) ++abits;
+  const uint32_t bits = 1 + dbits + abits;
+  if (bits > 32) return hipSuccess;
+  const uint32_t bkb = bits <= 8 ? 1 : bits <= 16 ? 2 : 4;
   // every launch's memory from one budget: free HBM (pooled blocks released first) less a
   // 24 GB reserve, 90 % of it; the plans are made one at a time per device (EnginePool::heavy)
   std::unique_lock<std::mutex> heavy(engine_pool(dev_).heavy);
@@ -1278,14 +1287,17 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
       uint64_t avail = fr;
-      for (size_t b : {kLbWin, kLbBack, kLbIdr, kLbFut}) avail += sizes_[b];
+      for (size_t b : {kLbWin, kLbBk, kLbIdr, kLbFut}) avail += sizes_[b];
       const uint64_t reserve = 24ull << 30;
       budget = avail > 2 * reserve ? (avail - reserve) / 10 * 9 : avail / 2;
     }
     if (const char* be = std::getenv("FSTAMD_DENSE_BUDGET_GB"))
       budget = (uint64_t)std::max(1, std::atoi(be)) << 30;
   }
-  const uint32_t max_waves = (uint32_t)num_cus_ * 16;
+  // waves per CU: ~5 KB of LDS and 61 VGPRs each, so 32 fit
+  uint32_t wpc = 32;
+  if (const char* we = std::getenv("FSTAMD_BAND_WAVES_PER_CU")) wpc = (uint32_t)std::max(1, std::atoi(we));
+  const uint32_t max_waves = (uint32_t)num_cus_ * wpc;
   const char* ge = std::getenv("FSTAMD_DENSE_GRID");
   auto make_plan = [&](uint32_t max_len, uint32_t count, Plan& p) -> bool {
     p.lcap = std::max<uint32_t>(max_len, 1);
@@ -1295,11 +1307,11 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     while (w < want) w <<= 1;
     p.wstates = w;
     p.wn = (uint64_t)w * (p.lcap + 1) * 2;
-    p.idcap = (uint64_t)(p.lcap + 1) * NS * 2 + 64;
-    if (p.idcap > kLdDenseMax) return false;
-    p.lds = kRing / 8 + (size_t)w * 4 + (size_t)p.lcap * 4;
+    p.tn = (uint64_t)(p.lcap + 1) * NS * 2;  // ids and tuple indices fit 31 bits
+    if (p.tn > kLdDenseMax) return false;
+    p.lds = kRing / 8 + (size_t)p.lcap * 4;
     if (p.lds > kLdMaxDynLds) return false;
-    const uint64_t per_wave = p.wn * 16 + p.idcap * 8 + (uint64_t)kRing * 4 + (uint64_t)kFcap * 16;
+    const uint64_t per_wave = p.wn * 16 + p.tn * bkb + (uint64_t)kRing * 4 + (uint64_t)kFcap * 16;
     p.grid = (uint32_t)std::min<uint64_t>(
         {(uint64_t)max_waves, (uint64_t)count, std::max<uint64_t>(1, budget / per_wave)});
     if (ge) p.grid = std::min<uint32_t>(p.grid, (uint32_t)std::max(1, std::atoi(ge)));
@@ -1326,20 +1338,22 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     std::reverse(order.begin() + lo, order.begin() + hi);
     plans.push_back(p);
   }
-  uint64_t need_win = 0, need_back = 0;
+  uint64_t need_win = 0, need_bk = 0;
   uint32_t gmax = 0;
   for (const Plan& p : plans) {
     need_win = std::max<uint64_t>(need_win, (uint64_t)p.grid * p.wn);
-    need_back = std::max<uint64_t>(need_back, (uint64_t)p.grid * p.idcap);
+    need_bk = std::max<uint64_t>(need_bk, (uint64_t)p.grid * p.tn);
     gmax = std::max(gmax, p.grid);
   }
   LbWs ws{};
   ws.win = (uint4*)scratch(kLbWin, need_win * 16);
-  ws.back = (uint2*)scratch(kLbBack, need_back * 8);
+  ws.bk = scratch(kLbBk, need_bk * bkb);
+  ws.bkb = bkb;
+  ws.dbits = dbits;
   ws.idr = (uint32_t*)scratch(kLbIdr, (size_t)gmax * kRing * 4);
   ws.fut = (uint4*)scratch(kLbFut, (size_t)gmax * kFcap * 16);
   uint32_t* d_order = (uint32_t*)scratch(kLbItems, (size_t)num * 4);
-  if (!ws.win || !ws.back || !ws.idr || !ws.fut || !d_order) return hipErrorOutOfMemory;
+  if (!ws.win || !ws.bk || !ws.idr || !ws.fut || !d_order) return hipErrorOutOfMemory;
   if (lb_clean_ != bufs_[kLbWin] || lb_clean_bytes_ != sizes_[kLbWin]) {  // new allocation
     HIP_TRY(hipMemsetAsync(ws.win, 0xFF, sizes_[kLbWin], stream));
     lb_clean_ = bufs_[kLbWin];
@@ -1357,7 +1371,7 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     ws.lcap = p.lcap;
     ws.ws = p.wstates;
     ws.wn = p.wn;
-    ws.idcap = p.idcap;
+    ws.tn = p.tn;
     ws.wd_ticks = watchdog_ticks();
     ws.wd_tuple_ticks = std::getenv("FSTAMD_WATCHDOG_MS") ? 0ull : 1000ull;
     ws.items = d_order + p.first;
@@ -1407,10 +1421,10 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     }
   }
   uint64_t held = 0;
-  for (size_t b : {kLbWin, kLbBack, kLbIdr, kLbFut}) held += sizes_[b];
+  for (size_t b : {kLbWin, kLbBk, kLbIdr, kLbFut}) held += sizes_[b];
   if (held > (64ull << 30)) {  // give large arrays back after the call
     HIP_TRY(hipStreamSynchronize(stream));
-    for (size_t b : {kLbWin, kLbBack, kLbIdr, kLbFut}) {
+    for (size_t b : {kLbWin, kLbBk, kLbIdr, kLbFut}) {
       (void)hipFree(bufs_[b]);
       bufs_[b] = nullptr;
       sizes_[b] = 0;

@@ -3,11 +3,11 @@
 //
 // Same replay as lazy_dense.hpp (the reference's pops of src/ops/compose-shortest-path.zig:
 // 26-401 one by one, heap split by distance, candidates read lane-parallel and folded in
-// relax order), for the same domain, with a per-wave footprint ~3.5x smaller so that
-// ~4x as many strings run at once.  The dense replay is latency-bound: its throughput
-// scales with the waves in flight (T = 16,384, L = 87: 20 / 40 / 78 / 142 strings/s at
-// 128 / 256 / 512 / 1,024 waves, profiles/r03/dense_waves.log), and at config 3's full size
-// its 28 B per dense tuple (0.93 GB per wave at L = 251) cap them near 250.
+// relax order), for the same domain, with a per-wave footprint ~14x smaller so that many
+// more strings run at once.  The dense replay is latency-bound: its throughput scales
+// with the waves in flight (T = 16,384, L = 87: 20 / 40 / 78 / 142 strings/s at 128 / 256 /
+// 512 / 1,024 waves, profiles/r03/dense_waves.log), and at config 3's full size its 28 B
+// per dense tuple (0.93 GB per wave at L = 251) cap them near 250.
 //
 // What lives where (per wave):
 //   * the tuple records {dist, id | settled, back source id} (16 B) only for rhs states in
@@ -15,11 +15,14 @@
 //     going forward (t >= s, RhsView::jump_back == 0), a pop at state s only touches states
 //     >= s, so a tuple whose state lies below every open tuple's can never be touched or
 //     relaxed again (its record is final): the window slides up to the lowest state with an
-//     open tuple (a count per window state in LDS) when a target falls beyond its end.  On
+//     open tuple (found by walking the open set, rare) when a target falls beyond its end.  On
 //     epsilon-dense lattices the open tuples span L + 2 states (a diagonal across the input
 //     positions, tests/lazy_model.py), so Ws = 2 (L + 1) rounded up to a power of two;
-//   * per id, written through on every take: {back source id, rhs arc} (8 B) -- all the
-//     backtrace (:368-400) needs;
+//   * per tuple (every state, not just the window), written on every take: the back
+//     pointer packed in 1 B (2 or 4 B when the rhs needs it) -- the source tuple's filter, its
+//     state distance (t - s <= jump_fwd) and the arc's index within the source state's
+//     arcs; the source position follows from the target's filter (0: a labelled arc,
+//     k - 1; 1: an epsilon arc, k).  All the backtrace (:368-400) needs, walked by tuple;
 //   * the open-at-dcur set as a bitmap over the newest R ids (LDS): the open tuples' ids lie
 //     within ~12 L of the newest (2,997 at L = 251, T = 1,024); an id falling R behind
 //     while open, or a window overflow, hands the string to the dense replay (OVERFLOW);
@@ -37,19 +40,21 @@ namespace fstamd {
 #else
 #define LB_T(i) do { } while (0)
 #endif
-#ifdef FSTAMD_BAND_DEBUG
-constexpr uint32_t kLbProf = 512;  // per-wave profile words (+ the debug event log)
+#if defined(FSTAMD_BAND_DEBUG) || defined(FSTAMD_BAND_TIMING)
+constexpr uint32_t kLbProf = 512;  // per-wave profile words (+ the phase timing)
 #else
 constexpr uint32_t kLbProf = 16;
 #endif
 
 struct LbWs {
   uint4* win;                 // [grid * wn] window records (lazy_dense.hpp ld_rec layout)
-  uint2* back;                // [grid * idcap] per id {back source id, rhs arc}
+  void* bk;                   // [grid * tn] per tuple back pointer (bkb bytes each)
   uint32_t* idr;              // [grid * ring] id -> window index (id mod ring)
   uint4* fut;                 // [grid * fcap] {dist lo, dist hi, window index, id}
   unsigned long long wn;      // window records per wave = ws * (lcap + 1) * 2
-  unsigned long long idcap;   // ids per wave (every tuple the string can create)
+  unsigned long long tn;      // tuples per wave = num_states * (lcap + 1) * 2
+  uint32_t bkb;               // bytes per back pointer: 1, 2 or 4
+  uint32_t dbits;             // bits of the state distance in a back pointer
   uint32_t ws;                // window states (power of two)
   uint32_t ring;              // ids kept (power of two, multiple of 4096)
   uint32_t fcap, lcap;
@@ -60,11 +65,25 @@ struct LbWs {
   uint32_t num_items;
 };
 
+// The id -> window index map of the newest kLbRing ids also lives in LDS (the rest: the
+// per-wave HBM ring).  Small, so that 32 waves fit a CU's 160 KB of LDS (~5 KB each).
+constexpr uint32_t kLbRing = 256;
+
+struct LbLds {
+  uint32_t ring[kLbRing];  // id -> window index for id >= nn - kLbRing
+  uint32_t x[64];    // candidates in relax order: target window index
+  uint32_t a[64];    // rhs arc index
+  uint32_t il[64];
+  uint32_t ol[64];
+  double w[64];      // arc weight as relaxed (W.times(lhs arc, rhs arc) for phase 1)
+  double nd[64];     // dist[curr] (x) w
+};
+
 __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const ChainInput& in,
                                                  const LbWs& ws, const BatchOutDev& out,
-                                                 uint4* R, uint2* back, uint32_t* idr, uint4* fut,
-                                                 unsigned long long* bm, uint32_t* cnt,
-                                                 const uint32_t* lab, LdLds& S,
+                                                 uint4* R, void* bkv, uint32_t* idr, uint4* fut,
+                                                 unsigned long long* bm,
+                                                 const uint32_t* lab, LbLds& S,
                                                  unsigned long long* prof, uint32_t si,
                                                  uint32_t L) {
   const uint32_t lane = threadIdx.x;
@@ -79,6 +98,21 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   // ring slot of an open id is never reused
   const uint32_t LS = RING - 64;
   auto wix = [&](uint32_t k_, uint32_t s_) { return (s_ & wmask) * LC + k_; };  // x 2 + f
+  auto gix = [&](uint32_t k_, uint32_t s_) { return s_ * LC + k_; };            // x 2 + f
+  // back pointers: f_src | ds << 1 | local arc << (1 + dbits)
+  uint8_t* bk8 = (uint8_t*)bkv;
+  uint16_t* bk16 = (uint16_t*)bkv;
+  uint32_t* bk32 = (uint32_t*)bkv;
+  const uint32_t bkb = ws.bkb;  // bytes per back pointer: 1, 2 or 4
+  const uint32_t dbits = ws.dbits, dmask = (1u << dbits) - 1;
+  auto bk_get = [&](uint32_t g_) -> uint32_t {
+    return bkb == 1 ? (uint32_t)bk8[g_] : bkb == 2 ? (uint32_t)bk16[g_] : bk32[g_];
+  };
+  auto bk_put = [&](uint32_t g_, uint32_t c_) {
+    if (bkb == 1) bk8[g_] = (uint8_t)c_;
+    else if (bkb == 2) bk16[g_] = (uint16_t)c_;
+    else bk32[g_] = c_;
+  };
   if (prof && lane == 0) prof[3] += 1;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long wd = ws.wd_ticks + (uint64_t)LC * 2 * NS * ws.wd_tuple_ticks;
@@ -87,11 +121,9 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   const uint32_t x0 = 2 * wix(0, rhs.start);
   if (lane == 0) {
     R[x0] = ld_rec(w_one(), 0u, kLdNoPrev);
-    back[0] = make_uint2(kLdNoPrev, 0u);
     idr[0] = x0;
     S.ring[0] = x0;
     bm[0] = 1ull;
-    cnt[rhs.start & wmask] = 1;
   }
   wave_lds_sync();
   uint32_t nn = 1, fn = 0, pops = 0, advances = 0, slides = 0;
@@ -100,50 +132,19 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   unsigned long long cur_bits = 1ull;
   bool cache = true;
   double dcur = w_one();
-  uint32_t best_id = kNoState;
+  uint32_t best_id = kNoState, best_g = 0;
   double best_fw = w_zero(), best_total = w_zero();
   int32_t fail = kPathOk;
   uint32_t site = 0;  // INTERNAL / OVERFLOW: where it stopped (FSTAMD_BFS_PROF)
   uint32_t dbg_s = 0, dbg_t = 0;
-#ifdef FSTAMD_BAND_DEBUG
-  uint32_t dbg_ins = 0;
-  unsigned long long dbg_w0 = 0, dbg_w1 = 0, dbg_w2 = 0, dbg_w3 = 0;
-  uint32_t nev = 0;  // events on bitmap word 1 -> prof[16 + 2 e], prof[17 + 2 e]
-  auto ev = [&](uint32_t tag, uint32_t a, unsigned long long v) {
-    if (prof && lane == 0 && nev < 240) {
-      prof[16 + 2 * nev] = ((unsigned long long)tag << 56) | ((unsigned long long)a << 24) | pops;
-      prof[17 + 2 * nev] = v;
-    }
-    ++nev;
-  };
-#endif
   uint64_t relax = 0;
 
-  // open-at-dcur insert of lane-held ids: LDS bitmap bits, the cached word, lowp.  The
-  // bitmap is the wave's own: each word the lanes hit is OR-reduced across the wave and
-  // written by one lane (no same-word atomics from many lanes in one instruction)
+  // open-at-dcur insert of lane-held ids: LDS bitmap bits (ds_or_b64, no return), the
+  // cached word (one reduction when an id falls in it), lowp
   auto bucket_insert = [&](bool ins, uint32_t id) {
-    unsigned long long pend = __ballot(ins);
-    while (pend) {
-      const uint32_t wl = lane_read(id, (uint32_t)__ffsll((long long)pend) - 1) & ~63u;
-      const bool mine = ins && (id & ~63u) == wl;
-      const unsigned long long bits = uni64(wave_or_u64(mine ? 1ull << (id & 63) : 0ull));
-      pend &= ~__ballot(mine);
-      if (lane == 0) bm[(wl & rmask) >> 6] |= bits;
-      if (wl == cur_base) cur_bits = uni64(cur_bits | bits);
-#ifdef FSTAMD_BAND_DEBUG
-      wave_lds_sync();
-      const unsigned long long chk = uni64(bm[(wl & rmask) >> 6]);
-      if (((wl & rmask) >> 6) == 1) ev(1, wl, chk);
-      if ((chk & bits) != bits && dbg_ins == 0) {
-        dbg_ins = 1;
-        dbg_w0 = bits;
-        dbg_w1 = chk;
-        dbg_w2 = __ballot(1);
-        dbg_w3 = wl;
-      }
-#endif
-    }
+    if (ins) atomicOr(&bm[(id & rmask) >> 6], 1ull << (id & 63));
+    if (__ballot(ins && (id & ~63u) == cur_base))
+      cur_bits = uni64(cur_bits | wave_or_u64(ins && (id & ~63u) == cur_base ? 1ull << (id & 63) : 0ull));
     if (__ballot(ins && id < cur_base)) cache = false;
     if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
   };
@@ -179,9 +180,6 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         }
       }
       found = uni(found);
-#ifdef FSTAMD_BAND_DEBUG
-      ev(3, found, uni64(fw));
-#endif
       if (found != kNoState) {
         cur_base = found;
         cur_bits = uni64(fw);
@@ -249,7 +247,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     // ---- pop (:159-163) ----
     const uint32_t pid = uni(cur_base + (uint32_t)__ffsll((long long)cur_bits) - 1);
     cur_bits = uni64(cur_bits & (cur_bits - 1));
-    const uint32_t x = uni(pid + kLdRing >= nn ? S.ring[pid & (kLdRing - 1)] : idr[pid & rmask]);
+    const uint32_t x = uni(pid + kLbRing >= nn ? S.ring[pid & (kLbRing - 1)] : idr[pid & rmask]);
     const uint32_t sslot = (x >> 1) / LC;
     const uint32_t k = (x >> 1) - sslot * LC;
     const uint32_t s = slo + ((sslot - slo) & wmask);
@@ -262,25 +260,14 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         site = ((wbits >> (pid & 63)) & 1ull) ? 9 : 8;
         dbg_s = zz;
         dbg_t = pid;
-        if (prof && lane == 0) {
-          prof[4] = dbg_ins ? dbg_w0 : cur_base;
-          prof[5] = dbg_ins ? dbg_w1 : cur_bits;
-          prof[6] = dbg_ins ? dbg_w2 : wbits;
-          prof[7] = dbg_ins ? dbg_w3 : 0xC0000000ull + (cache ? 1 : 0);
-        }
         break;
       }
     }
 #endif
     if (lane == 0) {
-      bm[(pid & rmask) >> 6] &= ~(1ull << (pid & 63));
+      atomicAnd(&bm[(pid & rmask) >> 6], ~(1ull << (pid & 63)));
       Rw[4 * (size_t)x + 2] = pid | kLdSettled;
-      cnt[s & wmask] -= 1u;
     }
-#ifdef FSTAMD_BAND_DEBUG
-    wave_lds_sync();
-    if (((pid & rmask) >> 6) == 1) ev(2, pid, uni64(bm[1]));
-#endif
     ++pops;
     if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > wd) {
       fail = kPathInternal;
@@ -303,6 +290,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         const double total = w_times(dcur, fw);
         if (best_id == kNoState || total < best_total || (total == best_total && pid < best_id)) {
           best_id = pid;
+          best_g = 2 * gix(k, s) + (x & 1);
           best_fw = fw;
           best_total = total;
         }
@@ -359,47 +347,45 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     // open tuple (a pop at state s only ever touches states >= s) ----
     if (tmax >= slo + WS) {
       ++slides;
-      // lowest state >= slo with an open tuple (cnt > 0); none: the popped state s
+      // lowest state with an open tuple: the ids open at dcur (bitmap) and the live future
+      // entries (compacted on the way); none below: the popped state s.  Slides are rare
+      // (every ~Ws - L states), so the open set is walked rather than counted per pop.
       uint32_t smin = s;
-      for (uint32_t b = 0; b < WS; b += 64) {
-        const uint32_t st = slo + b + lane;
-        const bool v = b + lane < WS && st < s && cnt[st & wmask] != 0;
-        const unsigned long long m = __ballot(v);
-        if (m) {
-          smin = slo + b + (uint32_t)__ffsll((long long)m) - 1;
-          break;
+      {
+        auto state_of = [&](uint32_t xw) { return slo + (((xw >> 1) / LC - slo) & wmask); };
+        const uint32_t lo = max(lowp, nn > LS ? nn - LS : 0u);
+        for (uint32_t b0 = lo & ~63u; b0 < nn; b0 += 64 * 64) {
+          const uint32_t id0 = b0 + lane * 64;
+          unsigned long long v = id0 < nn ? bm[(id0 & rmask) >> 6] : 0ull;
+          while (v) {
+            const uint32_t id = id0 + (uint32_t)__ffsll((long long)v) - 1;
+            v &= v - 1;
+            const uint32_t xw = id + kLbRing >= nn ? S.ring[id & (kLbRing - 1)] : idr[id & rmask];
+            smin = min(smin, state_of(xw));
+          }
         }
+        uint32_t wpos = 0;
+        for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
+          const uint32_t e = e0 + lane;
+          const bool v = e < fn;
+          const uint4 en = v ? fut[e] : make_uint4(0, 0, 0, 0);
+          const uint4 rv = v ? R[en.z] : make_uint4(0, 0, kLdUntouched, 0);
+          const double ed = __hiloint2double((int)en.y, (int)en.x);
+          const bool live = v && rv.z == en.w && ld_dist(rv) == ed;
+          if (live) smin = min(smin, state_of(en.z));
+          const unsigned long long lm = __ballot(live);
+          if (live) fut[wpos + (uint32_t)__popcll(lm & lanemask_lt())] = en;
+          wpos += (uint32_t)__popcll(lm);
+        }
+        wave_fence();
+        fn = wpos;
+        smin = uni(wave_min_u32d(smin));
       }
-      smin = uni(smin);
       if (tmax >= smin + WS) {  // the open tuples span more than the window
         fail = kPathOverflow;
         site = 4;
         dbg_s = s;
         dbg_t = smin;
-#ifdef FSTAMD_BAND_DEBUG
-        if (prof) {  // the open records at state smin: (k, f, id, dist) of the first, count
-          uint32_t first = ~0u, nopen = 0;
-          for (uint32_t r0 = 0; r0 < LC * 2; r0 += 64) {
-            const uint32_t r = r0 + lane;
-            const uint32_t ix = 2 * ((smin & wmask) * LC) + r;
-            const uint32_t z = r < LC * 2 ? Rw[4 * (size_t)ix + 2] : kLdUntouched;
-            const bool op = z != kLdUntouched && !(z & kLdSettled);
-            const unsigned long long m = __ballot(op);
-            nopen += (uint32_t)__popcll(m);
-            if (m && first == ~0u) first = r0 + (uint32_t)__ffsll((long long)m) - 1;
-          }
-          first = uni(first);
-          if (lane == 0) {
-            prof[5] = nopen;
-            prof[6] = cnt[smin & wmask];
-            if (first != ~0u) {
-              const uint4 rr = R[2 * ((smin & wmask) * LC) + first];
-              prof[4] = first;  // (k << 1) | f
-              prof[7] = ((unsigned long long)rr.z << 32) | (uint32_t)ld_dist(rr);
-            }
-          }
-        }
-#endif
         break;
       }
       // clear the leaving states' records (every tuple there is final)
@@ -454,6 +440,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       }
       const bool act = lane < cnt_c;
       const uint32_t tx = act ? S.x[lane] : 0u;
+      // the target's tuple index (its state from the window slot: targets lie in the window)
+      const uint32_t tslot = (tx >> 1) / LC;
+      const uint32_t tstate = slo + ((tslot - slo) & wmask);
+      const uint32_t tg = 2 * gix((tx >> 1) - tslot * LC, tstate) + (tx & 1);
       const double nd = act ? w_times(dcur, S.w[lane]) : 0.0;
       S.nd[lane] = nd;
       const uint4 rv = act ? R[tx] : make_uint4(0, 0, kLdUntouched, 0);
@@ -479,7 +469,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       bool took = false;
       if (leader) {
         if (!untouched && bprev == pid) {  // back set earlier in this pop: its labels
-          const uint32_t a0 = back[(rv.z & ~kLdSettled)].y;
+          const uint32_t a0 = aoff + (bk_get(tg) >> (1 + dbits));
           bil = rhs.il[a0];
           bol = rhs.rec[a0].olabel;
         }
@@ -507,28 +497,17 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const unsigned long long fm = __ballot(fresh);
       const uint32_t id = fresh ? nn + (uint32_t)__popcll(fm & lanemask_lt()) : (rv.z & ~kLdSettled);
       nn += (uint32_t)__popcll(fm);
-      // a new id pushes id - LS out of the live span: that id must not be open at dcur
-      // (one open above dcur is checked when it joins the bitmap), nor may a tie re-open
-      // an id outside the span
-      const uint32_t oid = id - LS;
-      bool clash = fresh && id >= LS && ((bm[(oid & rmask) >> 6] >> (oid & 63)) & 1ull);
+      // the live span: every id open at dcur is >= pid (pops go in id order) or was
+      // re-opened by this pop (checked below); one open above dcur is checked when it joins
+      // the bitmap.  So the span holds while the newest id stays below pid + LS.
+      bool clash = (uint64_t)pid + LS <= nn;
       const bool settled = !untouched && (rv.z & kLdSettled);
       if (took) {
         R[tx] = ld_rec(cd, untouched ? id : rv.z, pid);
-        back[id] = make_uint2(pid, ba);
+        bk_put(tg, (x & 1) | ((tstate - s) << 1) | ((ba - aoff) << (1 + dbits)));
         if (fresh) {
           idr[id & rmask] = tx;
-          S.ring[id & (kLdRing - 1)] = tx;
-        }
-      }
-      {  // open tuples per window state: one add per distinct state slot
-        const uint32_t ts = (tx >> 1) / LC;
-        unsigned long long pend = fm;
-        while (pend) {
-          const uint32_t sl = lane_read(ts, (uint32_t)__ffsll((long long)pend) - 1);
-          const unsigned long long m = __ballot(fresh && ts == sl);
-          pend &= ~m;
-          if (lane == 0) cnt[sl] += (uint32_t)__popcll(m);
+          S.ring[id & (kLbRing - 1)] = tx;
         }
       }
       // push (:136-140): open at dcur -> bitmap, above -> future list.  An equal-dist
@@ -543,7 +522,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       bucket_insert(tob, id);
       wave_fence();
       wave_lds_sync();
-      if (__ballot(clash) || (uint64_t)nn >= ws.idcap) {
+      if (__ballot(clash)) {
         fail = kPathOverflow;
         site = 5;
         dbg_s = s;
@@ -559,7 +538,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     for (int i = 0; i < 6; ++i) prof[300 + i] += tacc[i];
 #endif
 
-  // ---- result (:368-400): the back chain by id ----
+  // ---- result (:368-400): the back chain, walked by tuple ----
   ld_drain();
   uint32_t P = 0;
   unsigned long long o = 0;
@@ -570,18 +549,22 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       if (best_id == kNoState) {
         st = kPathEmpty;
       } else {
-        uint32_t cur = best_id;
-        while (cur != 0) {  // init_id == 0
-          const uint32_t prev = back[cur].x;
-          if (prev == kLdNoPrev) {
-            st = kPathEmpty;
-            break;
-          }
+        // by tuple: the start tuple (0, start, 0) is id 0 (init_id, :372)
+        const uint32_t g0 = 2 * gix(0, rhs.start);
+        auto step = [&](uint32_t g_, uint32_t& a_) -> uint32_t {  // g_'s back source tuple
+          const uint32_t c = bk_get(g_);
+          const uint32_t st_ = (g_ >> 1) / LC, kk_ = (g_ >> 1) - st_ * LC;
+          const uint32_t sp_ = st_ - ((c >> 1) & dmask);
+          a_ = rhs.span[sp_].x + (c >> (1 + dbits));
+          return 2 * gix(kk_ - ((g_ & 1) ? 0u : 1u), sp_) + (c & 1);
+        };
+        uint32_t cur = best_g, arc = 0;
+        while (cur != g0) {
           if (++P > nn) {
             st = kPathCycle;
             break;
           }
-          cur = prev;
+          cur = step(cur, arc);
         }
         if (st == kPathOk) {
           o = atomicAdd(out.cursor, (unsigned long long)P);
@@ -589,16 +572,15 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
             st = kPathOutputFull;
           } else {
             uint32_t kk = P;
-            cur = best_id;
-            while (cur != 0 && kk > 0) {
-              const uint2 b = back[cur];
-              const uint32_t il = rhs.il[b.y];
-              const ArcRec r = rhs.rec[b.y];
+            cur = best_g;
+            while (cur != g0 && kk > 0) {
+              cur = step(cur, arc);
+              const uint32_t il = rhs.il[arc];
+              const ArcRec r = rhs.rec[arc];
               --kk;
               out.out_il[o + kk] = il;
               out.out_ol[o + kk] = r.olabel;
               out.out_w[o + kk] = il == kEpsilon ? r.weight : w_times(w_one(), r.weight);
-              cur = b.x;
             }
             fin = best_fw;
           }
@@ -639,7 +621,6 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   wave_fence();
   for (uint32_t i = lane; i < WS * LC * 2; i += 64) Rw[4 * (size_t)i + 2] = kLdUntouched;
   for (uint32_t i = lane; i < nbw; i += 64) bm[i] = 0ull;
-  for (uint32_t i = lane; i < WS; i += 64) cnt[i] = 0u;
   wave_fence();
   wave_lds_sync();
 }
@@ -648,20 +629,18 @@ __global__ void __launch_bounds__(64)
 lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item, LbWs ws,
                  BatchOutDev out) {
   extern __shared__ unsigned long long lb_dyn[];
-  __shared__ LdLds S;
+  __shared__ LbLds S;
   unsigned long long* bm = lb_dyn;                        // [ring / 64] open-at-dcur bitmap
-  uint32_t* cnt = (uint32_t*)(lb_dyn + ws.ring / 64);     // [ws] open tuples per window state
-  uint32_t* lab = cnt + ws.ws;                            // [lcap] the string's labels
+  uint32_t* lab = (uint32_t*)(lb_dyn + ws.ring / 64);     // [lcap] the string's labels
   const uint32_t lane = threadIdx.x;
   const size_t w = blockIdx.x;
   uint4* R = ws.win + w * ws.wn;
-  uint2* back = ws.back + w * ws.idcap;
+  void* bk = (void*)((uint8_t*)ws.bk + w * ws.tn * ws.bkb);
   uint32_t* idr = ws.idr + w * (size_t)ws.ring;
   uint4* fut = ws.fut + w * (size_t)ws.fcap;
   unsigned long long* prof = ws.prof ? ws.prof + w * kLbProf : nullptr;
 
   for (uint32_t i = lane; i < ws.ring / 64; i += 64) bm[i] = 0ull;
-  for (uint32_t i = lane; i < ws.ws; i += 64) cnt[i] = 0u;
   wave_lds_sync();
 
   const uint32_t num_items = ws.items ? ws.num_items : in.num_strings;
@@ -697,7 +676,7 @@ lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next
     if (pre != kPathOk) {
       if (lane == 0) write_status(out, si, pre, 0, 0);
     } else {
-      lazy_band_string(rhs, in, ws, out, R, back, idr, fut, bm, cnt, lab, S, prof, si, L);
+      lazy_band_string(rhs, in, ws, out, R, bk, idr, fut, bm, lab, S, prof, si, L);
     }
   }
 }
