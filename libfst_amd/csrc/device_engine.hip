@@ -1299,12 +1299,14 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   if (const char* we = std::getenv("FSTAMD_BAND_WAVES_PER_CU")) wpc = (uint32_t)std::max(1, std::atoi(we));
   const uint32_t max_waves = (uint32_t)num_cus_ * wpc;
   const char* ge = std::getenv("FSTAMD_DENSE_GRID");
+  const char* wse = std::getenv("FSTAMD_BAND_WS");  // tests: a window too small (overflows)
   auto make_plan = [&](uint32_t max_len, uint32_t count, Plan& p) -> bool {
     p.lcap = std::max<uint32_t>(max_len, 1);
     if (p.lcap > 4095) return false;
     uint32_t w = 64;
     const uint64_t want = 2ull * (p.lcap + 1) + 2ull * (rhs.view.jump_fwd + 1);
     while (w < want) w <<= 1;
+    if (wse) w = std::max<uint32_t>(64, 1u << (31 - __builtin_clz((uint32_t)std::max(1, std::atoi(wse)))));
     p.wstates = w;
     p.wn = (uint64_t)w * (p.lcap + 1) * 2;
     p.tn = (uint64_t)(p.lcap + 1) * NS * 2;  // ids and tuple indices fit 31 bits
