@@ -305,6 +305,8 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     const uint32_t aoff = sp.x, na = sp.y;
     uint32_t C = 0, lo1 = 0, n1 = 0, lo3 = 0, tmax = s;
     const bool small = na <= 64;
+    // the targets' largest state only matters near the window's end (t - s <= jump_fwd)
+    const bool near_end = (uint64_t)s + rhs.jump_fwd >= (uint64_t)slo + WS;
     if (small) {
       const bool v = lane < na;
       const uint32_t il = v ? rhs.il[aoff + lane] : 0xFFFFFFFFu;
@@ -314,7 +316,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const unsigned long long m1 = __ballot(p1), m3 = __ballot(p3);
       n1 = (uint32_t)__popcll(m1);
       C = n1 + (uint32_t)__popcll(m3);
-      tmax = max(tmax, __ockl_wfred_max_u32((p1 || p3) ? r.next : 0u));
+      if (near_end) tmax = max(tmax, __ockl_wfred_max_u32((p1 || p3) ? r.next : 0u));
       if (p1 || p3) {  // (a window index does not depend on slo: valid after any slide)
         const uint32_t rank = p1 ? (uint32_t)__popcll(m1 & lanemask_lt())
                                  : n1 + (uint32_t)__popcll(m3 & lanemask_lt());
@@ -333,11 +335,13 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       }
       span_by_ilabel(rhs, s, kEpsilon, lo3, hi);
       C = n1 + (hi - lo3);
-      for (uint32_t c = lane; c < C; c += 64) {
-        const uint32_t a = c < n1 ? lo1 + c : lo3 + (c - n1);
-        tmax = max(tmax, rhs.rec[a].next);
+      if (near_end) {
+        for (uint32_t c = lane; c < C; c += 64) {
+          const uint32_t a = c < n1 ? lo1 + c : lo3 + (c - n1);
+          tmax = max(tmax, rhs.rec[a].next);
+        }
+        tmax = __ockl_wfred_max_u32(tmax);
       }
-      tmax = __ockl_wfred_max_u32(tmax);
     }
     tmax = uni(tmax);
     relax += C;
