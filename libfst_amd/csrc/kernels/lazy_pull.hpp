@@ -474,7 +474,25 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           vary = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(dv >> 32)) << 32) |
                  (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)dv);
         }
-        if (counting) {
+        // already in order (the metric's layers, every one of them): the id order is the
+        // pop order and the identity ranks written in P3 stand
+        bool unsorted = false;
+#pragma unroll
+        for (int e = 0; e < EW; ++e) {
+          if ((uint32_t)e >= rows_s) continue;  // uniform
+          const uint32_t q = (uint32_t)e * 64 + lane;
+          if (q + 1 < n_next) {
+            const uint32_t a = S.ord0[q], b2 = S.ord0[q + 1];
+            if (ik) {
+              unsorted |= (a >> 9) > (b2 >> 9);
+            } else {
+              unsorted |= S.d[a & 511u] > S.d[b2 & 511u];
+            }
+          }
+        }
+        const bool in_order = !__ballot(unsorted);
+        if (in_order) vary = 0;
+        else if (counting) {
           // stable counting sort, 64 ids at a time in id order: the lanes holding key b
           // meet in mask[b] (LDS OR), a lane's rank among them = the equal keys before
           // it in the chunk; hist[b] carries the count from earlier chunks.  One wave's
@@ -577,7 +595,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           cur ^= 1u;
           wave_lds_sync();
         }
-        for (uint32_t q = lane; q < n_next && !counting; q += 64) {  // pop rank q -> cell
+        for (uint32_t q = lane; q < n_next && !counting && !in_order; q += 64) {  // pop rank q -> cell
           const uint32_t sl = (cur ? S.ord1 : S.ord0)[q] & 511u;
           const unsigned long long rpw = S.rp[sl];
           S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
