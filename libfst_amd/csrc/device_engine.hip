@@ -1047,7 +1047,7 @@ hipError_t DeviceEngine::run_lazy_pull(const DeviceFst& rhs, const ChainInput& i
   // kChaseBatch back slabs per wave, kPullW slots per layer (as tier P)
   const uint32_t back_cap =
       (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * kPullW, 1u << 22);
-  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)lazy_pull_waves_per_cu(rhs) * num_cus_,
+  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)lazy_pull_waves_per_cu(rhs, in.max_len) * num_cus_,
                                                in.num_strings);
   while (grid > 1 && (uint64_t)grid * kChaseBatch * back_cap * 8 > (24ull << 30)) grid /= 2;
   grid = std::max<uint32_t>(grid, 1);

@@ -98,6 +98,7 @@ struct DeviceFst {
   // within a same-ilabel run, candidate order = olabel order (relax's (id, il, ol) rule
   // then reduces to (id, candidate))
   bool lazy_pull_ok = false;
+  double int_wmax = -1.0;    // largest arc weight when every one is an integer >= 0, else -1
   // Routing hints learnt from earlier batches on this rhs: a small-lattice (LDS) tier that
   // handed on nearly every string is skipped next time (config 3's lattices never fit).
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};
@@ -206,7 +207,8 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
                              unsigned int* next_item, const EagerLaunch& lp,
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream);
 // Lazy pull tier (eager_pull.hip, kernels/lazy_pull.hpp): resident waves per CU, launch.
-int lazy_pull_waves_per_cu(const DeviceFst& rhs);
+int lazy_pull_waves_per_cu(const DeviceFst& rhs, uint32_t max_len);
+bool lazy_pull_f32(const DeviceFst& rhs, uint32_t max_len);
 hipError_t launch_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
                             unsigned int* next_item, const EagerLaunch& lp,
                             const BatchOutDev& out, uint32_t grid, hipStream_t stream);

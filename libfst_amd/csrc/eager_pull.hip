@@ -33,19 +33,31 @@ const void* pull_kernel_for(const RevView& rv) {
     default: return pull_kernel_ptr<8, 4>(dir);
   }
 }
+// Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 4 with f32 cells (10.2 KB)
+// when every distance is an integer below 2^24.
+#ifndef FSTAMD_LP_WAVES_F32  // A/B builds
+#define FSTAMD_LP_WAVES_F32 4
+#endif
 constexpr int kLazyPullWaves = 3;
-template <int KP>
+template <int KP, bool F32>
 const void* lazy_pull_ptr(bool direct) {
-  return direct ? (const void*)lazy_pull_kernel<kPullRows, KP, true, kLazyPullWaves>
-                : (const void*)lazy_pull_kernel<kPullRows, KP, false, kLazyPullWaves>;
+  constexpr int wv = (F32 && KP <= 5) ? FSTAMD_LP_WAVES_F32 : kLazyPullWaves;  // 8-record
+                                                                           // blocks spill at 4
+  return direct ? (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, F32>
+                : (const void*)lazy_pull_kernel<kPullRows, KP, false, wv, F32>;
 }
+template <bool F32>
 const void* lazy_pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
   switch (rv.kp) {
-    case 4: return lazy_pull_ptr<4>(dir);
-    case 5: return lazy_pull_ptr<5>(dir);
-    default: return lazy_pull_ptr<8>(dir);
+    case 4: return lazy_pull_ptr<4, F32>(dir);
+    case 5: return lazy_pull_ptr<5, F32>(dir);
+    default: return lazy_pull_ptr<8, F32>(dir);
   }
+}
+const void* lazy_pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
+  return lazy_pull_f32(rhs, max_len) ? lazy_pull_kernel_for<true>(rhs.rev)
+                                     : lazy_pull_kernel_for<false>(rhs.rev);
 }
 }  // namespace
 
@@ -207,6 +219,14 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
                    direct ? 1u : 0u};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
+  // integer arc weights: the lazy pull may keep its cells' distances as f32 (exact below
+  // 2^24; lazy_pull_f32 checks L * int_wmax per launch)
+  d->int_wmax = 0.0;
+  for (uint32_t a = 0; a < na && d->int_wmax >= 0.0; ++a) {
+    const double w = pa[a].weight;
+    if (!(w >= 0.0) || w != __builtin_trunc(w) || w >= 16777216.0) d->int_wmax = -1.0;
+    else d->int_wmax = std::max(d->int_wmax, w);
+  }
   return true;
 }
 
@@ -226,9 +246,14 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
   return hipLaunchKernel(pull_kernel_for(rhs.rev), dim3(grid), dim3(64), args, 0, stream);
 }
 
-int lazy_pull_waves_per_cu(const DeviceFst& rhs) {
+bool lazy_pull_f32(const DeviceFst& rhs, uint32_t max_len) {
+  return rhs.int_wmax >= 0.0 && (double)max_len * rhs.int_wmax < 16777216.0 &&
+         !std::getenv("FSTAMD_LP_F64");
+}
+
+int lazy_pull_waves_per_cu(const DeviceFst& rhs, uint32_t max_len) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lazy_pull_kernel_for(rhs.rev), 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lazy_pull_kernel_for(rhs, max_len), 64, 0) !=
       hipSuccess)
     occ = 1;
   return std::max(occ, 1);
@@ -239,7 +264,8 @@ hipError_t launch_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t
                             const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
   void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
                   (void*)&next_item, (void*)&lp, (void*)&out};
-  return hipLaunchKernel(lazy_pull_kernel_for(rhs.rev), dim3(grid), dim3(64), args, 0, stream);
+  return hipLaunchKernel(lazy_pull_kernel_for(rhs, in.max_len), dim3(grid), dim3(64), args, 0,
+                         stream);
 }
 
 }  // namespace fstamd

@@ -29,6 +29,8 @@
 // takes it.
 #pragma once
 
+#include <type_traits>
+
 #include "eager_pull.hpp"  // RevView helpers, pull_group, wave_incl_scan_dpp, ChaseJob
 
 extern "C" __device__ double __ockl_wfred_min_f64(double);
@@ -41,15 +43,19 @@ constexpr uint32_t kLpAbsent = 0xFFF00000u;  // rank words of a slot that holds 
 constexpr uint32_t kLpRunMask = 0xFFFu;      // run (<= 4095 layers) below the pop rank
 constexpr uint32_t kLpMaxLen = 4095;
 constexpr int kLpBins = 256;  // counting sort of the pop order: integer keys d - dmin < 256
+constexpr int kLpChase = 15;  // backtraces batched per wave (<= kChaseBatch: slabs)
 
-template <int W>
+// DT: the cells' distance storage.  double in general; float when every distance is an
+// integer below 2^24 (integer arc weights with L * max weight < 2^24, checked on the host:
+// DeviceFst::int_wmax), which is exact and saves 2.5 KB, so 4 waves fit per SIMD.
+template <int W, typename DT>
 struct LazyPullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys p << 3 | j < 8 W
   // the current layer's cells (slot W never holds a tuple), 8-B arrays addressed by one
   // byte offset
-  double d[W + 1];                 // distance (+inf: no tuple)
+  DT d[W + 1];                     // distance (+inf: no tuple)
   unsigned long long rp[W + 1];    // lo: id rank << 20; hi: pop rank << 20 | run
-  double tb[W + 1];                // distance of the first toucher (-1: the start)
+  DT tb[W + 1];                    // distance of the first toucher (-1: the start)
   uint32_t ord0[W];                // (key << 9 |) slot in id order
   // P1-P3 and the split sort use {bits, pre, ord1}; the counting sort overlays {mask,
   // hist} on them (bits lies under mask, which the counting sort leaves all zero)
@@ -66,17 +72,31 @@ struct LazyPullLds {
   };
   unsigned long long best;
   uint32_t bestp;
-  ChaseJob job[kChaseBatch];
+  ChaseJob job[kLpChase];
 };
 
-template <int EW, int KP, bool DIRECT, int WAVES_PER_EU>
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, bool F32>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
 lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                  unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
-  constexpr int kWords = LazyPullLds<W>::kWords;
+  using DT = typename std::conditional<F32, float, double>::type;
+  constexpr int kWords = LazyPullLds<W, DT>::kWords;
   static_assert(KP <= 16 && W < 512, "key layout as in eager_pull.hpp");
-  __shared__ LazyPullLds<W> S;
+  __shared__ LazyPullLds<W, DT> S;
+  // a cell's distance / first-toucher distance by the 8-B-cell byte offset o of the rp array
+  auto cell_d = [&](uint32_t o) -> double {
+    return (double)*reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.d) +
+                                                (F32 ? (o >> 1) : o));
+  };
+  auto cell_tb = [&](uint32_t o) -> double {
+    return (double)*reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.tb) +
+                                                (F32 ? (o >> 1) : o));
+  };
+#ifdef FSTAMD_LP_PAD  // occupancy experiment only: LDS padding to cut waves per SIMD
+  __shared__ uint32_t pad_[FSTAMD_LP_PAD];
+  if (threadIdx.x == 1000) pad_[0] = 0;
+#endif
   const uint32_t lane = threadIdx.x;
   const double kInf = __builtin_huge_val();
   const unsigned long long kAbsent2 = ((unsigned long long)kLpAbsent << 32) | kLpAbsent;
@@ -125,9 +145,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-    S.d[i] = kInf;
+    S.d[i] = (DT)kInf;
     S.rp[i] = kAbsent2;
-    S.tb[i] = kInf;
+    S.tb[i] = (DT)kInf;
   }
   if (lane < (uint32_t)kWords) S.bits[lane] = 0;
   wave_lds_sync();
@@ -156,15 +176,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     // layer 0: the start tuple (id 0, pop rank 0, tb -1 < every distance)
 #pragma unroll 1
     for (uint32_t i = lane; i < wlast; i += 64) {
-      S.d[i] = kInf;
+      S.d[i] = (DT)kInf;
       S.rp[i] = kAbsent2;
-      S.tb[i] = kInf;
+      S.tb[i] = (DT)kInf;
     }
     wave_lds_sync();
     if (lane == 0) {
-      S.d[0] = w_one();
+      S.d[0] = (DT)w_one();
       S.rp[0] = 0;
-      S.tb[0] = -1.0;
+      S.tb[0] = (DT)-1.0;
     }
     wave_lds_sync();
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
@@ -243,7 +263,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
           const uint32_t o = min(rr[m].src - tmin8, 8u * W);
-          const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + o);
+          const double d = cell_d(o);
           const unsigned long long rpw =
               *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
           nd[m] = d + rr[m].weight;  // times(d, w) for finite w >= 0 (:108)
@@ -265,7 +285,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             for (int m = 0; m < KP; ++m) {
               const RevRec r2 = rv.rrec[rxx + m];
               const uint32_t o = min(r2.src - tmin8, 8u * W);
-              const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + o);
+              const double d = cell_d(o);
               const unsigned long long rpw =
                   *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
               const double n2 = d + r2.weight;
@@ -286,15 +306,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const bool pres = ff < kLpAbsent;
         // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
         const uint32_t ou = pres ? (ff & 0x1FFFu) : 8u * W;
-        const double du = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + ou);
-        const double tbu = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + ou);
+        const double du = cell_d(ou);
+        const double tbu = cell_tb(ou);
         const uint32_t ruu =
             (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ou) >> 32) &
             kLpRunMask;
         // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
         // round trip: its certificate alone usually settles C
         const uint32_t ob = pres ? (c & 0x1FFFu) : 8u * W;
-        const double tbb = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + ob);
+        const double tbb = cell_tb(ob);
         const uint32_t rbb =
             (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ob) >> 32) &
             kLpRunMask;
@@ -320,7 +340,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
             const uint32_t o = bpk[m] & 0x1FFFu;
-            const double tbm = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + o);
+            const double tbm = cell_tb(o);
             const uint32_t rm =
                 (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
                 kLpRunMask;
@@ -334,8 +354,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               for (int m = 0; m < KP; ++m) {
                 const RevRec r2 = rv.rrec[rxx + m];
                 const uint32_t o = min(r2.src - tmin8, 8u * W);
-                const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + o);
-                const double tbm = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.tb) + o);
+                const double d = cell_d(o);
+                const double tbm = cell_tb(o);
                 const uint32_t rm =
                     (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
                     kLpRunMask;
@@ -417,8 +437,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
-        S.d[i] = pres ? bd[e] : kInf;
-        S.tb[i] = pres ? tbx[e] : kInf;
+        S.d[i] = (DT)(pres ? bd[e] : kInf);
+        S.tb[i] = (DT)(pres ? tbx[e] : kInf);
         // pop rank: identity until the sort below fills it in
         S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
         if (pres && sort) {
@@ -486,7 +506,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             if (ik) {
               unsorted |= (a >> 9) > (b2 >> 9);
             } else {
-              unsorted |= S.d[a & 511u] > S.d[b2 & 511u];
+              unsorted |= (double)S.d[a & 511u] > (double)S.d[b2 & 511u];
             }
           }
         }
@@ -570,7 +590,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               v[e] = (el[e] >> bit) & 1u;
             } else {
               const unsigned long long key =
-                  (unsigned long long)__double_as_longlong(S.d[el[e] & 511u]);
+                  (unsigned long long)__double_as_longlong((double)S.d[el[e] & 511u]);
               v[e] = (uint32_t)(key >> bit) & 1u;
             }
             z[e] = __ballot(valid && !v[e]);
@@ -617,9 +637,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       wave_lds_sync();
 #pragma unroll 1
       for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-        S.d[i] = kInf;
+        S.d[i] = (DT)kInf;
         S.rp[i] = kAbsent2;
-        S.tb[i] = kInf;
+        S.tb[i] = (DT)kInf;
       }
       if (lane < (uint32_t)kWords) S.bits[lane] = 0;
       wave_lds_sync();
@@ -660,7 +680,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       j.off = off;
       j.fw = fw2;
     }
-    if (++njobs == (uint32_t)kChaseBatch) chase_batch();
+    if (++njobs == (uint32_t)kLpChase) chase_batch();
   }
   if (njobs) chase_batch();
 }
