@@ -35,6 +35,8 @@
 
 extern "C" __device__ double __ockl_wfred_min_f64(double);
 extern "C" __device__ double __ockl_wfred_max_f64(double);
+extern "C" __device__ float __ockl_wfred_min_f32(float);
+extern "C" __device__ float __ockl_wfred_max_f32(float);
 extern "C" __device__ unsigned long long __ockl_wfred_or_u64(unsigned long long);
 
 namespace fstamd {
@@ -80,25 +82,25 @@ __global__ void __launch_bounds__(64, WAVES_PER_EU)
 lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                  unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
+  // DT: the distance type of cells and of the merge's arithmetic (f32: exact for the
+  // integer distances below 2^24 the host checked)
   using DT = typename std::conditional<F32, float, double>::type;
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
   static_assert(KP <= 16 && W < 512, "key layout as in eager_pull.hpp");
   __shared__ LazyPullLds<W, DT> S;
   // a cell's distance / first-toucher distance by the 8-B-cell byte offset o of the rp array
-  auto cell_d = [&](uint32_t o) -> double {
-    return (double)*reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.d) +
-                                                (F32 ? (o >> 1) : o));
+  auto cell_d = [&](uint32_t o) -> DT {
+    return *reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.d) + (F32 ? (o >> 1) : o));
   };
-  auto cell_tb = [&](uint32_t o) -> double {
-    return (double)*reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.tb) +
-                                                (F32 ? (o >> 1) : o));
+  auto cell_tb = [&](uint32_t o) -> DT {
+    return *reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.tb) + (F32 ? (o >> 1) : o));
   };
 #ifdef FSTAMD_LP_PAD  // occupancy experiment only: LDS padding to cut waves per SIMD
   __shared__ uint32_t pad_[FSTAMD_LP_PAD];
   if (threadIdx.x == 1000) pad_[0] = 0;
 #endif
   const uint32_t lane = threadIdx.x;
-  const double kInf = __builtin_huge_val();
+  const DT kInf = (DT)__builtin_huge_val();
   const unsigned long long kAbsent2 = ((unsigned long long)kLpAbsent << 32) | kLpAbsent;
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;
@@ -145,9 +147,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-    S.d[i] = (DT)kInf;
+    S.d[i] = kInf;
     S.rp[i] = kAbsent2;
-    S.tb[i] = (DT)kInf;
+    S.tb[i] = kInf;
   }
   if (lane < (uint32_t)kWords) S.bits[lane] = 0;
   wave_lds_sync();
@@ -176,9 +178,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     // layer 0: the start tuple (id 0, pop rank 0, tb -1 < every distance)
 #pragma unroll 1
     for (uint32_t i = lane; i < wlast; i += 64) {
-      S.d[i] = (DT)kInf;
+      S.d[i] = kInf;
       S.rp[i] = kAbsent2;
-      S.tb[i] = (DT)kInf;
+      S.tb[i] = kInf;
     }
     wave_lds_sync();
     if (lane == 0) {
@@ -220,7 +222,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
       // ---- (P1) pull merge per target: first toucher, distance, back-pointer, C ----
       uint32_t fst[EW], bk[EW], bra[EW], runx[EW];
-      double bd[EW], tbx[EW];
+      DT bd[EW], tbx[EW];
       bool uncert = false;
 #pragma unroll
       for (int e = 0; e < EW; ++e) {
@@ -257,16 +259,16 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
         for (int m = 0; m < KP; ++m) rr[m] = R[m];
         uint32_t bpk[KP];
-        double nd[KP];
+        DT nd[KP];
         uint32_t ff = kEmptyKey, wpos = 0;
-        double b = kInf;
+        DT b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
           const uint32_t o = min(rr[m].src - tmin8, 8u * W);
-          const double d = cell_d(o);
+          const DT d = cell_d(o);
           const unsigned long long rpw =
               *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
-          nd[m] = d + rr[m].weight;  // times(d, w) for finite w >= 0 (:108)
+          nd[m] = d + (DT)rr[m].weight;  // times(d, w) for finite w >= 0 (:108)
           bpk[m] = (uint32_t)rpw | rr[m].y | o;
           ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | rr[m].y | o);
           b = fmin(b, nd[m]);
@@ -285,10 +287,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             for (int m = 0; m < KP; ++m) {
               const RevRec r2 = rv.rrec[rxx + m];
               const uint32_t o = min(r2.src - tmin8, 8u * W);
-              const double d = cell_d(o);
+              const DT d = cell_d(o);
               const unsigned long long rpw =
                   *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
-              const double n2 = d + r2.weight;
+              const DT n2 = d + (DT)r2.weight;
               const uint32_t p2 = (uint32_t)rpw | r2.y | o;
               ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | r2.y | o);
               if (n2 < b || (n2 == b && p2 < c)) {
@@ -306,19 +308,19 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const bool pres = ff < kLpAbsent;
         // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
         const uint32_t ou = pres ? (ff & 0x1FFFu) : 8u * W;
-        const double du = cell_d(ou);
-        const double tbu = cell_tb(ou);
+        const DT du = cell_d(ou);
+        const DT tbu = cell_tb(ou);
         const uint32_t ruu =
             (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ou) >> 32) &
             kLpRunMask;
         // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
         // round trip: its certificate alone usually settles C
         const uint32_t ob = pres ? (c & 0x1FFFu) : 8u * W;
-        const double tbb = cell_tb(ob);
+        const DT tbb = cell_tb(ob);
         const uint32_t rbb =
             (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ob) >> 32) &
             kLpRunMask;
-        const double tx = du;
+        const DT tx = du;
         const uint32_t rx = 1u + (tbu == tx ? ruu : 0u);
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
         // source certified by (tb, run).  The back source is tight, so its certificate is
@@ -340,7 +342,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
             const uint32_t o = bpk[m] & 0x1FFFu;
-            const double tbm = cell_tb(o);
+            const DT tbm = cell_tb(o);
             const uint32_t rm =
                 (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
                 kLpRunMask;
@@ -354,12 +356,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               for (int m = 0; m < KP; ++m) {
                 const RevRec r2 = rv.rrec[rxx + m];
                 const uint32_t o = min(r2.src - tmin8, 8u * W);
-                const double d = cell_d(o);
-                const double tbm = cell_tb(o);
+                const DT d = cell_d(o);
+                const DT tbm = cell_tb(o);
                 const uint32_t rm =
                     (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
                     kLpRunMask;
-                cert |= d + r2.weight == b &&
+                cert |= d + (DT)r2.weight == b &&
                         (r2.weight > 0.0 || tbm < tx || (tbm == tx && rm < rx));
               }
             }
@@ -405,22 +407,27 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // P4's sort keys from the distances still in registers ----
       const bool last = k + 1 == L;
       const bool sort = !last && n_next > 1;  // the last layer's pop order is never used
-      double mn = kInf, mx = -kInf;
+      DT mn = kInf, mx = -kInf;
       bool nonint = false;
 #pragma unroll
       for (int e = 0; e < EW; ++e) {
         if ((uint32_t)e >= rows_n || fst[e] >= kLpAbsent) continue;
         mn = fmin(mn, bd[e]);
         mx = fmax(mx, bd[e]);
-        nonint |= bd[e] != __builtin_trunc(bd[e]);
+        if (!F32) nonint |= bd[e] != __builtin_trunc(bd[e]);
       }
       bool ik = false;  // integer distances with d - dmin < 2^23: keys d - dmin
       if (sort) {
-        mn = __ockl_wfred_min_f64(mn);
-        mx = __ockl_wfred_max_f64(mx);
-        ik = __ballot(nonint) == 0 && mx - mn < 8388608.0;
+        if constexpr (F32) {
+          mn = __ockl_wfred_min_f32(mn);
+          mx = __ockl_wfred_max_f32(mx);
+        } else {
+          mn = __ockl_wfred_min_f64(mn);
+          mx = __ockl_wfred_max_f64(mx);
+        }
+        ik = __ballot(nonint) == 0 && (double)mx - (double)mn < 8388608.0;
       }
-      const unsigned long long mnb = (unsigned long long)__double_as_longlong(mn);
+      const unsigned long long mnb = (unsigned long long)__double_as_longlong((double)mn);
       uint32_t kacc = 0;            // OR of the integer keys
       unsigned long long diff = 0;  // OR of the f64 patterns' differences from dmin's
       const uint32_t rows_w = max(rows_n, (wk + 63) / 64);
@@ -437,15 +444,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
-        S.d[i] = (DT)(pres ? bd[e] : kInf);
-        S.tb[i] = (DT)(pres ? tbx[e] : kInf);
+        S.d[i] = pres ? bd[e] : kInf;
+        S.tb[i] = pres ? tbx[e] : kInf;
         // pop rank: identity until the sort below fills it in
         S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
         if (pres && sort) {
           const uint32_t key = ik ? (uint32_t)(bd[e] - mn) : 0u;  // exact: integers < 2^23
           S.ord0[rank] = (key << 9) | i;
           kacc |= key;
-          diff |= ik ? 0ull : (unsigned long long)__double_as_longlong(bd[e]) ^ mnb;
+          diff |= ik ? 0ull : (unsigned long long)__double_as_longlong((double)bd[e]) ^ mnb;
         }
         const unsigned long long pm = __ballot(pres);
         if (pm) {
@@ -458,7 +465,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 72)];
             if (!w_is_zero(fw2)) {
-              const unsigned long long kk = okey(bd[e] + fw2);
+              const unsigned long long kk = okey((double)bd[e] + fw2);
               const uint32_t pp = (rank << 9) | i;
               if (kk < mykey || (kk == mykey && pp < myp)) {
                 mykey = kk;
@@ -484,7 +491,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #ifdef FSTAMD_LP_SPLIT_ONLY  // A/B: the split sort for every layer
         const bool counting = false;
 #else
-        const bool counting = ik && mx - mn < (double)kLpBins;
+        const bool counting = ik && mx - mn < (DT)kLpBins;
 #endif
         unsigned long long vary;
         if (ik) {
@@ -506,7 +513,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             if (ik) {
               unsorted |= (a >> 9) > (b2 >> 9);
             } else {
-              unsorted |= (double)S.d[a & 511u] > (double)S.d[b2 & 511u];
+              unsorted |= S.d[a & 511u] > S.d[b2 & 511u];
             }
           }
         }
@@ -637,9 +644,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       wave_lds_sync();
 #pragma unroll 1
       for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-        S.d[i] = (DT)kInf;
+        S.d[i] = kInf;
         S.rp[i] = kAbsent2;
-        S.tb[i] = (DT)kInf;
+        S.tb[i] = kInf;
       }
       if (lane < (uint32_t)kWords) S.bits[lane] = 0;
       wave_lds_sync();
