@@ -493,16 +493,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #else
         const bool counting = ik && mx - mn < (DT)kLpBins;
 #endif
-        unsigned long long vary;
-        if (ik) {
-          vary = (unsigned long long)__builtin_amdgcn_readfirstlane(__ockl_wfred_or_u32(kacc)) << 9;
-        } else {
-          const unsigned long long dv = __ockl_wfred_or_u64(diff);
-          vary = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(dv >> 32)) << 32) |
-                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)dv);
-        }
         // already in order (the metric's layers, every one of them): the id order is the
-        // pop order and the identity ranks written in P3 stand
+        // pop order and the identity ranks written in P3 stand; nothing below runs
         bool unsorted = false;
 #pragma unroll
         for (int e = 0; e < EW; ++e) {
@@ -518,8 +510,16 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           }
         }
         const bool in_order = !__ballot(unsorted);
-        if (in_order) vary = 0;
-        else if (counting) {
+        if (!in_order) {
+        unsigned long long vary;
+        if (ik) {
+          vary = (unsigned long long)__builtin_amdgcn_readfirstlane(__ockl_wfred_or_u32(kacc)) << 9;
+        } else {
+          const unsigned long long dv = __ockl_wfred_or_u64(diff);
+          vary = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(dv >> 32)) << 32) |
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)dv);
+        }
+        if (counting) {
           // stable counting sort, 64 ids at a time in id order: the lanes holding key b
           // meet in mask[b] (LDS OR), a lane's rank among them = the equal keys before
           // it in the chunk; hist[b] carries the count from earlier chunks.  One wave's
@@ -622,12 +622,13 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           cur ^= 1u;
           wave_lds_sync();
         }
-        for (uint32_t q = lane; q < n_next && !counting && !in_order; q += 64) {  // pop rank q -> cell
+        for (uint32_t q = lane; q < n_next && !counting; q += 64) {  // pop rank q -> cell
           const uint32_t sl = (cur ? S.ord1 : S.ord0)[q] & 511u;
           const unsigned long long rpw = S.rp[sl];
           S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
         }
         wave_lds_sync();
+        }  // !in_order
       }
       tmin = tn;
       base = nbase;
