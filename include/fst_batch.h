@@ -96,7 +96,11 @@ void fst_batch_result_free(FstBatchResult* r);
 /* Device-resident batch: every pointer is device memory on opts->device; the call is
  * asynchronous on `stream` (a hipStream_t, or NULL for the null stream).  Paths are
  * appended to the arc arena; *arc_cursor (device) is reset by the call.  `work`, if
- * non-NULL, receives two counters per string: product states and relaxations. */
+ * non-NULL, receives two counters per string: product states and relaxations.
+ * max_len (fst_device_compose_shortest_path) is the caller's bound on the strings'
+ * lengths: it sizes workspaces and picks kernels (e.g. f32 cells when every distance
+ * stays an exact integer below 2^24).  A string longer than max_len is still answered
+ * exactly, by a slower tier. */
 typedef struct {
     int32_t* status;            /* [num_strings] */
     uint32_t* path_len;         /* [num_strings] */

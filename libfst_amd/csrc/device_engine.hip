@@ -637,7 +637,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     uint2* back_p = nullptr;
     uint32_t* list_pw = nullptr;
     if (use_p) {
-      grid_p = (uint32_t)std::min<uint64_t>((uint64_t)pull_waves_per_cu(rhs) * num_cus_,
+      grid_p = (uint32_t)std::min<uint64_t>((uint64_t)pull_waves_per_cu(rhs, in.max_len) * num_cus_,
                                             in.num_strings);
       while (grid_p > 1 && (uint64_t)grid_p * kChaseBatch * back_cap_w * 8 > (24ull << 30))
         grid_p /= 2;

@@ -74,6 +74,10 @@ struct RevView {
   uint32_t gsearch;       // binary-search steps over the longest gtab run (0: no gtab)
   uint32_t direct;        // 1: block 0 of state t at record t * kp (every state has at most
                           // one in-label group); rspan.x = the record of its block 1
+  // [nblocks * kp] the same records with an f32 weight and the olabel: {src, y, f32 bits of
+  // the weight, olabel}; only when every arc weight is an integer in [0, 2^24) (exact in
+  // f32; DeviceFst::int_wmax), else null
+  const uint4* rrec32;
 };
 
 struct DeviceFst {
@@ -103,7 +107,7 @@ struct DeviceFst {
   // handed on nearly every string is skipped next time (config 3's lattices never fit).
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};
   RevView rev{};
-  void* rev_bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* rev_bufs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a
   // breadth-first renumbering of an rhs with scattered ids (device_engine.hip
   // bfs_renumbering).  Every device view (RhsView, RevView) uses it; results do not.
@@ -202,7 +206,10 @@ constexpr uint32_t kPullW = 64 * kPullRows;
 bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f);
 void free_reverse_mirror(DeviceFst* d);
 // Resident waves per CU of the pull kernel for this rhs.
-int pull_waves_per_cu(const DeviceFst& rhs);
+int pull_waves_per_cu(const DeviceFst& rhs, uint32_t max_len);
+// f32 cells for the pull tiers: every distance of a string of <= max_len labels is an
+// integer below 2^24 (exact in f32)
+bool pull_f32(const DeviceFst& rhs, uint32_t max_len);
 hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n_best,
                              unsigned int* next_item, const EagerLaunch& lp,
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream);

@@ -17,21 +17,30 @@ namespace {
 // metric: 5 waves 20.3 M strings/s, 4 waves 18.5 M, 6 waves 19.8 M with spills);
 // 8-record blocks need 4.
 
-template <int KP, int WV>
+template <int KP, int WV, bool F32>
 const void* pull_kernel_ptr(bool direct) {
-  return direct ? (const void*)eager_pull_kernel<kPullRows, KP, true, WV>
-                : (const void*)eager_pull_kernel<kPullRows, KP, false, WV>;
+  return direct ? (const void*)eager_pull_kernel<kPullRows, KP, true, WV, F32>
+                : (const void*)eager_pull_kernel<kPullRows, KP, false, WV, F32>;
 }
 #ifndef FSTAMD_PULL_WAVES_SMALL  // A/B builds: waves per SIMD for blocks of <= 5 records
 #define FSTAMD_PULL_WAVES_SMALL 5
 #endif
+#ifndef FSTAMD_PULL_WAVES_F32  // A/B builds: the same with f32 cells (8-B cells, f32 merge)
+#define FSTAMD_PULL_WAVES_F32 6
+#endif
+template <bool F32>
 const void* pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
+  constexpr int wv = F32 ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
   switch (rv.kp) {
-    case 4: return pull_kernel_ptr<4, FSTAMD_PULL_WAVES_SMALL>(dir);
-    case 5: return pull_kernel_ptr<5, FSTAMD_PULL_WAVES_SMALL>(dir);
-    default: return pull_kernel_ptr<8, 4>(dir);
+    case 4: return pull_kernel_ptr<4, wv, F32>(dir);
+    case 5: return pull_kernel_ptr<5, wv, F32>(dir);
+    default: return pull_kernel_ptr<8, 4, F32>(dir);
   }
+}
+const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
+  return pull_f32(rhs, max_len) && !std::getenv("FSTAMD_P_F64") ? pull_kernel_for<true>(rhs.rev)
+                                                                 : pull_kernel_for<false>(rhs.rev);
 }
 // Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 4 with f32 cells (10.2 KB)
 // when every distance is an integer below 2^24.
@@ -200,6 +209,24 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   if (!gtab.empty())
     while ((1u << gsearch) < max_groups + 1) ++gsearch;
 
+  // integer arc weights in [0, 2^24): the pull tiers may keep their cells' distances in f32
+  // (exact while L * int_wmax < 2^24, pull_f32), reading the f32 copy of the records
+  d->int_wmax = 0.0;
+  for (uint32_t a = 0; a < na && d->int_wmax >= 0.0; ++a) {
+    const double w = pa[a].weight;
+    if (!(w >= 0.0) || w != __builtin_trunc(w) || w >= 16777216.0) d->int_wmax = -1.0;
+    else d->int_wmax = std::max(d->int_wmax, w);
+  }
+  std::vector<uint4> rrec32;
+  if (d->int_wmax >= 0.0) {
+    rrec32.resize(rrec.size());
+    for (size_t r = 0; r < rrec.size(); ++r) {
+      const float wf = (float)rrec[r].weight;  // exact: an integer below 2^24
+      uint32_t wb;
+      std::memcpy(&wb, &wf, 4);
+      rrec32[r] = make_uint4(rrec[r].src, rrec[r].y, wb, rolab[r]);
+    }
+  }
   auto up = [&](int i, const void* src_p, size_t bytes) -> bool {
     if (bytes == 0) bytes = 16;
     if (hipMalloc(&d->rev_bufs[i], bytes) != hipSuccess) return false;
@@ -210,29 +237,26 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   if (!up(0, rspan.data(), rspan.size() * sizeof(uint4)) ||
       !up(1, gtab.data(), gtab.size() * sizeof(uint4)) ||
       !up(2, rrec.data(), rrec.size() * sizeof(RevRec)) ||
-      !up(3, rolab.data(), rolab.size() * sizeof(uint32_t))) {
+      !up(3, rolab.data(), rolab.size() * sizeof(uint32_t)) ||
+      (!rrec32.empty() && !up(4, rrec32.data(), rrec32.size() * sizeof(uint4)))) {
     free_reverse_mirror(d);
     return false;
   }
   d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
-                   direct ? 1u : 0u};
+                   direct ? 1u : 0u, (const uint4*)d->rev_bufs[4]};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
-  // integer arc weights: the lazy pull may keep its cells' distances as f32 (exact below
-  // 2^24; lazy_pull_f32 checks L * int_wmax per launch)
-  d->int_wmax = 0.0;
-  for (uint32_t a = 0; a < na && d->int_wmax >= 0.0; ++a) {
-    const double w = pa[a].weight;
-    if (!(w >= 0.0) || w != __builtin_trunc(w) || w >= 16777216.0) d->int_wmax = -1.0;
-    else d->int_wmax = std::max(d->int_wmax, w);
-  }
   return true;
 }
 
-int pull_waves_per_cu(const DeviceFst& rhs) {
+bool pull_f32(const DeviceFst& rhs, uint32_t max_len) {
+  return rhs.int_wmax >= 0.0 && rhs.rev.rrec32 && (double)max_len * rhs.int_wmax < 16777216.0;
+}
+
+int pull_waves_per_cu(const DeviceFst& rhs, uint32_t max_len) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pull_kernel_for(rhs.rev), 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pull_kernel_for(rhs, max_len), 64, 0) !=
       hipSuccess)
     occ = 1;
   return std::max(occ, 1);
@@ -243,12 +267,11 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
   void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
                   (void*)&next_item, (void*)&lp, (void*)&out};
-  return hipLaunchKernel(pull_kernel_for(rhs.rev), dim3(grid), dim3(64), args, 0, stream);
+  return hipLaunchKernel(pull_kernel_for(rhs, in.max_len), dim3(grid), dim3(64), args, 0, stream);
 }
 
 bool lazy_pull_f32(const DeviceFst& rhs, uint32_t max_len) {
-  return rhs.int_wmax >= 0.0 && (double)max_len * rhs.int_wmax < 16777216.0 &&
-         !std::getenv("FSTAMD_LP_F64");
+  return pull_f32(rhs, max_len) && !std::getenv("FSTAMD_LP_F64");
 }
 
 int lazy_pull_waves_per_cu(const DeviceFst& rhs, uint32_t max_len) {

@@ -38,6 +38,8 @@
 // source}: the batched backtrace walks one dependent 8-B load per arc.
 #pragma once
 
+#include <type_traits>
+
 #include "device_common.hpp"
 #include "eager_layered.hpp"  // EagerLaunch, write_status
 #include "eager_wave.hpp"     // wave_lds_sync, wave_pick_best
@@ -48,7 +50,7 @@ namespace fstamd {
 constexpr uint32_t kPullAbsent = 0xFFFF0000u;  // rank word of a slot that holds no tuple
 
 
-template <int W>
+template <int W, bool F32 = false>
 struct PullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys rank << 3 | j < 8 W
   // the current layer's cells, slot W never holds a tuple.  Two arrays of 8-B entries
@@ -58,6 +60,18 @@ struct PullLds {
   unsigned long long rk[W + 1];    // rank << 20 (kPullAbsent: no tuple) in the low word
   unsigned long long bits[kWords];
   uint4 pre[kWords];                         // {prefix popcount, 0, word lo, word hi}
+  unsigned long long best;
+  uint32_t bestp;
+  ChaseJob job[kChaseBatch];
+};
+// f32 cells (every distance an integer below 2^24, exact): one 8-B cell {f32 distance,
+// rank word} per slot, read by one ds_read_b64 per in-arc; 4.3 KB instead of 6.9 KB
+template <int W>
+struct PullLds<W, true> {
+  static constexpr int kWords = W * 8 / 64;
+  uint2 cell[W + 1];               // {f32 bits of the distance (+inf: no tuple), rank << 20}
+  unsigned long long bits[kWords];
+  uint4 pre[kWords];
   unsigned long long best;
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
@@ -80,6 +94,18 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec
   // times(d, times(One, w)) for w >= +0 (compose.zig:104, shortest-path.zig:72); +inf
   // stays +inf
   nd = d + r.weight;
+}
+// The same on f32 cells and the f32 record copy {src, y, f32 weight, olabel}: the sum of
+// two integers below 2^24 is exact, so it equals the f64 one.
+template <int W>
+__device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const uint4& r,
+                                               uint32_t tmin8, uint32_t& pk, float& nd,
+                                               uint32_t& rank_word) {
+  const uint32_t off = min(r.x - tmin8, 8u * W);
+  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
+  pk = c.y | r.y | off;
+  rank_word = c.y;
+  nd = __uint_as_float(c.x) + __uint_as_float(r.z);
 }
 
 // The in-arc group of target t for input label `lab`: the index of its first record and
@@ -117,17 +143,36 @@ __device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, uint
 // DIRECT (RevView::direct): block 0 of target t is records [t * KP, t * KP + KP), loaded
 // together with rspan[t] (which then only confirms the label); otherwise the group is
 // looked up first (pull_group) and its records loaded after.
-template <int EW, int KP, bool DIRECT, int WAVES_PER_EU>
+// F32: cells and merge in f32, records from RevView::rrec32 -- chosen by the host when every
+// distance of the launch is an integer below 2^24 (pull_f32: integer arc weights, max_len *
+// max weight < 2^24), where every f32 sum, min and compare equals the f64 one.  Strings
+// longer than in.max_len (a caller's wrong bound) are handed on, so the bound always holds.
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, bool F32 = false>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
 eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                   unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
-  constexpr int kWords = PullLds<W>::kWords;
+  using DT = typename std::conditional<F32, float, double>::type;
+  using RT = typename std::conditional<F32, uint4, RevRec>::type;
+  constexpr int kWords = PullLds<W, F32>::kWords;
   static_assert(KP <= 16, "m is 4 bits of the key");
   static_assert(W < 512, "8 * slot is 12 bits of the key, ranks 9 bits");
-  __shared__ PullLds<W> S;
+  __shared__ PullLds<W, F32> S;
   const uint32_t lane = threadIdx.x;
-  const double kInf = __builtin_huge_val();
+  const DT kInf = (DT)__builtin_huge_val();
+  // a cell: {distance, rank word}
+  auto set_cell = [&](uint32_t i, DT d, uint32_t rw) {
+    if constexpr (F32) {
+      S.cell[i] = make_uint2(__float_as_uint(d), rw);
+    } else {
+      S.d[i] = d;
+      S.rk[i] = rw;
+    }
+  };
+  auto rec = [&](uint32_t r) -> RT {
+    if constexpr (F32) return rv.rrec32[r];
+    else return rv.rrec[r];
+  };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;  // uniform: pending backtraces (slab j belongs to job j)
 
@@ -149,8 +194,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint32_t k = jb.L - 1 - t;
         const uint2 b = sl[FB(id, lp.back_cap, 60)];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
-        out.out_ol[jb.o + k] = rv.rolab[b.x];
-        out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+        if constexpr (F32) {
+          const uint4 r = rv.rrec32[b.x];
+          out.out_ol[jb.o + k] = r.w;
+          out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
+        } else {
+          out.out_ol[jb.o + k] = rv.rolab[b.x];
+          out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+        }
         id = b.y;
       }
     }
@@ -172,10 +223,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   const bool want_work = out.work != nullptr;
 
 #pragma unroll 1
-  for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-    S.d[i] = kInf;
-    S.rk[i] = kPullAbsent;
-  }
+  for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) set_cell(i, kInf, kPullAbsent);
   if (lane < (uint32_t)kWords) S.bits[lane] = 0;
   wave_lds_sync();
   uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
@@ -203,26 +251,20 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
     // layer 0: the start tuple alone, slot 0 of a window at the start state
 #pragma unroll 1
-    for (uint32_t i = lane; i < wlast; i += 64) {
-      S.d[i] = kInf;
-      S.rk[i] = kPullAbsent;
-    }
+    for (uint32_t i = lane; i < wlast; i += 64) set_cell(i, kInf, kPullAbsent);
     wave_lds_sync();
-    if (lane == 0) {
-      S.d[0] = w_one();
-      S.rk[0] = 0;
-    }
+    if (lane == 0) set_cell(0, (DT)w_one(), 0u);
     wave_lds_sync();
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
     uint32_t cmin = rhs.start, cmax = rhs.start;  // bounds of the current layer's states
     uint32_t tuples = 1, relax = 0;
-    int32_t fail = kPathOk;
+    int32_t fail = F32 && L > in.max_len ? kPathOverflow : kPathOk;
     unsigned long long mykey = kMaxU64;  // this lane's best final candidate
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
 
     uint32_t labs = 0;
-    for (uint32_t k = 0; k < L; ++k) {
+    for (uint32_t k = 0; k < L && fail == kPathOk; ++k) {
       if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
         fail = kPathInternal;
         break;
@@ -247,7 +289,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
       // ---- (P1) pull: every target slot of the window merges its in-arcs ----
       uint32_t fst[EW], bk[EW], bra[EW];
-      double bd[EW];
+      DT bd[EW];
 #pragma unroll
       for (int e = 0; e < EW; ++e) {
         fst[e] = kEmptyKey;
@@ -273,14 +315,17 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         } else {
           pull_group(rv, lab, t, rec0, nb);
         }
-        const RevRec* R = rv.rrec + rec0;
-        RevRec rr[KP];
+        RT rr[KP];
+        // one base address, the records at immediate offsets
+        const RT* R;
+        if constexpr (F32) R = rv.rrec32 + rec0;
+        else R = rv.rrec + rec0;
 #pragma unroll
         for (int m = 0; m < KP; ++m) rr[m] = R[m];
         uint32_t pk[KP], rw[KP];
-        double nd[KP];
+        DT nd[KP];
         uint32_t f = kEmptyKey;
-        double b = kInf;
+        DT b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
           pull_candidate<W>(S, rr[m], tmin8, pk[m], nd[m], rw[m]);
@@ -307,8 +352,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
             for (int m = 0; m < KP; ++m) {
               uint32_t p2, w2;
-              double n2;
-              pull_candidate<W>(S, rv.rrec[rx + m], tmin8, p2, n2, w2);
+              DT n2;
+              pull_candidate<W>(S, rec(rx + m), tmin8, p2, n2, w2);
               f = min(f, p2);
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
@@ -364,8 +409,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
-        S.d[i] = pres ? bd[e] : kInf;
-        S.rk[i] = pres ? rank << 20 : kPullAbsent;
+        set_cell(i, pres ? bd[e] : kInf, pres ? rank << 20 : kPullAbsent);
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -376,8 +420,9 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
-            if (!w_is_zero(bd[e]) && !w_is_zero(fw2)) {
-              const unsigned long long kk = okey(bd[e] + fw2);  // times(d, times(One, fw2))
+            if (!w_is_zero((double)bd[e]) && !w_is_zero(fw2)) {
+              // times(d, times(One, fw2)), in f64 (f32 cells hold d exactly)
+              const unsigned long long kk = okey((double)bd[e] + fw2);
               const uint32_t pp = (rank << 9) | i;
               if (kk < mykey || (kk == mykey && pp < myp)) {
                 mykey = kk;

@@ -85,6 +85,20 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   // DT: the distance type of cells and of the merge's arithmetic (f32: exact for the
   // integer distances below 2^24 the host checked)
   using DT = typename std::conditional<F32, float, double>::type;
+  // records: RevRec, or with f32 cells RevView::rrec32 {src, y, f32 weight, olabel}
+  using RT = typename std::conditional<F32, uint4, RevRec>::type;
+  auto rec = [&](uint32_t r) -> RT {
+    if constexpr (F32) return rv.rrec32[r];
+    else return rv.rrec[r];
+  };
+  auto r_src = [](const RT& r) -> uint32_t {
+    if constexpr (F32) return r.x;
+    else return r.src;
+  };
+  auto r_w = [](const RT& r) -> DT {
+    if constexpr (F32) return __uint_as_float(r.z);
+    else return r.weight;
+  };
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
   static_assert(KP <= 16 && W < 512, "key layout as in eager_pull.hpp");
   __shared__ LazyPullLds<W, DT> S;
@@ -123,8 +137,14 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint32_t k = jb.L - 1 - t;
         const uint2 b = sl[FB(id, lp.back_cap, 70)];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
-        out.out_ol[jb.o + k] = rv.rolab[b.x];
-        out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+        if constexpr (F32) {
+          const uint4 r = rv.rrec32[b.x];
+          out.out_ol[jb.o + k] = r.w;
+          out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
+        } else {
+          out.out_ol[jb.o + k] = rv.rolab[b.x];
+          out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+        }
         id = b.y;
       }
     }
@@ -192,7 +212,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
     uint32_t cmin = rhs.start, cmax = rhs.start;
     uint32_t tuples = 1, relax = 0;
-    int32_t fail = L > kLpMaxLen ? kPathOverflow : kPathOk;
+    int32_t fail = L > kLpMaxLen || (F32 && L > in.max_len) ? kPathOverflow : kPathOk;
     unsigned long long mykey = kMaxU64;
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
@@ -254,8 +274,11 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           return DIRECT ? rhs.num_states * KP : 0u;
         };
         const bool hubs = __ballot(nb > 1) != 0;  // uniform
-        const RevRec* R = rv.rrec + rec0;
-        RevRec rr[KP];
+        RT rr[KP];
+        // one base address, the records at immediate offsets
+        const RT* R;
+        if constexpr (F32) R = rv.rrec32 + rec0;
+        else R = rv.rrec + rec0;
 #pragma unroll
         for (int m = 0; m < KP; ++m) rr[m] = R[m];
         uint32_t bpk[KP];
@@ -264,15 +287,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         DT b = kInf;
 #pragma unroll
         for (int m = 0; m < KP; ++m) {
-          const uint32_t o = min(rr[m].src - tmin8, 8u * W);
+          const uint32_t o = min(r_src(rr[m]) - tmin8, 8u * W);
           const DT d = cell_d(o);
           const unsigned long long rpw =
               *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
-          nd[m] = d + (DT)rr[m].weight;  // times(d, w) for finite w >= 0 (:108)
+          nd[m] = d + r_w(rr[m]);  // times(d, w) for finite w >= 0 (:108)
           bpk[m] = (uint32_t)rpw | rr[m].y | o;
           ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | rr[m].y | o);
           b = fmin(b, nd[m]);
-          wpos |= (rr[m].weight > 0.0 ? 1u : 0u) << m;
+          wpos |= (r_w(rr[m]) > (DT)0 ? 1u : 0u) << m;
           if (want_work) relax += (uint32_t)__popcll(__ballot((uint32_t)rpw < kLpAbsent));
         }
         uint32_t c = kEmptyKey;
@@ -285,12 +308,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t rxx = block_rec(x);
 #pragma unroll
             for (int m = 0; m < KP; ++m) {
-              const RevRec r2 = rv.rrec[rxx + m];
-              const uint32_t o = min(r2.src - tmin8, 8u * W);
+              const RT r2 = rec(rxx + m);
+              const uint32_t o = min(r_src(r2) - tmin8, 8u * W);
               const DT d = cell_d(o);
               const unsigned long long rpw =
                   *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
-              const DT n2 = d + (DT)r2.weight;
+              const DT n2 = d + r_w(r2);
               const uint32_t p2 = (uint32_t)rpw | r2.y | o;
               ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | r2.y | o);
               if (n2 < b || (n2 == b && p2 < c)) {
@@ -354,15 +377,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               const uint32_t rxx = block_rec(x);
 #pragma unroll
               for (int m = 0; m < KP; ++m) {
-                const RevRec r2 = rv.rrec[rxx + m];
-                const uint32_t o = min(r2.src - tmin8, 8u * W);
+                const RT r2 = rec(rxx + m);
+                const uint32_t o = min(r_src(r2) - tmin8, 8u * W);
                 const DT d = cell_d(o);
                 const DT tbm = cell_tb(o);
                 const uint32_t rm =
                     (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
                     kLpRunMask;
-                cert |= d + (DT)r2.weight == b &&
-                        (r2.weight > 0.0 || tbm < tx || (tbm == tx && rm < rx));
+                cert |= d + r_w(r2) == b &&
+                        (r_w(r2) > (DT)0 || tbm < tx || (tbm == tx && rm < rx));
               }
             }
           }
@@ -406,16 +429,40 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // ---- (P3) the next layer's cells (pop ranks after the sort), back records, and
       // P4's sort keys from the distances still in registers ----
       const bool last = k + 1 == L;
-      const bool sort = !last && n_next > 1;  // the last layer's pop order is never used
       DT mn = kInf, mx = -kInf;
       bool nonint = false;
+      // a layer at one distance (the metric's, every layer): the id order is the pop order,
+      // no keys, no sort; ref = the distance of the first present slot
+      bool neq = false, have = false;
+      DT ref = (DT)0;
 #pragma unroll
       for (int e = 0; e < EW; ++e) {
-        if ((uint32_t)e >= rows_n || fst[e] >= kLpAbsent) continue;
+        if ((uint32_t)e >= rows_n) continue;  // uniform
+        const bool pres = fst[e] < kLpAbsent;
+        const unsigned long long pm = __ballot(pres);
+        if (!have && pm) {  // uniform
+          const uint32_t fl = (uint32_t)__builtin_ctzll(pm);
+          if constexpr (F32) {
+            ref = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(bd[e]), fl));
+          } else {
+            const unsigned long long bb = (unsigned long long)__double_as_longlong(bd[e]);
+            ref = __longlong_as_double(
+                (long long)(((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(bb >> 32), fl) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)bb, fl)));
+          }
+          have = true;
+        }
+        if (!pres) continue;
+        neq |= bd[e] != ref;
         mn = fmin(mn, bd[e]);
         mx = fmax(mx, bd[e]);
         if (!F32) nonint |= bd[e] != __builtin_trunc(bd[e]);
       }
+      // the last layer's pop order is never used
+#ifdef FSTAMD_LP_NO_ALLEQ  // A/B: no one-distance shortcut
+      neq = true;
+#endif
+      const bool sort = !last && n_next > 1 && __ballot(neq) != 0;
       bool ik = false;  // integer distances with d - dmin < 2^23: keys d - dmin
       if (sort) {
         if constexpr (F32) {

@@ -1,0 +1,119 @@
+"""GPU parity of the pull tiers' f32 cells (kernels/eager_pull.hpp, kernels/lazy_pull.hpp).
+
+The pull tiers keep distances in f32 when every distance of the launch is an integer below
+2^24 (integer arc weights in [0, 2^24) and max_len * max weight < 2^24: pull_f32 in
+eager_pull.hip); every f32 sum, min and compare then equals the f64 one, so the answers
+are the reference's f64 answers bit for bit (compose.zig:104, shortest-path.zig:72,
+compose-shortest-path.zig:108).  These tests sit on the edges of that rule:
+  * distances up to 2^24 - 1 (the largest exact f32 integers), f32 chosen;
+  * the same rhs with one string longer, so the launch must take the f64 cells;
+  * the f64 cells forced (FSTAMD_P_F64 / FSTAMD_LP_F64) on integer weights;
+  * a device call whose max_len understates its strings: the f32 kernels must hand the
+    longer strings on (their distances pass 2^24, where f32 would round).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import libfst_amd as F
+import libfst_amd.fst as FF
+import oracle_ffi as O
+from test_gpu_parity import bits, check, csr, expected_status, load_blob
+
+pytestmark = pytest.mark.gpu
+
+EAGER, LAZY = F.FST_SEM_EAGER, F.FST_SEM_LAZY
+
+
+def banded_int_rhs(rng, ns, wmax, labels=3, fanout=3):
+    """A banded rhs without input epsilon (tier P / LP window) and integer weights up to
+    wmax, several in-arcs per state, ties on purpose (half the weights are wmax)."""
+    f = O.Fst()
+    for _ in range(ns):
+        f.add_state(float(rng.integers(0, 5)) if rng.random() < 0.7 else float("inf"))
+    f.start = 0
+    for s in range(ns):
+        for _ in range(fanout):
+            t = min(ns - 1, s + int(rng.integers(0, 4)))
+            w = float(wmax) if rng.random() < 0.5 else float(rng.integers(0, wmax + 1))
+            f.add_arc(s, int(rng.integers(1, labels + 1)), int(rng.integers(1, 9)), w, t)
+    return f
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_distances_up_to_2p24(sem):
+    rng = np.random.default_rng(77)
+    max_len = 63
+    wmax = (1 << 24) // max_len  # 63 * wmax = 2^24 - 1: the largest exact f32 integer
+    assert max_len * wmax < 1 << 24 <= (max_len + 1) * wmax
+    blob = O.freeze(banded_int_rhs(rng, 200, wmax))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(40, max_len + 1)))]
+            for _ in range(300)]
+    seqs.append([1] * max_len)
+    check(blob, *csr(seqs), sem)
+    # one string of 64 labels: the launch's max_len makes every distance bound 2^24 or
+    # more, so the f64 cells run -- for every string of the batch
+    check(blob, *csr(seqs + [[1] * (max_len + 1)]), sem)
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_f64_cells_forced_on_integer_weights(sem, monkeypatch):
+    monkeypatch.setenv("FSTAMD_P_F64", "1")
+    monkeypatch.setenv("FSTAMD_LP_F64", "1")
+    rng = np.random.default_rng(78)
+    blob = O.freeze(banded_int_rhs(rng, 150, 7))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 30)))] for _ in range(200)]
+    check(blob, *csr(seqs), sem)
+
+
+def device_call(rhs, seqs, max_len, sem):
+    labels, offsets = csr(seqs)
+    dev = torch.device("cuda", 0)
+    lab = torch.as_tensor(labels.astype(np.int32), device=dev)
+    off = torch.as_tensor(offsets.astype(np.int64), device=dev)
+    n = len(seqs)
+    cap = int(offsets[-1]) * 4 + 64
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    plen = torch.empty(n, dtype=torch.int32, device=dev)
+    poff = torch.empty(n, dtype=torch.int64, device=dev)
+    fin = torch.empty(n, dtype=torch.float64, device=dev)
+    il = torch.empty(cap, dtype=torch.int32, device=dev)
+    ol = torch.empty(cap, dtype=torch.int32, device=dev)
+    w = torch.empty(cap, dtype=torch.float64, device=dev)
+    cur = torch.zeros(1, dtype=torch.int64, device=dev)
+    desc = FF.FstDeviceBatch(status.data_ptr(), plen.data_ptr(), poff.data_ptr(),
+                             fin.data_ptr(), il.data_ptr(), ol.data_ptr(), w.data_ptr(), cap,
+                             cur.data_ptr(), 0)
+    opts = FF.FstBatchOptions(0, sem, 0)
+    rc = F.lib().fst_device_compose_shortest_path(
+        rhs.h, C.c_void_p(lab.data_ptr()), C.c_void_p(off.data_ptr()), n, max_len, 1,
+        C.byref(opts), C.byref(desc), None)
+    assert rc == FF.FST_OK
+    torch.cuda.synchronize()
+    return (status.cpu().numpy(), plen.cpu().numpy(), poff.cpu().numpy(), fin.cpu().numpy(),
+            il.cpu().numpy().view(np.uint32), ol.cpu().numpy().view(np.uint32), w.cpu().numpy())
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_understated_max_len_hands_longer_strings_on(sem):
+    rng = np.random.default_rng(79)
+    wmax = (1 << 24) // 32 + 1  # 32 labels reach 2^24 + 32: odd sums round in f32
+    blob = O.freeze(banded_int_rhs(rng, 160, wmax))
+    rhs = load_blob(blob)
+    seqs = [[int(x) for x in rng.integers(1, 4, L)] for L in (8, 31, 40, 48, 60, 16, 55)]
+    # the caller claims max_len 16: f32 by that bound, but 5 strings are longer
+    status, plen, poff, fin, il, ol, w = device_call(rhs, seqs, 16, sem)
+    labels, offsets = csr(seqs)
+    ref = O.batch_run(blob, labels, offsets, 0 if sem == LAZY else 1, 1)
+    exp = expected_status(ref)
+    assert np.array_equal(status, exp)
+    for i in np.nonzero(exp == F.FST_PATH_OK)[0]:
+        a, b = int(ref.offsets[i]), int(ref.offsets[i + 1])
+        assert plen[i] == b - a, i
+        g = slice(int(poff[i]), int(poff[i]) + b - a)
+        assert np.array_equal(il[g], ref.ilabels[a:b]), i
+        assert np.array_equal(ol[g], ref.olabels[a:b]), i
+        assert np.array_equal(bits(w[g]), bits(ref.weights[a:b])), i
+        assert bits(fin[i:i + 1])[0] == bits(ref.finals[i:i + 1])[0], i
