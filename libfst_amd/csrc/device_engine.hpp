@@ -55,8 +55,12 @@ struct RhsView {
 // state t, grouped by ilabel, each group in padded blocks of `kp` records.  Record m of a
 // block: 8 * the source state (its LDS cell offset before the window shift), y = (j << 17)
 // | (m << 13) with j = the arc's position in its source's run of equal ilabels (the
-// candidate order of compose.zig:93-121), and the weight.  Padding records have src =
-// 0xFFFFFFF8.  Block 0 is all padding (the null block).
+// candidate order of compose.zig:93-121) | kRevPos when the weight is > 0, and the weight.
+// Padding records have src = 0xFFFFFFF8.  Block 0 is all padding (the null block).
+// y's flag of a positive-weight arc: bit 12, below m; the pull keys OR y with the cell's
+// byte offset (< 4096), so the flag never decides a key comparison (keys of two in-arcs
+// always differ in rank, j or m) and is masked off with the offset (& 0xFFF)
+constexpr uint32_t kRevPos = 0x1000u;
 struct RevRec {
   uint32_t src;
   uint32_t y;

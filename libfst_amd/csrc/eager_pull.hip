@@ -198,7 +198,9 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
         const uint64_t slot = direct ? (r < kp ? (uint64_t)t * kp + r : blk * kp + (r - kp))
                                      : blk * kp + r;
         const uint32_t m = r % kp;
-        rrec[slot] = RevRec{src[a] << 3, ((uint32_t)jpos[a] << 17) | (m << 13), pa[a].weight};
+        rrec[slot] = RevRec{src[a] << 3,
+                            ((uint32_t)jpos[a] << 17) | (m << 13) | (pa[a].weight > 0.0 ? kRevPos : 0u),
+                            pa[a].weight};
         rolab[slot] = pa[a].olabel;
       }
       blk += nb - (direct ? 1 : 0);

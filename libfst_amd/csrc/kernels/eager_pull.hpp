@@ -416,7 +416,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + ((bk[e] & 0x1FFFu) >> 3));
+          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + ((bk[e] & 0xFFFu) >> 3));
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
