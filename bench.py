@@ -455,7 +455,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            # results and the CPU port are f64; on this integer-weight rhs the pull tiers
+            # keep the cells' distances in f32, exact (every distance an integer < 2^24),
+            # so every output bit equals the f64 computation (checked_vs_oracle)
             "dtype": "f64",
+            "cell_dtype": "f32 (exact: integer weights, max_len * max weight < 2^24)",
             "data": "synthetic (reference bench generators: 1^64 repeat acceptors, "
                     "ambiguous-chain rhs)",
             "config": {"workload": "compose_frozen_shortest_path_ambiguous",
