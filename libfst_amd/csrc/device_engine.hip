@@ -818,24 +818,42 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       unsigned int* c = counter + 40;  // [40] items (LDS 128), [41] |la|, [42] items (256), [43] |lb|
       HIP_TRY(hipMemsetAsync(c, 0, 16, stream));
       uint32_t g = 0;
-      HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 1, nullptr, num, c, &g));
-      if (stats) stats->grid = g;
-      collect_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(out.status, num, kPathOverflow,
-                                                                  la, c + 1);
-      HIP_TRY(hipGetLastError());
+      // the 128-tuple size first, unless it handed on over a third of an earlier batch on
+      // this rhs (DeviceFst::tiny_lazy_256: the WeText-scale tagger's lattices, 54 % over
+      // 128 tuples: tagger stage 46.7 -> 40.0 ms per 64 K utterances starting at 256);
+      // FSTAMD_LAZY_TINY_START=1|2 forces the first size
+      const char* ts = std::getenv("FSTAMD_LAZY_TINY_START");
+      const bool first128 = ts && *ts ? std::strcmp(ts, "2") != 0
+                                      : rhs.tiny_lazy_256.load(std::memory_order_relaxed) == 0;
       uint32_t cnt[2] = {0, 0};
-      HIP_TRY(hipMemcpyAsync(&cnt[0], c + 1, 4, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+      if (first128) {
+        HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 1, nullptr, num, c, &g));
+        if (stats) stats->grid = g;
+        collect_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(out.status, num,
+                                                                    kPathOverflow, la, c + 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&cnt[0], c + 1, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+      } else {
+        cnt[0] = num;
+      }
       if (cnt[0] > 0) {
-        HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 2, la, cnt[0], c + 2, &g));
-        collect_list_kernel<<<(cnt[0] + 255) / 256, 256, 0, stream>>>(la, c + 1, out.status,
+        HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 2, first128 ? la : nullptr, cnt[0], c + 2, &g));
+        if (first128) {
+          collect_list_kernel<<<(cnt[0] + 255) / 256, 256, 0, stream>>>(la, c + 1, out.status,
+                                                                        kPathOverflow, lb, c + 3);
+        } else {
+          collect_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(out.status, num,
                                                                       kPathOverflow, lb, c + 3);
+        }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(&cnt[1], c + 3, 4, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         if (stats) stats->launches += 1;
       }
-      if (num >= 64 && (uint64_t)cnt[0] * 10 > (uint64_t)num * 9)
+      if (first128 && num >= 1024 && (uint64_t)cnt[0] * 3 > (uint64_t)num)
+        rhs.tiny_lazy_256.store(1, std::memory_order_relaxed);
+      if (first128 && num >= 64 && (uint64_t)cnt[0] * 10 > (uint64_t)num * 9)
         rhs.skip_tiny_lazy.store(1, std::memory_order_relaxed);
       todo = lb;
       todo_n = cnt[1];
@@ -1727,8 +1745,13 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
                     ((uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384 ||
                      rhs.skip_tiny_eager.load(std::memory_order_relaxed) == 0);
   const uint32_t count0 = count;
-  // tier -2: the 128-tuple tiny size, tier -1: the 256-tuple one, then the HBM tiers
-  for (int tier = tiny ? -2 : 0; count > 0; ++tier) {
+  // tier -2: the 128-tuple tiny size, tier -1: the 256-tuple one, then the HBM tiers.
+  // The 128-tuple size is skipped on an rhs where it handed on over a third of an earlier
+  // batch (DeviceFst::tiny_eager_256); FSTAMD_BFS_TINY_START=1|2 forces the first size.
+  const char* tse = std::getenv("FSTAMD_BFS_TINY_START");
+  const bool first128 = tse && *tse ? std::strcmp(tse, "2") != 0
+                                    : rhs.tiny_eager_256.load(std::memory_order_relaxed) == 0;
+  for (int tier = tiny ? (first128 ? -2 : -1) : 0; count > 0; ++tier) {
     const TinyCaps tc = tiny_caps(tier == -2 ? 1 : 2);
     const BfsCaps c = tier < 0 ? BfsCaps{tc.n, tc.a, tc.h, tc.l, 0} : bfs_caps(tier);
     const uint64_t fit = tier < 0 ? ~0ull : std::max<uint64_t>(1, kBfsBudget / c.stride);
@@ -1799,6 +1822,8 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     HIP_TRY(hipMemcpyAsync(cnt, cnt + 2, 4, hipMemcpyDeviceToDevice, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::swap(list, list2);
+    if (tier == -2 && count0 >= 1024 && (uint64_t)count * 3 > (uint64_t)count0)
+      rhs.tiny_eager_256.store(1, std::memory_order_relaxed);
     // the 128-tuple tier handed on nearly every string: skip the tiny tiers on this rhs
     if (tier == -2 && count0 >= 64 && (uint64_t)count * 10 > (uint64_t)count0 * 9 &&
         (uint64_t)(in.max_len + 1) * rhs.view.num_states > 16384)

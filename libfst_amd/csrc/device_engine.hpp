@@ -110,6 +110,8 @@ struct DeviceFst {
   // Routing hints learnt from earlier batches on this rhs: a small-lattice (LDS) tier that
   // handed on nearly every string is skipped next time (config 3's lattices never fit).
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};
+  // ... and one whose 128-tuple LDS size handed on over a third of a batch starts at 256
+  mutable std::atomic<int> tiny_lazy_256{0}, tiny_eager_256{0};
   RevView rev{};
   void* rev_bufs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a

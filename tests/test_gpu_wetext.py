@@ -34,6 +34,19 @@ def test_tagger_stage(standin, sem):
     assert (got.status == F.FST_PATH_OK).all()
 
 
+@pytest.mark.parametrize("sem", [LAZY, EAGER])
+@pytest.mark.parametrize("start", ["1", "2"])
+def test_tagger_stage_tiny_start(standin, sem, start, monkeypatch):
+    # the LDS tiny sizes start at 128 tuples, or at 256 on an rhs whose 128-tuple pass
+    # handed on over a third of a batch (learnt per rhs; forced here both ways)
+    monkeypatch.setenv("FSTAMD_LAZY_TINY_START", start)
+    monkeypatch.setenv("FSTAMD_BFS_TINY_START", start)
+    tb, _, _, _ = standin
+    labels, offsets = W.utterances(np.random.default_rng(57 + sem), 1200)
+    got, ref = check(tb, labels, offsets, sem)
+    assert (got.status == F.FST_PATH_OK).all()
+
+
 def oracle_pipeline(blobs, labels, offsets, sem):
     num = len(offsets) - 1
     fail = np.full(num, F.FST_PATH_OK, np.int32)
