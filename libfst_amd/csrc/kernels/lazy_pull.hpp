@@ -423,36 +423,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         break;
       }
 
-      // ---- (P3) the next layer's cells (pop ranks after the sort), back records, and
-      // P4's sort keys from the distances still in registers ----
+      // ---- (P3) the next layer's cells (pop ranks after the sort), back records, and the
+      // id order's slots for P4 ----
       const bool last = k + 1 == L;
-      DT mn = kInf, mx = -kInf;
-      bool nonint = false;
-#pragma unroll
-      for (int e = 0; e < EW; ++e) {
-        if ((uint32_t)e >= rows_n || fst[e] >= kLpAbsent) continue;
-        mn = fmin(mn, bd[e]);
-        mx = fmax(mx, bd[e]);
-        if (!F32) nonint |= bd[e] != __builtin_trunc(bd[e]);
-      }
-      // (a one-distance shortcut here -- a ballot of d != the first present slot's d,
-      // skipping the keys and the order check -- measured slower: 72.5 vs 69.4 ms per 1M
-      // metric strings; the order check below is cheap)
       const bool sort = !last && n_next > 1;  // the last layer's pop order is never used
-      bool ik = false;  // integer distances with d - dmin < 2^23: keys d - dmin
-      if (sort) {
-        if constexpr (F32) {
-          mn = __ockl_wfred_min_f32(mn);
-          mx = __ockl_wfred_max_f32(mx);
-        } else {
-          mn = __ockl_wfred_min_f64(mn);
-          mx = __ockl_wfred_max_f64(mx);
-        }
-        ik = __ballot(nonint) == 0 && (double)mx - (double)mn < 8388608.0;
-      }
-      const unsigned long long mnb = (unsigned long long)__double_as_longlong((double)mn);
-      uint32_t kacc = 0;            // OR of the integer keys
-      unsigned long long diff = 0;  // OR of the f64 patterns' differences from dmin's
       const uint32_t rows_w = max(rows_n, (wk + 63) / 64);
       uint32_t lo_slot = kEmptyKey, hi_slot = 0;
 #pragma unroll
@@ -471,13 +445,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         S.tb[i] = pres ? tbx[e] : kInf;
         // pop rank: identity until the sort below fills it in
         S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
-        if (pres && sort) {
-          const uint32_t key = ik ? (uint32_t)(bd[e] - mn) : 0u;  // exact: integers < 2^23
-          S.ord0[rank] = (key << 9) | i;
-          kacc |= key;
-          if constexpr (!F32)  // (f32 cells: integer distances, ik)
-            diff |= ik ? 0ull : (unsigned long long)__double_as_longlong((double)bd[e]) ^ mnb;
-        }
+        if (pres && sort) S.ord0[rank] = i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -512,29 +480,67 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       if (sort) {
 #endif
         const uint32_t rows_s = (n_next + 63) / 64;
-#ifdef FSTAMD_LP_SPLIT_ONLY  // A/B: the split sort for every layer
-        const bool counting = false;
-#else
-        const bool counting = ik && mx - mn < (DT)kLpBins;
-#endif
         // already in order (the metric's layers, every one of them): the id order is the
-        // pop order and the identity ranks written in P3 stand; nothing below runs
+        // pop order and the identity ranks written in P3 stand; nothing below runs (no
+        // reductions, no keys: the check compares the cells' distances in id order)
         bool unsorted = false;
 #pragma unroll
         for (int e = 0; e < EW; ++e) {
           if ((uint32_t)e >= rows_s) continue;  // uniform
           const uint32_t q = (uint32_t)e * 64 + lane;
-          if (q + 1 < n_next) {
-            const uint32_t a = S.ord0[q], b2 = S.ord0[q + 1];
-            if (ik) {
-              unsorted |= (a >> 9) > (b2 >> 9);
-            } else {
-              unsorted |= S.d[a & 511u] > S.d[b2 & 511u];
-            }
-          }
+          if (q + 1 < n_next) unsorted |= S.d[S.ord0[q]] > S.d[S.ord0[q + 1]];
         }
         const bool in_order = !__ballot(unsorted);
         if (!in_order) {
+        // keys: integer distances with d - dmin < 2^23 (ik) sort by d - dmin, others by
+        // their f64 bit patterns; dmin / dmax over the layer, then key << 9 | slot in ord0
+        DT mn = kInf, mx = -kInf;
+        bool nonint = false;
+        uint32_t cs[EW];
+        DT cd[EW];
+#pragma unroll
+        for (int e = 0; e < EW; ++e) {
+          cs[e] = 0;
+          cd[e] = (DT)0;
+          if ((uint32_t)e >= rows_s) continue;  // uniform
+          const uint32_t q = (uint32_t)e * 64 + lane;
+          if (q < n_next) {
+            cs[e] = S.ord0[q];
+            cd[e] = S.d[cs[e]];
+            mn = fmin(mn, cd[e]);
+            mx = fmax(mx, cd[e]);
+            if (!F32) nonint |= cd[e] != __builtin_trunc(cd[e]);
+          }
+        }
+        if constexpr (F32) {
+          mn = __ockl_wfred_min_f32(mn);
+          mx = __ockl_wfred_max_f32(mx);
+        } else {
+          mn = __ockl_wfred_min_f64(mn);
+          mx = __ockl_wfred_max_f64(mx);
+        }
+        const bool ik = __ballot(nonint) == 0 && (double)mx - (double)mn < 8388608.0;
+        const unsigned long long mnb = (unsigned long long)__double_as_longlong((double)mn);
+        uint32_t kacc = 0;            // OR of the integer keys
+        unsigned long long diff = 0;  // OR of the f64 patterns' differences from dmin's
+#pragma unroll
+        for (int e = 0; e < EW; ++e) {
+          if ((uint32_t)e >= rows_s) continue;  // uniform
+          const uint32_t q = (uint32_t)e * 64 + lane;
+          if (q < n_next) {
+            const uint32_t key = ik ? (uint32_t)(cd[e] - mn) : 0u;  // exact: integers < 2^23
+            S.ord0[q] = (key << 9) | cs[e];
+            kacc |= key;
+            if constexpr (!F32)  // (f32 cells: integer distances, ik)
+              diff |= ik ? 0ull : (unsigned long long)__double_as_longlong((double)cd[e]) ^ mnb;
+          }
+        }
+        wave_lds_sync();
+#ifdef FSTAMD_LP_SPLIT_ONLY  // A/B: the split sort for every layer
+        const bool counting = false;
+#else
+        const bool counting = ik && mx - mn < (DT)kLpBins;
+#endif
         unsigned long long vary;
         if (ik) {
           vary = (unsigned long long)__builtin_amdgcn_readfirstlane(__ockl_wfred_or_u32(kacc)) << 9;
