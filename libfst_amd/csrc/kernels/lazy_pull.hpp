@@ -295,7 +295,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           bpk[m] = (uint32_t)rpw | rr[m].y | o;
           ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | rr[m].y | o);
           b = fmin(b, nd[m]);
-          if (want_work) relax += (uint32_t)__popcll(__ballot((uint32_t)rpw < kLpAbsent));
+        }
+        if (want_work) {  // (one uniform branch per row; an absent source's key >= kLpAbsent)
+#pragma unroll
+          for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(bpk[m] < kLpAbsent));
         }
         uint32_t c = kEmptyKey;
 #pragma unroll
