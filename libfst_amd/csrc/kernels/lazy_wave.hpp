@@ -23,6 +23,9 @@
 
 #include "device_common.hpp"
 
+extern "C" __device__ double __ockl_wfred_min_f64(double);
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
 namespace fstamd {
 
 struct LazyWs {
@@ -435,27 +438,22 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           if (dead) break;
           const uint32_t cc = c0 + lane;
           const bool v = cc < qn;
-          double md = v ? qd[cc] : 0.0;
-          uint32_t mi = v ? qid[cc] : 0u;
-          uint32_t mp = cc;
-          bool mv = v;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            const double od = __shfl_xor(md, o, 64);
-            const uint32_t oi = __shfl_xor(mi, o, 64);
-            const uint32_t op = __shfl_xor(mp, o, 64);
-            const bool ov = __shfl_xor((int)mv, o, 64) != 0;
-            // duplicates of one (dist, id) exist (equal-dist tie takes push again):
-            // break ties by heap position so every lane agrees on the winner
-            const bool take =
-                ov && (!mv || qless(od, oi, md, mi) || (od == md && oi == mi && op < mp));
-            if (take) {
-              md = od;
-              mi = oi;
-              mp = op;
-              mv = true;
-            }
-          }
+          const double cd = v ? qd[cc] : 0.0;
+          const uint32_t ci = v ? qid[cc] : 0u;
+          // the minimum child by (dist, id), duplicates of one (dist, id) (an equal-dist tie
+          // takes push again) by heap position: three DPP reductions (min dist, then min id
+          // among those, then min position), the winner's exact dist read from its lane
+          // (-0.0 == +0.0 as in qless); lane 0 (child c0 < qn) is always valid
+          const double dmn = __ockl_wfred_min_f64(v ? cd : __builtin_huge_val());
+          const bool c1 = v && cd == dmn;
+          const uint32_t mi = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(c1 ? ci : ~0u));
+          const uint32_t mp = __builtin_amdgcn_readfirstlane(
+              __ockl_wfred_min_u32(c1 && ci == mi ? cc : ~0u));
+          const uint32_t wl = mp - c0;
+          const unsigned long long cb = (unsigned long long)__double_as_longlong(cd);
+          const double md = __longlong_as_double(
+              (long long)(((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(cb >> 32), wl) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)cb, wl)));
           // all lanes now hold the minimum child
           if (qless(md, mi, xd, xi)) {
             if (lane == 0) {
@@ -551,7 +549,9 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           LZ_WD(4);
           if (dead) break;
           const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
-          const unsigned long long lk = __shfl(x.key, (int)l, 64);
+          const unsigned long long lk =
+              ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(x.key >> 32), l) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((uint32_t)x.key, l);
           const bool same = need && x.key == lk;
           const unsigned long long m = __ballot(same);
           if (same) leader = l;
@@ -657,7 +657,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             LZ_WD(5);
             if (dead) break;
             const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
-            const uint32_t lt2 = __shfl(tid, (int)l, 64);
+            const uint32_t lt2 = __builtin_amdgcn_readlane(tid, l);
             const bool same = act && tid == lt2;
             const unsigned long long m = __ballot(same);
             if (lane == l) gmask = m;
@@ -715,8 +715,11 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           }
           const uint32_t l = (uint32_t)__ffsll((long long)pm) - 1;
           pm &= pm - 1;
-          const double xd = __shfl(push_d, (int)l, 64);
-          const uint32_t xi = __shfl(tid, (int)l, 64);
+          const unsigned long long pb2 = (unsigned long long)__double_as_longlong(push_d);
+          const double xd = __longlong_as_double(
+              (long long)(((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pb2 >> 32), l) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)pb2, l)));
+          const uint32_t xi = __builtin_amdgcn_readlane(tid, l);
           if (qn >= ws.qcap) {
             fail = kPathOverflow;
             break;
