@@ -1096,9 +1096,12 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       }
       if (tid == 0) T.aoff[f1] = n_arcs + carry;
       __syncthreads();
-      // (B) write arcs, insert targets (first candidate of a new key wins)
+      // (B) write arcs, insert targets (first candidate of a new key wins).  A thread
+      // expands its tuples' candidates (arcs, and each target's key parked in anext/cslot),
+      // then every thread inserts candidates of the level in parallel: a tuple's dozen
+      // hash inserts are no longer a chain of dependent atomics on one thread
       if (tid == 0) SH.flag = 0;
-      __syncthreads();
+      const uint32_t c0 = n_arcs, c1 = n_arcs + carry;
       for (uint32_t p = f0 + tid; p < f1; p += WG) {
         const unsigned long long k = T.nkey[p];
         const uint32_t s1 = (uint32_t)(k >> 2) & 0x3FFFFFFFu, s2 = (uint32_t)(k >> 32),
@@ -1109,23 +1112,29 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
                              T.ail[a] = il;
                              T.aol[a] = ol;
                              T.aw[a] = w;
-                             uint32_t h = bfs_hash(key) & hmask, slot = kEmptyKey;
-                             for (uint32_t probe = 0; probe <= hmask; ++probe) {
-                               const unsigned long long old = atomicCAS(&T.hkey[h], ~0ull, key);
-                               if (old == ~0ull || old == key) {
-                                 slot = h;
-                                 break;
-                               }
-                               h = (h + 1) & hmask;
-                             }
-                             if (slot == kEmptyKey) {
-                               SH.flag = 1;
-                             } else {
-                               atomicMin(&T.hval[slot], 0x80000000u | a);  // ids stay smaller
-                             }
-                             T.cslot[a] = slot;
+                             T.anext[a] = (uint32_t)(key >> 32);  // (D) overwrites it
+                             T.cslot[a] = (uint32_t)key;
                              ++a;
                            });
+      }
+      __syncthreads();
+      for (uint32_t a = c0 + tid; a < c1; a += WG) {
+        const unsigned long long key = ((unsigned long long)T.anext[a] << 32) | T.cslot[a];
+        uint32_t h = bfs_hash(key) & hmask, slot = kEmptyKey;
+        for (uint32_t probe = 0; probe <= hmask; ++probe) {
+          const unsigned long long old = atomicCAS(&T.hkey[h], ~0ull, key);
+          if (old == ~0ull || old == key) {
+            slot = h;
+            break;
+          }
+          h = (h + 1) & hmask;
+        }
+        if (slot == kEmptyKey) {
+          SH.flag = 1;
+        } else {
+          atomicMin(&T.hval[slot], 0x80000000u | a);  // ids stay smaller
+        }
+        T.cslot[a] = slot;
       }
       __syncthreads();
       if (SH.flag) {
@@ -1133,7 +1142,6 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
         break;
       }
       // (C) ids of first occurrences, in candidate order (contiguous chunks per thread)
-      const uint32_t c0 = n_arcs, c1 = n_arcs + carry;
       constexpr uint32_t K = 4;
       uint32_t newc = 0;
       for (uint32_t b = c0; b < c1; b += WG * K) {
