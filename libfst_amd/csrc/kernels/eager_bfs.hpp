@@ -1146,11 +1146,14 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       uint32_t newc = 0;
       for (uint32_t b = c0; b < c1; b += WG * K) {
         const uint32_t a0 = b + tid * K;
-        uint32_t nf = 0;
+        uint32_t nf = 0, slots[K];
+        bool first[K];  // (kept from the count pass: no second round of dependent loads)
 #pragma unroll
         for (uint32_t q = 0; q < K; ++q) {
           const uint32_t a = a0 + q;
-          if (a < c1 && ld_agent(&T.hval[T.cslot[a]]) == (0x80000000u | a)) ++nf;
+          slots[q] = a < c1 ? T.cslot[a] : 0u;
+          first[q] = a < c1 && ld_agent(&T.hval[slots[q]]) == (0x80000000u | a);
+          nf += first[q] ? 1u : 0u;
         }
         uint32_t tot;
         uint32_t rank = block_excl_scan<WG>(nf, SH.scan, tot);
@@ -1159,10 +1162,9 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
         } else {
 #pragma unroll
           for (uint32_t q = 0; q < K; ++q) {
-            const uint32_t a = a0 + q;
-            if (a < c1) {
-              const uint32_t slot = T.cslot[a];
-              if (ld_agent(&T.hval[slot]) == (0x80000000u | a)) {
+            {
+              const uint32_t slot = slots[q];
+              if (first[q]) {
                 const uint32_t id = n_nodes + newc + rank++;
                 T.hval[slot] = id;
                 T.nkey[id] = ld_agent(&T.hkey[slot]);
