@@ -39,7 +39,7 @@ namespace fstamd {
 // perm (optional): the device's state numbering (old id -> new id, DeviceFst::perm).
 __global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t na,
                                     const uint32_t* perm, uint2* span, double* fin, uint32_t* il,
-                                    ArcRec* rec, uint4* sspan) {
+                                    ArcRec* rec, uint4* sspan, uint4* sspan2) {
   const StateEntry* se = reinterpret_cast<const StateEntry*>(blob + sizeof(Header));
   const PackedArc* pa =
       reinterpret_cast<const PackedArc*>(blob + sizeof(Header) + (size_t)ns * sizeof(StateEntry));
@@ -56,6 +56,14 @@ __global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t n
       uniq = a == z ? a : kSpanMixed;
     }
     sspan[ni] = make_uint4(e.arc_offset, e.num_arcs, uniq, 0u);
+    uint4 two = make_uint4(kSpanNone, kSpanNone, 0u, 0u);
+    if (uniq == kSpanMixed) {
+      const uint32_t a = pa[e.arc_offset].ilabel, z = pa[e.arc_offset + e.num_arcs - 1].ilabel;
+      uint32_t na_ = 1;
+      while (na_ < e.num_arcs && pa[e.arc_offset + na_].ilabel == a) ++na_;
+      two = make_uint4(a, z, na_, pa[e.arc_offset + na_].ilabel == z ? 1u : 0u);
+    }
+    sspan2[ni] = two;
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {
     const PackedArc a = pa[i];
@@ -159,7 +167,8 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
             hipMalloc(&d->il, sizeof(uint32_t) * std::max<uint32_t>(na, 1)) == hipSuccess &&
             hipMalloc(&d->rec, sizeof(ArcRec) * ((size_t)na + kRecPad)) == hipSuccess &&
             hipMemset(d->rec + na, 0, sizeof(ArcRec) * kRecPad) == hipSuccess &&
-            hipMalloc(&d->sspan, sizeof(uint4) * std::max<uint32_t>(ns, 1)) == hipSuccess;
+            hipMalloc(&d->sspan, sizeof(uint4) * 2 * (size_t)std::max<uint32_t>(ns, 1)) ==
+                hipSuccess;  // sspan, then sspan2
   if (!ok) {
     DeviceFst::destroy(d);
     return nullptr;
@@ -169,7 +178,7 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   if (work > 0) {
     build_mirror_kernel<<<std::max<uint32_t>(blocks, 1), 256>>>(d->blob, ns, na, d_perm, d->span,
                                                                 d->final_w, d->il, d->rec,
-                                                                d->sspan);
+                                                                d->sspan, d->sspan + ns);
   }
   const bool synced = hipStreamSynchronize(nullptr) == hipSuccess;  // the null stream only:
   if (d_perm) (void)hipFree(d_perm);          // other calls' engines run on their own streams
@@ -183,7 +192,7 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   const uint32_t start = (d->perm.empty() || h.start_state >= ns) ? h.start_state
                                                                   : d->perm[h.start_state];
   d->view = RhsView{d->span, d->final_w, d->il,       d->rec,     d->sspan,
-                    ns,      na,         start,        max_span,   jb, jf};
+                    ns,      na,         start,        max_span,   jb, jf, d->sspan + ns};
   d->has_eps = f.has_epsilon_input();
   d->nonneg = f.weights_nonnegative();
   d->nan = f.has_nan_weight();

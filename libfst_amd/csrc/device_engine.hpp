@@ -49,6 +49,10 @@ struct RhsView {
   uint32_t jump_back;       // max (s - t) over arcs s -> t (0 if none goes backwards)
   uint32_t jump_fwd;        // max (t - s) over arcs s -> t: a layer's targets lie within
                             // [min state - jump_back, max state + jump_fwd]
+  // [num_states] for states with several ilabels: {first ilabel a, last ilabel z, arcs
+  // carrying a, 1 when every other arc carries z}: a two-label state (an epsilon run then
+  // one label, the epsilon-dense rhs) answers arcsByIlabel without a search
+  const uint4* sspan2;
 };
 
 // Reverse arc mirror for the pull tier (kernels/eager_pull.hpp): the in-arcs of every rhs

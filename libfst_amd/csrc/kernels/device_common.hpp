@@ -95,6 +95,11 @@ __device__ __forceinline__ void span_by_ilabel(const RhsView& r, uint32_t s, uin
 
 // arcsByIlabel (src/fst.zig:112-136) with the per-state summary: one 16-B load when all
 // arcs of the state share an ilabel (or it has none), binary search otherwise.
+// kTwo: answer a two-label state (RhsView::sspan2) without the search.  Only the general
+// engine's graph-lhs expansion asks for it (config 1's epsilon-dense lattice: every state
+// is an epsilon run then label 1; kernel 133.6 -> 123.6 ms); on the batch tiers' small
+// lattices the extra branch measured 2-3 % slower.
+template <bool kTwo = false>
 __device__ __forceinline__ void span_summary(const RhsView& r, uint32_t s, uint32_t label,
                                              uint32_t& lo, uint32_t& cnt) {
   const uint4 ss = r.sspan[FB(s, r.num_states, 30)];
@@ -104,6 +109,17 @@ __device__ __forceinline__ void span_summary(const RhsView& r, uint32_t s, uint3
   } else if (ss.z != kSpanMixed) {
     lo = ss.x;
     cnt = 0;
+  } else if (!kTwo) {
+    uint32_t a, b;
+    span_by_ilabel(r, s, label, a, b);
+    lo = a;
+    cnt = b - a;
+  } else if (const uint4 s2 = r.sspan2[FB(s, r.num_states, 31)]; label == s2.x) {
+    lo = ss.x;  // the first ilabel's run
+    cnt = s2.z;
+  } else if (s2.w) {  // two labels: a run of a, then z (ilabels ascending)
+    lo = label < s2.x ? ss.x : label <= s2.y ? ss.x + s2.z : ss.x + ss.y;
+    cnt = label == s2.y ? ss.y - s2.z : 0u;
   } else {
     uint32_t a, b;
     span_by_ilabel(r, s, label, a, b);

@@ -170,7 +170,7 @@ __device__ __forceinline__ void bfs_expand(const RhsView& rhs, const BfsLhs<kGra
     lhs.arc(s1, i, il, ol, w, nx);
     if (ol == kEpsilon) continue;
     uint32_t lo, cnt;
-    span_summary(rhs, s2, ol, lo, cnt);
+    span_summary<kGraph>(rhs, s2, ol, lo, cnt);
     for (uint32_t a = lo; a < lo + cnt; ++a) {
       const ArcRec r = rhs.rec[a];
       emit(il, r.olabel, w_times(w, r.weight), bfs_key(nx, r.next, 0));
@@ -187,7 +187,7 @@ __device__ __forceinline__ void bfs_expand(const RhsView& rhs, const BfsLhs<kGra
     }
   }
   uint32_t elo, ecnt;
-  span_summary(rhs, s2, kEpsilon, elo, ecnt);
+  span_summary<kGraph>(rhs, s2, kEpsilon, elo, ecnt);
   const uint32_t ehi = elo + ecnt;
   if (f != 2) {  // phase 3: rhs epsilon input alone
     const uint32_t nf = f == 0 ? 1u : f;
