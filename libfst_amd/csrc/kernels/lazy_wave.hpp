@@ -117,15 +117,29 @@ __device__ __forceinline__ void prepare_chain(const RhsView& rhs, const ChainLhs
                                               PopCands& P) {
   const bool has_arc = P.s1 < lhs.L;
   P.label = has_arc ? lhs.labels[P.s1] : 0u;
-  uint32_t lo3, hi3;
-  span_by_ilabel(rhs, P.s2, kEpsilon, lo3, hi3);
+  // arcsByIlabel for the epsilon and the label runs of the (wave-uniform) popped state:
+  // up to 64 arcs, every lane reads one ilabel and both runs come from ballots (one round
+  // trip; ilabels ascending, epsilon = 0 first); beyond, the binary searches
+  const uint2 sp = rhs.span[FB(P.s2, rhs.num_states, 1)];
+  const uint32_t off = sp.x, n = sp.y;
+  uint32_t lo3, hi3, lo1 = 0, hi1 = 0;
+  if (n <= 64) {
+    const uint32_t lane = lane_id();
+    const bool v = lane < n;
+    const uint32_t x = v ? rhs.il[FB(off + lane, rhs.num_arcs, 2)] : 0u;
+    lo3 = off;
+    hi3 = off + (uint32_t)__popcll(__ballot(v && x == kEpsilon));
+    lo1 = off + (uint32_t)__popcll(__ballot(v && x < P.label));
+    hi1 = off + (uint32_t)__popcll(__ballot(v && x <= P.label));
+  } else {
+    span_by_ilabel(rhs, P.s2, kEpsilon, lo3, hi3);
+    if (has_arc && P.label != kEpsilon) span_by_ilabel(rhs, P.s2, P.label, lo1, hi1);
+  }
   P.lo3 = lo3;
   const uint32_t ne = hi3 - lo3;
   P.n1 = 0;
   P.lo1 = 0;
   if (has_arc && P.label != kEpsilon) {  // :182-224
-    uint32_t lo1, hi1;
-    span_by_ilabel(rhs, P.s2, P.label, lo1, hi1);
     P.lo1 = lo1;
     P.n1 = hi1 - lo1;
   }
