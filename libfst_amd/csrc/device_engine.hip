@@ -55,14 +55,16 @@ __global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t n
       const uint32_t a = pa[e.arc_offset].ilabel, z = pa[e.arc_offset + e.num_arcs - 1].ilabel;
       uniq = a == z ? a : kSpanMixed;
     }
-    sspan[ni] = make_uint4(e.arc_offset, e.num_arcs, uniq, 0u);
     uint4 two = make_uint4(kSpanNone, kSpanNone, 0u, 0u);
+    uint32_t neps = 0;  // mixed states: the leading epsilon run (ilabel 0 sorts first)
     if (uniq == kSpanMixed) {
       const uint32_t a = pa[e.arc_offset].ilabel, z = pa[e.arc_offset + e.num_arcs - 1].ilabel;
       uint32_t na_ = 1;
       while (na_ < e.num_arcs && pa[e.arc_offset + na_].ilabel == a) ++na_;
       two = make_uint4(a, z, na_, pa[e.arc_offset + na_].ilabel == z ? 1u : 0u);
+      neps = a == 0u ? na_ : 0u;
     }
+    sspan[ni] = make_uint4(e.arc_offset, e.num_arcs, uniq, neps);
     sspan2[ni] = two;
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) {

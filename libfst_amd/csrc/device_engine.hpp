@@ -41,7 +41,8 @@ struct RhsView {
   const uint32_t* il;       // [num_arcs] sorted ilabels per state span
   const ArcRec* rec;        // [num_arcs] {nextstate, olabel, weight}
   const uint4* sspan;       // [num_states] {arc_offset, num_arcs, ilabel shared by all
-                            //  arcs of the state | kSpanMixed | kSpanNone, 0}
+                            //  arcs of the state | kSpanMixed | kSpanNone, leading epsilon
+                            //  arcs of a kSpanMixed state (ilabel 0 sorts first) else 0}
   uint32_t num_states;
   uint32_t num_arcs;
   uint32_t start;

@@ -109,6 +109,9 @@ __device__ __forceinline__ void span_summary(const RhsView& r, uint32_t s, uint3
   } else if (ss.z != kSpanMixed) {
     lo = ss.x;
     cnt = 0;
+  } else if (label == 0u) {  // kEpsilon: a mixed state's leading epsilon run, ss.w arcs
+    lo = ss.x;
+    cnt = ss.w;
   } else if (!kTwo) {
     uint32_t a, b;
     span_by_ilabel(r, s, label, a, b);
