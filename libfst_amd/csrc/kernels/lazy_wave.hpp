@@ -120,10 +120,18 @@ __device__ __forceinline__ void prepare_chain(const RhsView& rhs, const ChainLhs
   // arcsByIlabel for the epsilon and the label runs of the (wave-uniform) popped state:
   // up to 64 arcs, every lane reads one ilabel and both runs come from ballots (one round
   // trip; ilabels ascending, epsilon = 0 first); beyond, the binary searches
-  const uint2 sp = rhs.span[FB(P.s2, rhs.num_states, 1)];
-  const uint32_t off = sp.x, n = sp.y;
+  // (the state summary first: a state whose arcs share one ilabel -- most of a tagger's
+  // -- needs no ilabel loads, so its arc records are the next and last round trip)
+  const uint4 ss = rhs.sspan[FB(P.s2, rhs.num_states, 30)];
+  const uint32_t off = ss.x, n = ss.y;
   uint32_t lo3, hi3, lo1 = 0, hi1 = 0;
-  if (n <= 64) {
+  if (ss.z != kSpanMixed) {  // one ilabel (or no arc)
+    const bool eps = ss.z == kEpsilon;
+    lo3 = off;
+    hi3 = eps ? off + n : off;
+    lo1 = off;
+    hi1 = !eps && ss.z == P.label ? off + n : off;
+  } else if (n <= 64) {
     const uint32_t lane = lane_id();
     const bool v = lane < n;
     const uint32_t x = v ? rhs.il[FB(off + lane, rhs.num_arcs, 2)] : 0u;
