@@ -440,7 +440,12 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       dbg_pops = pops;
       dbg_qn = qn;
       dbg_nn = nn;
-      LZ_WD(1);
+      // the watchdog every 16 pops: the loops inside a pop are bounded by the pop's
+      // candidates and the heap depth (an s_memrealtime round trip per inner iteration
+      // had sat on the pop's critical path)
+      if ((pops & 15u) == 0) {
+        LZ_WD(1);
+      }
       if (dead || ++pops > ws.max_pops) {  // a heap yields only as many items as were pushed
         fail = kPathInternal;
         break;
@@ -456,7 +461,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         for (;;) {
           const uint32_t c0 = i * 64 + 1;
           if (c0 >= qn) break;
-          LZ_WD(2);
           if (dead) break;
           const uint32_t cc = c0 + lane;
           const bool v = cc < qn;
@@ -537,7 +541,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       dbg_C = C;
       for (uint32_t cb = 0; cb < C; cb += 64) {
         dbg_cb = cb;
-        LZ_WD(3);
         if (dead) {
           fail = kPathInternal;
           break;
@@ -568,7 +571,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         uint32_t leader = lane;
         unsigned long long pending = __ballot(need);
         while (pending) {
-          LZ_WD(4);
           if (dead) break;
           const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
           const unsigned long long lk =
@@ -676,7 +678,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         {
           unsigned long long pend = __ballot(act);
           while (pend) {
-            LZ_WD(5);
             if (dead) break;
             const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
             const uint32_t lt2 = __builtin_amdgcn_readlane(tid, l);
@@ -730,7 +731,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         // pushes in lane order, one lane at a time (sift-up is short in practice)
         unsigned long long pm = __ballot(push);
         while (pm) {
-          LZ_WD(6);
           if (dead) {
             fail = kPathInternal;
             break;
