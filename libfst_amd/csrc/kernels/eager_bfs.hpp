@@ -1204,13 +1204,17 @@ eager_bfs_kernel(RhsView rhs, ChainInput in, GraphInput graph, uint32_t n_best,
       ++level;
       if (tid == 0) T.lvl[level + 1] = n_nodes;
       __syncthreads();
-      if (__builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {  // uniform per wave...
-        if (tid == 0) SH.flag = 1;
-      }
-      __syncthreads();
-      if (SH.flag) {  // ...made uniform for the workgroup through LDS
-        fail = kPathInternal;
-        break;
+      // the watchdog every 8 levels (a level's work is bounded by its tuples and arcs; the
+      // s_memrealtime round trip and its barrier had sat in every level's latency)
+      if ((level & 7u) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ws.wd_ticks) {  // uniform per wave...
+          if (tid == 0) SH.flag = 1;
+        }
+        __syncthreads();
+        if (SH.flag) {  // ...made uniform for the workgroup through LDS
+          fail = kPathInternal;
+          break;
+        }
       }
     }
     const uint32_t n_levels = level;
