@@ -191,6 +191,11 @@ FstHandle fst_load_att(const char* path, uint32_t flags);
 /* Header weight type of a frozen FST: 0 tropical, 1 log, -1 invalid handle. */
 int32_t fst_weight_type(FstHandle b);
 
+/* Diagnostics: the coalescer of single fst_compose_frozen_shortest_path calls on `device`
+ * (leader slots in use, calls waiting in its queue).  Both are 0 when no call is in
+ * flight; tests check that no slot leaks.  Returns -1 for a negative device. */
+int32_t fst_debug_coalescer_state(int32_t device, uint32_t* queued);
+
 #ifdef __cplusplus
 }
 #endif

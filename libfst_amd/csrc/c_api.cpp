@@ -684,6 +684,17 @@ FstError shard_download(Shard& S, FstBatchResult* out, uint64_t arc_base) {
 FstError run_sharded(const std::vector<int>& devices, uint32_t nsh, uint32_t num,
                      const std::vector<double>& cost,
                      const std::function<FstError(Shard&)>& compute, FstBatchResult* out) {
+  // shard 0 runs on the calling thread and switches its current device: give the caller
+  // its device back on every return (later calls that use current_device() rely on it)
+  struct DeviceRestore {
+    int dev = -1;
+    DeviceRestore() {
+      if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceRestore() {
+      if (dev >= 0) (void)hipSetDevice(dev);
+    }
+  } restore;
   nsh = std::max<uint32_t>(1, std::min<uint32_t>(nsh, std::max<uint32_t>(num, 1)));
   std::vector<Shard> sh(nsh);
   if (nsh == 1) {
@@ -885,7 +896,7 @@ struct ChainCall {
   // so a finished batch wakes exactly its callers and one queued caller to lead next
   std::condition_variable cv;
   bool done = false;
-  bool lead = false;
+  bool taken = false;  // in a leader's batch
 };
 
 struct ChainCombiner {
@@ -961,34 +972,32 @@ FstError coalesced_chain_call(int dev, ChainCall* c) {
   ChainCombiner& C = chain_combiner(dev);
   std::unique_lock<std::mutex> lk(C.mu);
   C.q.push_back(c);
-  if (C.leaders < kChainLeaders) {
-    c->lead = true;
-    ++C.leaders;
+  // a call leads when a leader slot is free and no leader has taken it yet; a slot is only
+  // ever taken here, by the thread itself under the lock, and given back by the same thread
+  // after its batch, so slots can be neither lost nor duplicated (round-3 ADVICE)
+  c->cv.wait(lk, [&] { return c->done || (!c->taken && C.leaders < kChainLeaders); });
+  if (c->done) return c->err;
+  ++C.leaders;
+  // this call first, then the oldest queued ones
+  auto it = std::find(C.q.begin(), C.q.end(), c);
+  C.q.erase(it);
+  C.q.push_front(c);
+  const size_t take = std::min(C.q.size(), kChainMaxBatch);
+  std::vector<ChainCall*> batch(C.q.begin(), C.q.begin() + take);
+  C.q.erase(C.q.begin(), C.q.begin() + take);
+  for (ChainCall* x : batch) x->taken = true;
+  // a second free slot: let the oldest remaining caller lead a batch beside this one
+  if (!C.q.empty() && C.leaders < kChainLeaders) C.q.front()->cv.notify_one();
+  lk.unlock();
+  run_chain_calls(dev, batch);
+  lk.lock();
+  for (ChainCall* x : batch) {
+    x->done = true;
+    if (x != c) x->cv.notify_one();
   }
-  for (;;) {
-    c->cv.wait(lk, [c] { return c->done || c->lead; });
-    if (c->done) return c->err;
-    // leading: take the queue (this call is in it: a leader is picked from the queue)
-    c->lead = false;
-    const size_t take = std::min(C.q.size(), kChainMaxBatch);
-    std::vector<ChainCall*> batch(C.q.begin(), C.q.begin() + take);
-    C.q.erase(C.q.begin(), C.q.begin() + take);
-    lk.unlock();
-    run_chain_calls(dev, batch);
-    lk.lock();
-    for (ChainCall* x : batch) {
-      x->done = true;
-      if (x != c) x->cv.notify_one();
-    }
-    // hand the lead to the oldest queued caller, or retire
-    if (!C.q.empty()) {
-      C.q.front()->lead = true;
-      C.q.front()->cv.notify_one();
-    } else {
-      --C.leaders;
-    }
-    if (c->done) return c->err;
-  }
+  --C.leaders;
+  if (!C.q.empty()) C.q.front()->cv.notify_one();
+  return c->err;
 }
 
 }  // namespace
@@ -1768,6 +1777,14 @@ double fst_chain_cost(FstHandle b, uint64_t len) {
   std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(b);
   return f ? f->chain_cost(len) : -1.0;
+}
+
+int32_t fst_debug_coalescer_state(int32_t device, uint32_t* queued) {
+  if (device < 0) return -1;
+  ChainCombiner& C = chain_combiner(device);
+  std::lock_guard<std::mutex> g(C.mu);
+  if (queued) *queued = (uint32_t)C.q.size();
+  return C.leaders;
 }
 
 int32_t fst_weight_type(FstHandle b) {

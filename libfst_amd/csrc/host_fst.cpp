@@ -9,6 +9,8 @@
 #include <cerrno>
 #include <cmath>
 #include <cctype>
+#include <exception>
+#include <new>
 #include <cstdlib>
 #include <string>
 #include <thread>
@@ -62,10 +64,26 @@ bool parse_weight(const char* b, const char* e, double* out) {
 }  // namespace
 
 bool MutableFst::read_text(const char* data, size_t len, MutableFst* out) {
+  // a state id asks for that many states (ensure below): a huge one fails the allocation,
+  // which must come back as an error, not cross the C ABI as an exception
+  try {
+    return read_text_impl(data, len, out);
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+bool MutableFst::read_text_impl(const char* data, size_t len, MutableFst* out) {
   MutableFst f;
   bool start_set = false;
+  // states up to the largest id named (the reference adds them one by one and fails with
+  // OutOfMemory when they do not fit): a table larger than the host's physical memory is
+  // refused up front instead of being left to the allocator and overcommit
+  const size_t phys = (size_t)sysconf(_SC_PHYS_PAGES) * (size_t)sysconf(_SC_PAGESIZE);
   auto ensure = [&](uint32_t s) {
-    if (f.num_states() <= s) f.add_states((size_t)s + 1 - f.num_states());
+    if (f.num_states() > s) return;
+    if (((size_t)s + 1) * sizeof(State) > phys) throw std::bad_alloc();
+    f.add_states((size_t)s + 1 - f.num_states());
   };
   const char* p = data;
   const char* end = data + len;

@@ -53,6 +53,7 @@ class MutableFst {
   // readText, src/io/text.zig:20-115 (OpenFst AT&T text: "src dest il [ol] [w]" arcs,
   // "state [w]" finals, first source = start).  Returns false for error.InvalidFormat.
   static bool read_text(const char* data, size_t len, MutableFst* out);
+  static bool read_text_impl(const char* data, size_t len, MutableFst* out);
   // att2lfst's label normalisation (src/tools/att2lfst.zig:54-60): every non-epsilon
   // ilabel / olabel + 1 (OpenFst byte labels -> libfst's byte + 1 convention).
   void shift_labels();

@@ -436,14 +436,17 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
     int32_t fail = kPathOk;
 
     uint32_t pops = 0, pushes = 1;
+    uint32_t wd_work = 256;  // candidates since the last watchdog read (read at once)
     while (qn > 0) {
       dbg_pops = pops;
       dbg_qn = qn;
       dbg_nn = nn;
-      // the watchdog every 16 pops: the loops inside a pop are bounded by the pop's
-      // candidates and the heap depth (an s_memrealtime round trip per inner iteration
-      // had sat on the pop's critical path)
-      if ((pops & 15u) == 0) {
+      // the watchdog once per ~256 candidates (16 pops of 16; a pop with more candidates
+      // also reads it every 64 chunks below): an s_memrealtime round trip per inner loop
+      // iteration had sat on the pop's critical path, and the loops inside one chunk
+      // (sift-down, dedup, grouping: at most the heap depth or 64 iterations) need none
+      if (wd_work >= 256u) {
+        wd_work = 0;
         LZ_WD(1);
       }
       if (dead || ++pops > ws.max_pops) {  // a heap yields only as many items as were pushed
@@ -461,7 +464,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         for (;;) {
           const uint32_t c0 = i * 64 + 1;
           if (c0 >= qn) break;
-          if (dead) break;
           const uint32_t cc = c0 + lane;
           const bool v = cc < qn;
           const double cd = v ? qd[cc] : 0.0;
@@ -536,11 +538,15 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
       else prepare_chain(rhs, cl, P);
       const uint32_t C = P.n1 + P.n2 + P.n3 + P.n4;
       relax_count += C;
+      wd_work += C + 16u;
       double cur_dist = pdist;  // dist[curr_id]; changes only through a self-loop
 
       dbg_C = C;
       for (uint32_t cb = 0; cb < C; cb += 64) {
         dbg_cb = cb;
+        if (cb != 0 && (cb & 4095u) == 0) {
+          LZ_WD(2);
+        }
         if (dead) {
           fail = kPathInternal;
           break;
@@ -571,7 +577,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         uint32_t leader = lane;
         unsigned long long pending = __ballot(need);
         while (pending) {
-          if (dead) break;
           const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
           const unsigned long long lk =
               ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(x.key >> 32), l) << 32) |
@@ -580,10 +585,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
           const unsigned long long m = __ballot(same);
           if (same) leader = l;
           pending &= ~m;
-        }
-        if (dead) {
-          fail = kPathInternal;
-          break;
         }
         const bool is_new_leader = need && leader == lane;
         const unsigned long long nlm = __ballot(is_new_leader);
@@ -678,7 +679,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         {
           unsigned long long pend = __ballot(act);
           while (pend) {
-            if (dead) break;
             const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
             const uint32_t lt2 = __builtin_amdgcn_readlane(tid, l);
             const bool same = act && tid == lt2;
@@ -686,10 +686,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             if (lane == l) gmask = m;
             pend &= ~m;
           }
-        }
-        if (dead) {
-          fail = kPathInternal;
-          break;
         }
         bool push = false;
         double push_d = 0.0;
@@ -731,10 +727,6 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
         // pushes in lane order, one lane at a time (sift-up is short in practice)
         unsigned long long pm = __ballot(push);
         while (pm) {
-          if (dead) {
-            fail = kPathInternal;
-            break;
-          }
           const uint32_t l = (uint32_t)__ffsll((long long)pm) - 1;
           pm &= pm - 1;
           const unsigned long long pb2 = (unsigned long long)__double_as_longlong(push_d);

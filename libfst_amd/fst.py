@@ -122,6 +122,7 @@ SIGNATURES = {
     "fst_weight_type": (C.c_int32, [_u64]),
     "fst_read_text": (_u64, [C.c_char_p]),
     "fst_chain_cost": (_f64, [_u64, _u64]),
+    "fst_debug_coalescer_state": (C.c_int32, [C.c_int32, C.POINTER(_u32)]),
     "fst_load_att": (_u64, [C.c_char_p, _u32]),
     "fst_device_project_output": (C.c_int, [C.c_void_p, _u32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(_u32), C.c_void_p]),
@@ -410,6 +411,12 @@ def _take_result(res, num) -> BatchResult:
                        olabels=arr(res.olabels, tot, np.uint32, C.c_uint32),
                        weights=arr(res.weights, tot, np.float64, C.c_double),
                        finals=arr(res.final_weights, num, np.float64, C.c_double))
+
+
+def coalescer_state(device: int = 0):
+    """(leader slots in use, queued calls) of the single-call coalescer on `device`."""
+    q = _u32(0)
+    return int(lib().fst_debug_coalescer_state(device, C.byref(q))), int(q.value)
 
 
 def last_launch_stats() -> FstLaunchStats:

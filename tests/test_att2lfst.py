@@ -84,7 +84,7 @@ def test_att_forms_and_errors(tmp_path):
     ref = O.read_att(text)
     assert F.MutableFst.read_text(p).to_lists() == (ref.start, ref.finals, ref.arcs)
     for bad in ("x 1 2 3\n", "0 1 a 2\n", "0 1 2 3 4 5\n", "0 1.5 7\n", "0 -1 2 3\n",
-                "4294967296 1 2\n"):
+                "4294967296 1 2\n", "4294967295 1 2\n", "0 4294967295 7\n"):
         pb = write(str(tmp_path), "bad.att", bad)
         with pytest.raises(ValueError):
             F.MutableFst.read_text(pb)

@@ -67,6 +67,30 @@ def test_threads_single_chain_calls():
     run_threads(32, work)
 
 
+def test_coalescer_slots_never_leak():
+    # round-3 ADVICE: a leader slot handed to a caller that another leader had already taken
+    # into its batch was lost, and after two such losses every later call waited forever.
+    # Many threads with short strings make such hand-offs frequent; afterwards no slot may
+    # be held and no call queued, and a lone call must still complete.
+    blob = O.freeze(O.gen("ambiguous", 64, 4))
+    rhs = load_blob(blob)
+    texts = [bytes([0] * L) for L in (0, 1, 2, 5, 9)]
+    expect = [oracle_single(O.compile_string(t), blob) for t in texts]
+
+    def work(t):
+        for i in range(60):
+            k = (t + i) % len(texts)
+            got = F.compose_frozen_shortest_path(F.MutableFst.compile_string(texts[k]), rhs, 1)
+            g = None if got is None else norm(*got.to_lists())
+            assert g == expect[k], (t, i, k)
+    for _ in range(3):
+        run_threads(96, work)
+        assert F.coalescer_state(0) == (0, 0)
+    got = F.compose_frozen_shortest_path(F.MutableFst.compile_string(texts[3]), rhs, 1)
+    assert norm(*got.to_lists()) == expect[3]
+    assert F.coalescer_state(0) == (0, 0)
+
+
 def test_threads_mixed_entries():
     # chain calls, general-lhs calls, fst_compose_frozen, fst_shortest_path and batch calls
     # at the same time, each against the oracle
