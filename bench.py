@@ -8,8 +8,10 @@ pass of the engine over a device-resident batch of --batch strings per GPU (defa
 
 N GPUs: one process per GPU (torchrun); the frozen rhs blob is built on rank 0 and
 broadcast once over xGMI with RCCL (torch.distributed "nccl"), then adopted by every
-rank (fst_device_adopt_blob).  No per-step collectives: each rank runs its own shard
-(weak scaling); timing is barrier + synchronize on both sides, max over ranks.
+rank (fst_device_adopt_blob).  No per-step collectives: each rank runs its own shard;
+timing is barrier + synchronize on both sides, max over ranks.  The metric's form is
+"batch=1M, 1/2/4/8 GPU": by default the 1M strings of a step are split over the ranks
+(--scaling strong, --global-batch); --scaling weak gives every rank --batch strings.
 """
 import argparse
 import ctypes as C
@@ -130,7 +132,18 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch", type=int, default=1 << 20, help="strings per GPU per step")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="strong: --global-batch strings per step split over the ranks (the "
+                        "metric's batch=1M at 1/2/4/8 GPUs); weak: --batch strings per rank")
+    p.add_argument("--global-batch", type=int, default=1 << 20,
+                   help="strong scaling: strings per step over all GPUs")
+    p.add_argument("--batch", type=int, default=1 << 20,
+                   help="weak scaling: strings per GPU per step")
+    p.add_argument("--backend", default="nccl",
+                   help="torch.distributed backend (nccl = RCCL; gloo for ranks sharing a GPU "
+                        "in tests)")
+    p.add_argument("--no-f64", dest="f64", action="store_false",
+                   help="skip the f64-cell and fractional-weight legs")
     p.add_argument("--len", type=int, default=64)
     p.add_argument("--transducer-len", type=int, default=4096)
     p.add_argument("--branches", type=int, default=12)
@@ -261,10 +274,15 @@ def timed(batch, rhs, sem, dev_index, steps, warmup, world):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{dev_index}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = max_over_ranks(el, dev_index)
     return el, kms, st
+
+
+def max_over_ranks(x, dev_index):
+    on = f"cuda:{dev_index}" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def nproc():
@@ -326,6 +344,45 @@ def cpu_baseline(args, blob_bytes, sem, seconds=None):
                       f"on {threads} host threads (= nproc), oracle/fst_oracle.c -O3, {s:.1f} s"}
 
 
+def fractional_ambiguous(T, B, delta=0.5):
+    """The metric's ambiguous-chain rhs (bench/optimize-bench.zig:250-277) with every arc
+    weight + delta (a WeText-like fractional grammar weight): built through the library's
+    MutableFst API and frozen (fst_freeze).  Distances stop being integers, so the pull
+    tiers take their f64 cells (src/weight.zig:15-37 semantics throughout)."""
+    m = F.MutableFst()
+    for _ in range(T + 1):
+        m.add_state()
+    m.set_start(0)
+    fan = max(1, min(B, 4))
+    for i in range(T + 1):
+        m.set_final(i, 0.0)
+        m.add_arc(i, 1, 1, 0.0 + delta, i)
+        for b in range(fan):
+            m.add_arc(i, 1, ((i + b) % 255) + 1, float(b) + delta, min(i + b + 1, T))
+    return m.freeze()
+
+
+def leg(batch, rhs, sem, dev_index, world, total_per_step, blob, env=None, steps=3):
+    """One extra timed leg on the metric batch (3 steps after 1 warm-up), every string OK
+    and the first 256 bit-compared with the oracle.  env: variables set for the leg only
+    (read by the library at each call)."""
+    env = env or {}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        el, kms, st = timed(batch, rhs, sem, dev_index, steps, 1, world)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    status = batch.status.cpu().numpy()
+    assert np.all(status == F.FST_PATH_OK), np.unique(status, return_counts=True)
+    return {"value": total_per_step * steps / el, "kernel_ms": float(np.mean(kms)),
+            "checked_vs_oracle": check_sample(batch, blob, sem)}
+
+
 def end_to_end(args, rhs, sem, dev_index, steps=3, warmup=1):
     """The host batch entry fst_compose_frozen_shortest_path_batch on the metric batch: host
     labels in, H2D, kernels, device CSR compaction, D2H into pooled pinned host arrays,
@@ -355,19 +412,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; ranks beyond the visible devices share them (gloo tests only)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
     sem = F.FST_SEM_EAGER if args.semantics == "eager" else F.FST_SEM_LAZY
+    if args.scaling == "strong":  # this rank's contiguous share of the global batch
+        b0, b1 = D.shard_range(args.global_batch, rank, world)
+        args.batch = b1 - b0
+    total_per_step = args.global_batch if args.scaling == "strong" else args.batch * world
 
     # ---- rhs: built on rank 0, broadcast once over xGMI (RCCL), adopted on every rank ----
     blob_host = None
     if rank == 0:
         blob_host = D.blob_bytes(
             F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, args.transducer_len, args.branches))
-    if world > 1:
+    if world > 1 and args.backend == "nccl":
         buf = D.broadcast_blob(blob_host, rank, dev)
+    elif world > 1:  # gloo: broadcast through host memory
+        buf = D.broadcast_blob(blob_host, rank, torch.device("cpu")).to(dev)
     else:
         buf = torch.frombuffer(bytearray(blob_host), dtype=torch.uint8).to(dev)
     rhs = D.adopt_on_device(buf, local)
@@ -392,7 +460,7 @@ def main():
     torch.cuda.synchronize()
     work = batch.work.cpu().numpy().astype(np.int64)
 
-    total_strings = args.batch * args.steps * world
+    total_strings = total_per_step * args.steps
     value = total_strings / el
     avg_k = float(np.mean(kms))
     balg = b_alg_bytes(work, lengths, plen)   # bytes per launch on this rank
@@ -408,7 +476,7 @@ def main():
             return x + kill
         vb = DeviceBatch(vl, vlabels, dev)
         vel, vk, _ = timed(vb, rhs, sem, local, args.steps, args.warmup, world)
-        extra["varied"] = {"value": args.batch * args.steps * world / vel,
+        extra["varied"] = {"value": total_per_step * args.steps / vel,
                            "kernel_ms": float(np.mean(vk)),
                            "lengths": "uniform 1..%d, ~10%% strings with a dead label" % L,
                            "checked_vs_oracle": check_sample(vb, blob_check, sem)}
@@ -421,7 +489,10 @@ def main():
         lel, lk, _ = timed(lb, rhs, F.FST_SEM_LAZY, local, 3, 1, world)
         ls = lb.status.cpu().numpy()
         assert np.all(ls == F.FST_PATH_OK)
-        extra["lazy"] = {"value": args.lazy_batch * 3 * world / lel, "kernel_ms": float(np.mean(lk)),
+        lazy_total = args.lazy_batch * world
+        if args.scaling == "strong" and args.lazy_batch == args.batch:
+            lazy_total = total_per_step
+        extra["lazy"] = {"value": lazy_total * 3 / lel, "kernel_ms": float(np.mean(lk)),
                          "batch": args.lazy_batch,
                          "checked_vs_oracle": check_sample(lb, blob_check, F.FST_SEM_LAZY),
                          "note": "fst_compose_frozen_shortest_path semantics (lazy_pull_kernel, exact vs the oracle)"}
@@ -429,15 +500,34 @@ def main():
         if rank == 0 and not args.no_cpu and world == 1:  # the CPU port beside it (~3 s)
             extra["lazy"]["cpu_baseline"] = cpu_baseline(args, blob_check, 0, seconds=3.0)
 
+    if args.f64:
+        # the f64-cell rates beside the headline: the f32 cells above hold only because the
+        # metric's weights are small integers; fractional grammar weights take f64 cells
+        E, Lz = F.FST_SEM_EAGER, F.FST_SEM_LAZY
+        extra["f64_cells"] = {
+            "eager": leg(batch, rhs, E, local, world, total_per_step, blob_check,
+                         {"FSTAMD_P_F64": "1"}),
+            "lazy": leg(batch, rhs, Lz, local, world, total_per_step, blob_check,
+                        {"FSTAMD_LP_F64": "1"}),
+            "note": "same metric batch and rhs, the pull kernels forced to f64 cells "
+                    "(FSTAMD_P_F64 / FSTAMD_LP_F64)"}
+        fr = fractional_ambiguous(args.transducer_len, args.branches)
+        fr_blob = D.blob_bytes(fr)
+        extra["fractional_weights"] = {
+            "eager": leg(batch, fr, E, local, world, total_per_step, fr_blob),
+            "lazy": leg(batch, fr, Lz, local, world, total_per_step, fr_blob),
+            "rhs": f"ambiguous chain T={args.transducer_len} B={args.branches}, every arc "
+                   "weight + 0.5 (f64 cells)"}
+        del fr
+
     if args.e2e:
         del batch
         torch.cuda.empty_cache()
         extra["end_to_end"] = end_to_end(args, rhs, sem, local)
         if world > 1:  # every rank ran its own; report the slowest as the job's rate
-            t = torch.tensor([extra["end_to_end"]["ms_per_call"]], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            extra["end_to_end"]["ms_per_call"] = float(t.item())
-            extra["end_to_end"]["value"] = args.batch * world / (float(t.item()) * 1e-3)
+            ms = max_over_ranks(extra["end_to_end"]["ms_per_call"], local)
+            extra["end_to_end"]["ms_per_call"] = ms
+            extra["end_to_end"]["value"] = total_per_step / (ms * 1e-3)
 
     if rank == 0:
         traffic, traffic_src = measured_traffic(args, sem)
@@ -453,7 +543,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             # results and the CPU port are f64; on this integer-weight rhs the pull tiers
             # keep the cells' distances in f32, exact (every distance an integer < 2^24),
@@ -466,8 +556,12 @@ def main():
                        "semantics": args.semantics, "len": L,
                        "transducer_len": args.transducer_len, "branches": args.branches,
                        "strings_per_gpu": args.batch,
-                       "global_batch": args.batch * world,
-                       "parallelism": f"dp{world} (string shards, rhs replicated via RCCL broadcast)"},
+                       "global_batch": total_per_step,
+                       "scaling_mode": (f"strong: {total_per_step} strings per step split over "
+                                        f"{world} GPU(s)" if args.scaling == "strong" else
+                                        f"weak: {args.batch} strings per GPU per step"),
+                       "parallelism": f"dp{world} (string shards, rhs replicated via "
+                                      f"{'RCCL' if args.backend == 'nccl' else args.backend} broadcast)"},
             "roofline": roofline_block(args, sem, avg_k, balg, work, lengths, plen, traffic,
                                        traffic_src),
             "cpu_baseline": cpu,

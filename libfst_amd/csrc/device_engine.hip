@@ -905,11 +905,19 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     if (todo_n > 0) {
       // the band replay first (rhs whose arcs all go forward: config 3), the dense replay
       // for what it hands on
-      bool band = false;
-      HIP_TRY(run_lazy_band(rhs, in, n, out, stream, &band, todo, todo ? todo_n : 0));
-      if (band) {
+      // With the exact early exit a string only reaches ~2 L states past the start
+      // (config 3: DESIGN.md §4.2c), so the first launch keeps back pointers for a few
+      // windows of states; what reaches further runs again over the whole rhs.
+      const bool early_ok = rhs.nonneg && rhs.finite && !std::getenv("FSTAMD_NO_EARLY");
+      for (int pass = early_ok ? 0 : 1; pass < 2 && todo_n > 0; ++pass) {
+        bool band = false;
+        HIP_TRY(run_lazy_band(rhs, in, n, out, stream, &band, todo, todo ? todo_n : 0,
+                              pass == 0));
+        if (!band) break;
         if (stats) stats->launches += 1;
-        uint32_t* la = (uint32_t*)scratch(kItems, (size_t)in.num_strings * 4);
+        // (the list `todo` may be kItems or kItems2: the next one goes elsewhere)
+        uint32_t* la = (uint32_t*)scratch(pass == 0 ? kItems3 : kItems4,
+                                          (size_t)in.num_strings * 4);
         if (!la) return hipErrorOutOfMemory;
         unsigned int* c = counter + 46;  // [46] |la|
         HIP_TRY(hipMemsetAsync(c, 0, 4, stream));
@@ -920,7 +928,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
         HIP_TRY(hipStreamSynchronize(stream));
         todo = la;
         if (std::getenv("FSTAMD_ROUTE_LOG"))
-          std::fprintf(stderr, "[libfst_amd route] lazy: band replay handed on %u\n", todo_n);
+          std::fprintf(stderr, "[libfst_amd route] lazy: band replay (%s) handed on %u\n",
+                       pass == 0 ? "capped, early exit" : "whole rhs", todo_n);
       }
     }
     if (todo_n > 0) {
@@ -1265,9 +1274,11 @@ constexpr size_t kLdMaxDynLds = 150 * 1024;
 // the rounds engine, take them).  subset_dev: the strings to run (nullptr: all).
 hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                        const BatchOutDev& out, hipStream_t stream, bool* ran,
-                                       const uint32_t* subset_dev, uint32_t subset_n) {
+                                       const uint32_t* subset_dev, uint32_t subset_n,
+                                       bool capped) {
   *ran = false;
   if (rhs.view.jump_back != 0 || std::getenv("FSTAMD_NO_BAND")) return hipSuccess;
+  if (rhs.view.start >= rhs.view.num_states) capped = false;  // (no start: all EMPTY)
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [36] is ours
   if (!ctr) return hipErrorOutOfMemory;
   // the strings and their lengths on the host (plans, buckets, longest first)
@@ -1293,8 +1304,10 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len(a) < len(b); });
   const uint32_t NS = rhs.view.num_states;
   constexpr uint32_t kRing = 4096, kFcap = 65536;
+  // states past the start (every reachable state is: arcs go forward)
+  const uint32_t srange = rhs.view.start < NS ? NS - rhs.view.start : NS;
   struct Plan {
-    uint32_t lcap, wstates, grid, first, count;
+    uint32_t lcap, wstates, scap, grid, first, count;
     uint64_t wn, tn;
     size_t lds;
   };
@@ -1338,7 +1351,8 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     if (wse) w = std::max<uint32_t>(64, 1u << (31 - __builtin_clz((uint32_t)std::max(1, std::atoi(wse)))));
     p.wstates = w;
     p.wn = (uint64_t)w * (p.lcap + 1) * 2;
-    p.tn = (uint64_t)(p.lcap + 1) * NS * 2;  // ids and tuple indices fit 31 bits
+    p.scap = capped ? std::min<uint32_t>(srange, 2 * w) : srange;
+    p.tn = (uint64_t)(p.lcap + 1) * p.scap * 2;  // ids and tuple indices fit 31 bits
     if (p.tn > kLdDenseMax) return false;
     p.lds = kRing / 8 + (size_t)p.lcap * 4;
     if (p.lds > kLdMaxDynLds) return false;
@@ -1398,8 +1412,12 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)gmax * kLbProf * 8, stream));
   ws.ring = kRing;
   ws.fcap = kFcap;
+  // the exact early exit needs every arc and final weight >= +0, finite
+  // arcs; FSTAMD_NO_EARLY=1 replays the whole product as the reference does (tests, A/B)
+  ws.early = (rhs.nonneg && rhs.finite && !std::getenv("FSTAMD_NO_EARLY")) ? 1u : 0u;
   for (const Plan& p : plans) {
     ws.lcap = p.lcap;
+    ws.scap = p.scap;
     ws.ws = p.wstates;
     ws.wn = p.wn;
     ws.tn = p.tn;
@@ -1419,14 +1437,18 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     std::vector<unsigned long long> h((size_t)gmax * kLbProf);
     HIP_TRY(hipMemcpyAsync(h.data(), ws.prof, h.size() * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    unsigned long long sum[8] = {};
-    for (size_t w = 0; w < gmax; ++w)
+    unsigned long long sum[8] = {}, ee = 0, oc = 0;
+    for (size_t w = 0; w < gmax; ++w) {
       for (int j = 0; j < 8; ++j) sum[j] += h[w * kLbProf + j];
+      ee += h[w * kLbProf + 16];
+      oc += h[w * kLbProf + 17];
+    }
     const double it = (double)std::max(1ull, sum[3]);
     std::fprintf(stderr, "[lazy-band prof] grid %u items %llu | per item: pops %.0f advances "
-                 "%.1f slides %.1f | overflows: window %llu ids %llu future %llu ring %llu\n",
-                 gmax, sum[3], sum[0] / it, sum[1] / it, sum[2] / it, sum[4], sum[5], sum[6],
-                 sum[7]);
+                 "%.1f slides %.1f | early exits %llu | overflows: window %llu ids %llu future "
+                 "%llu ring %llu states %llu\n",
+                 gmax, sum[3], sum[0] / it, sum[1] / it, sum[2] / it, ee, sum[4], sum[5], sum[6],
+                 sum[7], oc);
     if (kLbProf > 306) {
       unsigned long long tt[6] = {};
       for (size_t w = 0; w < gmax; ++w)

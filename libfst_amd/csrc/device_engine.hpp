@@ -350,10 +350,13 @@ class DeviceEngine {
   // 1 = 128 tuples, 2 = 256) over a device list of strings (nullptr: all); strings whose
   // lattice outgrows it end OVERFLOW.
   // The band replay (kernels/lazy_band.hpp); *ran = false when the rhs or the batch is not
-  // its (arcs going backwards, lengths > 4095); strings it hands on end OVERFLOW.
+  // its (arcs going backwards, lengths > 4095); strings it hands on end OVERFLOW.  capped:
+  // back pointers only for the first 2 x window states past the start (the early exit's
+  // footprint), strings reaching beyond end OVERFLOW.
   hipError_t run_lazy_band(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                            const BatchOutDev& out, hipStream_t stream, bool* ran,
-                           const uint32_t* subset_dev = nullptr, uint32_t subset_n = 0);
+                           const uint32_t* subset_dev = nullptr, uint32_t subset_n = 0,
+                           bool capped = false);
   hipError_t launch_lazy_hashed(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                 const BatchOutDev& out, hipStream_t stream, uint64_t want_nodes,
                                 const uint32_t* items, uint32_t num_items, unsigned int* ctr,

@@ -43,7 +43,7 @@ namespace fstamd {
 #if defined(FSTAMD_BAND_DEBUG) || defined(FSTAMD_BAND_TIMING)
 constexpr uint32_t kLbProf = 512;  // per-wave profile words (+ the phase timing)
 #else
-constexpr uint32_t kLbProf = 16;
+constexpr uint32_t kLbProf = 20;
 #endif
 
 struct LbWs {
@@ -58,9 +58,13 @@ struct LbWs {
   uint32_t ws;                // window states (power of two)
   uint32_t ring;              // ids kept (power of two, multiple of 4096)
   uint32_t fcap, lcap;
+  uint32_t scap;              // back pointers for states [start, start + scap) (a target
+                              // beyond: OVERFLOW, the next launch has the whole rhs)
+  uint32_t early;             // 1: exact early exit (weights and finals >= +0, finite)
   unsigned long long wd_ticks, wd_tuple_ticks;
-  unsigned long long* prof;   // [grid * 16] (FSTAMD_BFS_PROF): pops, advances, slides, items,
-                              // overflows by site (4..7), the wave's last overflow (8..15)
+  unsigned long long* prof;   // [grid * kLbProf] (FSTAMD_BFS_PROF): pops, advances, slides,
+                              // items, overflows by site (4..7), the wave's last overflow
+                              // (8..15), early exits (16), overflows past scap (17)
   const uint32_t* items;      // this launch's strings, or nullptr = all
   uint32_t num_items;
 };
@@ -97,8 +101,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   // then a scan over [nn - LS, nn) never meets one physical bitmap word twice, and the
   // ring slot of an open id is never reused
   const uint32_t LS = RING - 64;
+  const uint32_t S0 = rhs.start;  // every reachable state is >= S0 (arcs go forward)
+  const uint32_t SCAP = ws.scap;
   auto wix = [&](uint32_t k_, uint32_t s_) { return (s_ & wmask) * LC + k_; };  // x 2 + f
-  auto gix = [&](uint32_t k_, uint32_t s_) { return s_ * LC + k_; };            // x 2 + f
+  auto gix = [&](uint32_t k_, uint32_t s_) { return (s_ - S0) * LC + k_; };     // x 2 + f
   // back pointers: f_src | ds << 1 | local arc << (1 + dbits)
   uint8_t* bk8 = (uint8_t*)bkv;
   uint16_t* bk16 = (uint16_t*)bkv;
@@ -138,6 +144,23 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   uint32_t site = 0;  // INTERNAL / OVERFLOW: where it stopped (FSTAMD_BFS_PROF)
   uint32_t dbg_s = 0, dbg_t = 0;
   uint64_t relax = 0;
+  // exact early exit (ws.early): once the next pop is at dcur == best_total
+  // and every tuple with an id <= emax is settled, where emax bounds the ids on the best
+  // tuple's back chain, no later pop can change the best or a back pointer on that chain
+  const bool early = ws.early != 0;
+  uint32_t emax = 0;       // the largest id on the back chain when last walked (grows)
+  uint32_t fut_lb = ~0u;   // <= every live future entry's id (min pushed since the last scan)
+  uint32_t nn_slid = 0;    // every tuple that left the window has an id < nn_slid
+  uint32_t scan_gate = 0;  // pops before the next exact scan of the future list
+  bool stop = false;       // early exit taken
+  // back chain step by tuple (the result's walk below): g_'s back source tuple, a_ its arc
+  auto step = [&](uint32_t g_, uint32_t& a_) -> uint32_t {
+    const uint32_t c = bk_get(g_);
+    const uint32_t rs_ = (g_ >> 1) / LC, kk_ = (g_ >> 1) - rs_ * LC;
+    const uint32_t sp_ = S0 + rs_ - ((c >> 1) & dmask);
+    a_ = rhs.span[sp_].x + (c >> (1 + dbits));
+    return 2 * gix(kk_ - ((g_ & 1) ? 0u : 1u), sp_) + (c & 1);
+  };
 
   // open-at-dcur insert of lane-held ids: LDS bitmap bits (ds_or_b64, no return), the
   // cached word (one reduction when an id falls in it), lowp
@@ -216,6 +239,12 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       fn = wpos;
       if (!__ballot(any)) break;  // the queue is empty: done
       dcur = uni_f64(wave_min_f64(dmin));
+      // every later pop is at dcur > best_total: its total (final >= 0) and its relaxations
+      // of the chain (whose distances are <= best_total) can no longer win
+      if (early && best_id != kNoState && dcur > best_total) {
+        stop = true;
+        break;
+      }
       wpos = 0;
       cache = false;
       bool old = false;
@@ -244,6 +273,52 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     }
 
     LB_T(0);  // finding the next id (scans, advances)
+    if (early && best_id != kNoState && dcur == best_total &&
+        cur_base + (uint32_t)__ffsll((long long)cur_bits) - 1 > emax) {
+      // the next pop (the smallest open id at dcur) is past emax; the future list's live
+      // ids (above dcur) must be too -- its bound first, an exact scan (amortised) if not
+      if (fut_lb <= emax && pops >= scan_gate) {
+        uint32_t wpos = 0, mn = ~0u;
+        for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
+          const uint32_t e = e0 + lane;
+          const bool v = e < fn;
+          const uint4 en = v ? fut[e] : make_uint4(0, 0, 0, 0);
+          const uint4 rv = v ? R[en.z] : make_uint4(0, 0, kLdUntouched, 0);
+          const double ed = __hiloint2double((int)en.y, (int)en.x);
+          const bool live = v && rv.z == en.w && ld_dist(rv) == ed;
+          if (live) mn = min(mn, en.w);
+          const unsigned long long lm = __ballot(live);
+          if (live) fut[wpos + (uint32_t)__popcll(lm & lanemask_lt())] = en;
+          wpos += (uint32_t)__popcll(lm);
+        }
+        wave_fence();
+        fn = wpos;
+        fut_lb = uni(wave_min_u32d(mn));
+        scan_gate = pops + max(64u, fn / 16u);
+      }
+      if (fut_lb > emax) {
+        // the chain's ids now (lane 0 walks it): a tuple still in the window holds its id
+        // in its record; one that left it has an id < nn_slid
+        uint32_t m = best_id;
+        if (lane == 0) {
+          uint32_t g = best_g, a = 0, n = 0;
+          while (g != 0u && n++ <= nn) {
+            g = step(g, a);
+            const uint32_t rs = (g >> 1) / LC, kk = (g >> 1) - rs * LC, st = S0 + rs;
+            if (st >= slo && st - slo < WS)
+              m = max(m, Rw[4 * (size_t)(2 * wix(kk, st) + (g & 1)) + 2] & ~kLdSettled);
+            else
+              m = max(m, nn_slid);
+          }
+        }
+        m = uni(m);
+        if (m <= emax) {
+          stop = true;
+          break;
+        }
+        emax = m;
+      }
+    }
     // ---- pop (:159-163) ----
     const uint32_t pid = uni(cur_base + (uint32_t)__ffsll((long long)cur_bits) - 1);
     cur_bits = uni64(cur_bits & (cur_bits - 1));
@@ -291,6 +366,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         if (best_id == kNoState || total < best_total || (total == best_total && pid < best_id)) {
           best_id = pid;
           best_g = 2 * gix(k, s) + (x & 1);
+          emax = max(emax, pid);
           best_fw = fw;
           best_total = total;
         }
@@ -306,7 +382,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     uint32_t C = 0, lo1 = 0, n1 = 0, lo3 = 0, tmax = s;
     const bool small = na <= 64;
     // the targets' largest state only matters near the window's end (t - s <= jump_fwd)
-    const bool near_end = (uint64_t)s + rhs.jump_fwd >= (uint64_t)slo + WS;
+    const bool near_end = (uint64_t)s + rhs.jump_fwd >= min((uint64_t)slo + WS, (uint64_t)S0 + SCAP);
     if (small) {
       const bool v = lane < na;
       const uint32_t il = v ? rhs.il[aoff + lane] : 0xFFFFFFFFu;
@@ -345,6 +421,13 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     }
     tmax = uni(tmax);
     relax += C;
+    if (tmax - S0 >= SCAP) {  // beyond the back pointers' states: the next launch's
+      fail = kPathOverflow;
+      site = 10;
+      dbg_s = s;
+      dbg_t = tmax;
+      break;
+    }
 
     LB_T(2);  // candidates
     // ---- the window must hold every target: slide it up to the lowest state with an
@@ -401,6 +484,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       }
       wave_fence();
       slo = smin;
+      nn_slid = nn;
     }
 
     LB_T(3);  // slides
@@ -523,6 +607,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const unsigned long long fmk = __ballot(tof);
       if (tof) fut[fn + (uint32_t)__popcll(fmk & lanemask_lt())] = ld_rec(cd, tx, id);
       fn += (uint32_t)__popcll(fmk);
+      if (fmk && early) fut_lb = min(fut_lb, uni(wave_min_u32d(tof ? id : ~0u)));
       bucket_insert(tob, id);
       wave_fence();
       wave_lds_sync();
@@ -553,15 +638,8 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       if (best_id == kNoState) {
         st = kPathEmpty;
       } else {
-        // by tuple: the start tuple (0, start, 0) is id 0 (init_id, :372)
-        const uint32_t g0 = 2 * gix(0, rhs.start);
-        auto step = [&](uint32_t g_, uint32_t& a_) -> uint32_t {  // g_'s back source tuple
-          const uint32_t c = bk_get(g_);
-          const uint32_t st_ = (g_ >> 1) / LC, kk_ = (g_ >> 1) - st_ * LC;
-          const uint32_t sp_ = st_ - ((c >> 1) & dmask);
-          a_ = rhs.span[sp_].x + (c >> (1 + dbits));
-          return 2 * gix(kk_ - ((g_ & 1) ? 0u : 1u), sp_) + (c & 1);
-        };
+        // by tuple: the start tuple (0, start, 0) is id 0 (init_id, :372), index 0
+        const uint32_t g0 = 0;
         uint32_t cur = best_g, arc = 0;
         while (cur != g0) {
           if (++P > nn) {
@@ -605,11 +683,13 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       out.work[2 * si + 1] = (uint32_t)relax;
     }
     if (prof) {
+      if (stop) prof[16] += 1;
       prof[0] += pops;
       prof[1] += advances;
       prof[2] += slides;
       if (fail != kPathOk && site != 0) {
-        if (site >= 4) prof[site] += 1;
+        if (site >= 4 && site < 8) prof[site] += 1;
+        if (site == 10) prof[17] += 1;
         prof[8] = pops;  // the last failure of this wave
         prof[9] = site;
         prof[10] = dbg_s;

@@ -60,7 +60,7 @@ def main():
         stream = torch.cuda.current_stream().cuda_stream
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        st = b.run(rhs, F.FST_SEM_LAZY, 0, stream)
+        st = b.run(rhs, F.FST_SEM_LAZY, 0, stream, work=True)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         status = b.status.cpu().numpy()

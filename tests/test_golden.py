@@ -65,3 +65,23 @@ def test_gpu_matches_golden(name, sem):
         assert np.array_equal(got.olabels[a:b], e["olabels"][c:d])
         assert np.array_equal(got.weights[a:b].view(np.uint64), e["weights"][c:d].view(np.uint64))
     assert np.array_equal(got.finals[ok].view(np.uint64), e["finals"][ok].view(np.uint64))
+
+
+def test_oracle_reproduces_config3_fixture_short():
+    # tests/golden/config3_T65536.npz (config 3's full-size rhs, made by
+    # make_config3_golden.py): the oracle re-derives its shortest string here (L=44,
+    # 5.8 M tuples, ~10 s); the GPU suite checks all 8 (tests/test_gpu_fullsize.py)
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "config3_T65536.npz"),
+                allow_pickle=False)
+    lens = [int(x) for x in z["lengths"]]
+    i = int(np.argmin(lens))
+    blob = O.freeze(O.gen("eps_dense", int(z["T"]), int(z["B"])))
+    L = lens[i]
+    r = O.batch_run(blob, np.ones(L, np.uint32), np.array([0, L], np.uint64), 0)
+    a, b = int(z["offsets"][i]), int(z["offsets"][i + 1])
+    assert int(r.status[0]) == int(z["status"][i]) == 0
+    assert np.array_equal(r.ilabels, z["ilabels"][a:b])
+    assert np.array_equal(r.olabels, z["olabels"][a:b])
+    assert np.array_equal(r.weights.view(np.uint64), z["weights"][a:b].view(np.uint64))
+    assert r.finals.view(np.uint64)[0] == z["finals"].view(np.uint64)[i]
+    assert int(r.tuples[0]) == int(z["tuples"][i])

@@ -24,8 +24,19 @@ pytestmark = pytest.mark.gpu
 
 
 def handed_on(err):
-    m = re.findall(r"band replay handed on (\d+)", err)
+    """Strings each band launch handed on: the capped launch with the early exit, then
+    (if any) the whole-rhs launch."""
+    m = re.findall(r"band replay \([^)]*\) handed on (\d+)", err)
     return [int(x) for x in m]
+
+
+@pytest.fixture(params=["early", "full"])
+def early_mode(request, monkeypatch):
+    """Both ways of running the band: with the exact early exit (the default) and the
+    reference's whole-product replay (FSTAMD_NO_EARLY=1)."""
+    if request.param == "full":
+        monkeypatch.setenv("FSTAMD_NO_EARLY", "1")
+    return request.param
 
 
 @pytest.fixture
@@ -50,7 +61,7 @@ def forward_rhs(rng, ns, deg, jump, labels=3, wmax=2, frac=False, eps_loops=True
 
 
 @pytest.mark.parametrize("T", [1024, 3000])
-def test_eps_dense_slides(route, capfd, T):
+def test_eps_dense_slides(route, capfd, early_mode, T):
     blob = O.freeze(O.gen("eps_dense", T, 12))
     lens = [0, 1, 2, 11, 64, 130, 200, 251]
     check(blob, *csr([[1] * L for L in lens]), LAZY)
@@ -58,7 +69,7 @@ def test_eps_dense_slides(route, capfd, T):
 
 
 @pytest.mark.parametrize("seed", range(12))
-def test_random_forward(route, capfd, seed):
+def test_random_forward(route, capfd, early_mode, seed):
     rng = np.random.default_rng(7100 + seed)
     # deg / jump chosen so the back pointer takes 1 B (seeds 0-3), 2 B (4-7), 4 B (8-11)
     deg, jump = [(4, 3), (40, 5), (30, 5000)][seed // 4]
@@ -76,7 +87,8 @@ def test_window_too_small_falls_back(route, capfd, monkeypatch):
     blob = O.freeze(O.gen("eps_dense", 512, 12))
     lens = [70, 90, 151]  # open states span L + 3 > 64
     check(blob, *csr([[1] * L for L in lens]), LAZY)
-    assert handed_on(capfd.readouterr().err) == [3]
+    # both band launches (capped, then the whole rhs) hand all three on
+    assert handed_on(capfd.readouterr().err) == [3, 3]
 
 
 def test_label0_strings_go_on(route, capfd):
@@ -84,3 +96,35 @@ def test_label0_strings_go_on(route, capfd):
     seqs = [[1] * 20, [1, 0, 1], [0], [1] * 33]
     got, _ = check(blob, *csr(seqs), LAZY)
     assert got.status[0] == F.FST_PATH_OK and got.status[3] == F.FST_PATH_OK
+
+
+def test_early_exit_beyond_state_cap(route, capfd):
+    # the capped launch keeps back pointers for 2 x window states past the start; a string
+    # whose best final lies further (an epsilon ladder with the only final state far away)
+    # overflows there and is answered by the whole-rhs launch
+    ns = 5000
+    f = O.Fst()
+    for s in range(ns):
+        f.add_state(0.0 if s == ns - 1 else math.inf)
+    f.start = 0
+    for s in range(ns - 1):
+        f.add_arc(s, 0, 0, 0.0, s + 1)
+        f.add_arc(s, 1, 2, float(s % 3), min(ns - 1, s + 2))
+    blob = O.freeze(f)
+    check(blob, *csr([[1] * L for L in (1, 3, 8)]), LAZY)
+    assert handed_on(capfd.readouterr().err) == [3, 0]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_negative_finals_no_early_exit(route, capfd, seed):
+    # a negative final weight breaks the early exit's bound (total >= dist): such an rhs
+    # goes to the hashed replay (weights not all >= +0), which takes no early exit, and the
+    # answers stay the oracle's
+    rng = np.random.default_rng(7300 + seed)
+    f = forward_rhs(rng, int(rng.integers(20, 200)), 4, 3)
+    for s in range(0, f.num_states, 3):
+        f.finals[s] = -float(rng.integers(1, 4))
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 30)))] for _ in range(24)]
+    check(blob, *csr(seqs), LAZY)
+    assert handed_on(capfd.readouterr().err) == []  # not the band

@@ -9,7 +9,9 @@ config 3  compose_frozen_lazy_shortest_path_epsilon_dense (:398-401), its hard c
             epsilon placement and olabels): both semantics on the GPU
             equal their oracle, and differ from each other exactly as the oracle's do;
           - a mixed-length batch, L uniform in [11, 251] (seed 0x5EED), at T=4096;
-          - strings at the full T=65,536 with L in {11, 87}.
+          - strings at the full T=65,536 with L in {11, 87} (live oracle), and 8 strings of
+            the config's lengths up to L=251 against the oracle's fixture
+            (tests/golden/config3_T65536.npz, tests/golden/make_config3_golden.py).
 The oracle runs on the host (threads for the larger batches); the GPU path goes through the
 C ABI (fst_compose_frozen, fst_compose_frozen_shortest_path_batch).
 """
@@ -125,3 +127,23 @@ def test_config3_full_T65536():
     rhs = load_blob(blob)
     got, _ = check_batch(blob, [[1] * 11, [1] * 87, [1] * 11], LAZY, rhs=rhs, threads=3)
     assert np.all(got.status == F.FST_PATH_OK)
+
+
+def test_config3_full_T65536_golden():
+    # config 3's full rhs against strings of its length distribution, L up to 251 (33 M
+    # product tuples in the reference's replay), bit-exact vs the oracle's fixture; the
+    # GPU takes the band replay's exact early exit, the oracle replays
+    # the whole product as the reference does
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "config3_T65536.npz"),
+                allow_pickle=False)
+    rhs = F.Fst.bench_transducer(1, int(z["T"]), int(z["B"]))
+    lens = [int(x) for x in z["lengths"]]
+    labels, offsets = csr([[1] * L for L in lens])
+    got = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, LAZY)
+    assert np.all(z["status"] == 0) and np.all(got.status == F.FST_PATH_OK), got.status
+    assert np.array_equal(got.offsets, z["offsets"])
+    assert np.array_equal(got.ilabels, z["ilabels"])
+    assert np.array_equal(got.olabels, z["olabels"])
+    assert np.array_equal(bits(got.weights), bits(z["weights"]))
+    assert np.array_equal(bits(got.finals), bits(z["finals"]))

@@ -10,6 +10,7 @@ the oracle bit for bit.
 * two processes (gloo for the control plane) share cuda:0, each composes its
   cost-balanced shard (libfst_amd.dist.cost_shard_range) and rank 0 gathers.
 """
+import json
 import os
 import socket
 import subprocess
@@ -213,3 +214,26 @@ dist.destroy_process_group()
     ok = g["status"] == F.FST_PATH_OK   # (strings longer than T have no path: EMPTY)
     assert ok.sum() > 0 and (~ok).sum() > 0
     assert np.array_equal(bits(g["fin"][ok]), bits(ref.finals[ok]))
+
+
+@pytest.mark.parametrize("mode", ["strong", "weak"])
+def test_bench_two_ranks_one_gpu(mode):
+    # bench.py's multi-process path in both scaling modes (the driver's 1/2/4/8-GPU runs
+    # use RCCL, one GPU per rank): two ranks share cuda:0 over gloo here, each times its
+    # shard and checks a sample against the oracle; rank 0 prints the one JSON line
+    repo = os.path.dirname(HERE)
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--backend", "gloo", "--scaling", mode, "--global-batch", "8192", "--batch", "4096",
+           "--no-cpu", "--no-e2e", "--no-varied", "--lazy-batch", "0", "--no-f64"]
+    env = dict(os.environ)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == mode
+    assert line["config"]["global_batch"] == 8192
+    assert line["config"]["strings_per_gpu"] == 4096
+    assert line["checked_vs_oracle"] == 256 and line["value"] > 0
