@@ -770,6 +770,17 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       HIP_TRY(debug_wait(stream, grid_c, "tierC"));
 #endif
     }
+    if (std::getenv("FSTAMD_ROUTE_LOG")) {  // how many strings each fallback tier took
+      unsigned int h[16] = {};
+      HIP_TRY(hipMemcpyAsync(h, counter, sizeof(h), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      std::fprintf(stderr,
+                   "[libfst_amd route] eager: %u strings, tiers P %d A0 %d A %d B %d C %d | "
+                   "handed on: P->A0 %u, A0->A %u, ->B %u, ->C %u\n",
+                   in.num_strings, (int)use_p, (int)use_w, (int)use_a, (int)need_b, (int)need_c,
+                   use_p && use_w ? h[15] : 0u, use_w && use_a ? h[6] : 0u,
+                   need_b && (use_w || use_a) ? h[3] : 0u, need_c ? h[4] : 0u);
+    }
     // Strings the layered tiers cannot take (label-0 inputs -> UNSUPPORTED, tier-2
     // OVERFLOW) go to the general BFS engine.
     HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, false));

@@ -50,14 +50,55 @@ constexpr int kLpChase = 15;  // backtraces batched per wave (<= kChaseBatch: sl
 // DT: the cells' distance storage.  double in general; float when every distance is an
 // integer below 2^24 (integer arc weights with L * max weight < 2^24, checked on the host:
 // DeviceFst::int_wmax), which is exact and saves 2.5 KB, so 4 waves fit per SIMD.
+// The current layer's cells (slot W never holds a tuple) in arrays of 8-B entries addressed
+// by one byte offset o = 8 * slot.  Per cell: the distance d (+inf: no tuple), the id-rank
+// word idw = id rank << 20 (kLpAbsent: no tuple), the pop word pw = pop rank << 20 | run
+// (kLpAbsent: no tuple) and tb = the first toucher's distance (-1: the start).
+template <int W, typename DT>
+struct LazyPullCells {  // f64 distances: d, {idw, pw}, tb
+  double d[W + 1];
+  unsigned long long rp[W + 1];    // lo: idw; hi: pw
+  double tb[W + 1];
+  __device__ __forceinline__ const char* base(const void* a) const { return (const char*)a; }
+  __device__ __forceinline__ double get_d(uint32_t o) const { return *(const double*)(base(d) + o); }
+  __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return *(const uint32_t*)(base(rp) + o); }
+  __device__ __forceinline__ uint32_t get_pw(uint32_t o) const { return *(const uint32_t*)(base(rp) + o + 4); }
+  __device__ __forceinline__ double get_tb(uint32_t o) const { return *(const double*)(base(tb) + o); }
+  __device__ __forceinline__ void set(uint32_t i, double dd, uint32_t idw, uint32_t pw, double t) {
+    d[i] = dd;
+    rp[i] = ((unsigned long long)pw << 32) | idw;
+    tb[i] = t;
+  }
+  __device__ __forceinline__ void set_pop(uint32_t i, uint32_t q) {  // pop rank q
+    uint32_t* w = (uint32_t*)&rp[i] + 1;
+    *w = (*w & kLpRunMask) | (q << 20);
+  }
+};
+// f32 distances (exact: integers below 2^24): {d, idw} and {pw, tb} as two 8-B arrays, so
+// the merge reads one 8-B word per in-arc (as tier P) and the certificate one per source
+template <int W>
+struct LazyPullCells<W, float> {
+  uint2 a[W + 1];                  // {f32 bits of d, idw}
+  uint2 b[W + 1];                  // {pw, f32 bits of tb}
+  __device__ __forceinline__ uint2 get_a(uint32_t o) const { return *(const uint2*)((const char*)a + o); }
+  __device__ __forceinline__ uint2 get_b(uint32_t o) const { return *(const uint2*)((const char*)b + o); }
+  __device__ __forceinline__ float get_d(uint32_t o) const { return __uint_as_float(get_a(o).x); }
+  __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return get_a(o).y; }
+  __device__ __forceinline__ uint32_t get_pw(uint32_t o) const { return get_b(o).x; }
+  __device__ __forceinline__ float get_tb(uint32_t o) const { return __uint_as_float(get_b(o).y); }
+  __device__ __forceinline__ void set(uint32_t i, float dd, uint32_t idw, uint32_t pw, float t) {
+    a[i] = make_uint2(__float_as_uint(dd), idw);
+    b[i] = make_uint2(pw, __float_as_uint(t));
+  }
+  __device__ __forceinline__ void set_pop(uint32_t i, uint32_t q) {
+    b[i].x = (b[i].x & kLpRunMask) | (q << 20);
+  }
+};
+
 template <int W, typename DT>
 struct LazyPullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys p << 3 | j < 8 W
-  // the current layer's cells (slot W never holds a tuple), 8-B arrays addressed by one
-  // byte offset
-  DT d[W + 1];                     // distance (+inf: no tuple)
-  unsigned long long rp[W + 1];    // lo: id rank << 20; hi: pop rank << 20 | run
-  DT tb[W + 1];                    // distance of the first toucher (-1: the start)
+  LazyPullCells<W, DT> c;
   uint32_t ord0[W];                // (key << 9 |) slot in id order
   // P1-P3 and the split sort use {bits, pre, ord1}; the counting sort overlays {mask,
   // hist} on them (bits lies under mask, which the counting sort leaves all zero)
@@ -102,20 +143,13 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
   static_assert(KP <= 16 && W < 512, "key layout as in eager_pull.hpp");
   __shared__ LazyPullLds<W, DT> S;
-  // a cell's distance / first-toucher distance by the 8-B-cell byte offset o of the rp array
-  auto cell_d = [&](uint32_t o) -> DT {
-    return *reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.d) + (F32 ? (o >> 1) : o));
-  };
-  auto cell_tb = [&](uint32_t o) -> DT {
-    return *reinterpret_cast<const DT*>(reinterpret_cast<const char*>(S.tb) + (F32 ? (o >> 1) : o));
-  };
+  auto& CL = S.c;
 #ifdef FSTAMD_LP_PAD  // occupancy experiment only: LDS padding to cut waves per SIMD
   __shared__ uint32_t pad_[FSTAMD_LP_PAD];
   if (threadIdx.x == 1000) pad_[0] = 0;
 #endif
   const uint32_t lane = threadIdx.x;
   const DT kInf = (DT)__builtin_huge_val();
-  const unsigned long long kAbsent2 = ((unsigned long long)kLpAbsent << 32) | kLpAbsent;
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;
 
@@ -166,11 +200,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   const bool want_work = out.work != nullptr;
 
 #pragma unroll 1
-  for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-    S.d[i] = kInf;
-    S.rp[i] = kAbsent2;
-    S.tb[i] = kInf;
-  }
+  for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
   if (lane < (uint32_t)kWords) S.bits[lane] = 0;
   wave_lds_sync();
   uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
@@ -197,17 +227,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
     // layer 0: the start tuple (id 0, pop rank 0, tb -1 < every distance)
 #pragma unroll 1
-    for (uint32_t i = lane; i < wlast; i += 64) {
-      S.d[i] = kInf;
-      S.rp[i] = kAbsent2;
-      S.tb[i] = kInf;
-    }
+    for (uint32_t i = lane; i < wlast; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
     wave_lds_sync();
-    if (lane == 0) {
-      S.d[0] = (DT)w_one();
-      S.rp[0] = 0;
-      S.tb[0] = (DT)-1.0;
-    }
+    if (lane == 0) CL.set(0, (DT)w_one(), 0u, 0u, (DT)-1.0);
     wave_lds_sync();
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
     uint32_t cmin = rhs.start, cmax = rhs.start;
@@ -218,6 +240,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     double myfw = 0.0;
 
     uint32_t labs = 0;
+    // uniform: the current layer's pop ranks equal its id ranks (layer 0; every layer the
+    // sort below finds already in order, or with at most one tuple): the merge's first
+    // toucher is then its smallest candidate key, read from the id-rank words alone
+    bool io = true;
     for (uint32_t k = 0; k < L && fail == kPathOk; ++k) {
       if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
         fail = kPathInternal;
@@ -285,16 +311,24 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         DT nd[KP];
         uint32_t ff = kEmptyKey;
         DT b = kInf;
+        if (io) {  // pop ranks = id ranks: the first toucher is the smallest candidate key
 #pragma unroll
-        for (int m = 0; m < KP; ++m) {
-          const uint32_t o = min(r_src(rr[m]) - tmin8, 8u * W);
-          const DT d = cell_d(o);
-          const unsigned long long rpw =
-              *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
-          nd[m] = d + r_w(rr[m]);  // times(d, w) for finite w >= 0 (:108)
-          bpk[m] = (uint32_t)rpw | rr[m].y | o;
-          ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | rr[m].y | o);
-          b = fmin(b, nd[m]);
+          for (int m = 0; m < KP; ++m) {
+            const uint32_t o = min(r_src(rr[m]) - tmin8, 8u * W);
+            nd[m] = CL.get_d(o) + r_w(rr[m]);  // times(d, w) for finite w >= 0 (:108)
+            bpk[m] = CL.get_idw(o) | rr[m].y | o;
+            ff = min(ff, bpk[m]);
+            b = fmin(b, nd[m]);
+          }
+        } else {
+#pragma unroll
+          for (int m = 0; m < KP; ++m) {
+            const uint32_t o = min(r_src(rr[m]) - tmin8, 8u * W);
+            nd[m] = CL.get_d(o) + r_w(rr[m]);
+            bpk[m] = CL.get_idw(o) | rr[m].y | o;
+            ff = min(ff, (CL.get_pw(o) & kLpAbsent) | rr[m].y | o);
+            b = fmin(b, nd[m]);
+          }
         }
         if (want_work) {  // (one uniform branch per row; an absent source's key >= kLpAbsent)
 #pragma unroll
@@ -312,36 +346,30 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             for (int m = 0; m < KP; ++m) {
               const RT r2 = rec(rxx + m);
               const uint32_t o = min(r_src(r2) - tmin8, 8u * W);
-              const DT d = cell_d(o);
-              const unsigned long long rpw =
-                  *reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o);
-              const DT n2 = d + r_w(r2);
-              const uint32_t p2 = (uint32_t)rpw | r2.y | o;
-              ff = min(ff, ((uint32_t)(rpw >> 32) & kLpAbsent) | r2.y | o);
+              const DT n2 = CL.get_d(o) + r_w(r2);
+              const uint32_t iw = CL.get_idw(o);
+              const uint32_t p2 = iw | r2.y | o;
+              ff = min(ff, (CL.get_pw(o) & kLpAbsent) | r2.y | o);
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
                 c = p2;
                 ra = rxx + m;
               }
-              if (want_work) relax += (uint32_t)__popcll(__ballot((uint32_t)rpw < kLpAbsent));
+              if (want_work) relax += (uint32_t)__popcll(__ballot(iw < kLpAbsent));
             }
           }
         }
         const bool pres = ff < kLpAbsent;
         // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
         const uint32_t ou = pres ? (ff & 0xFFFu) : 8u * W;
-        const DT du = cell_d(ou);
-        const DT tbu = cell_tb(ou);
-        const uint32_t ruu =
-            (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ou) >> 32) &
-            kLpRunMask;
+        const DT du = CL.get_d(ou);
+        const DT tbu = CL.get_tb(ou);
+        const uint32_t ruu = CL.get_pw(ou) & kLpRunMask;
         // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
         // round trip: its certificate alone usually settles C
         const uint32_t ob = pres ? (c & 0xFFFu) : 8u * W;
-        const DT tbb = cell_tb(ob);
-        const uint32_t rbb =
-            (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + ob) >> 32) &
-            kLpRunMask;
+        const DT tbb = CL.get_tb(ob);
+        const uint32_t rbb = CL.get_pw(ob) & kLpRunMask;
         const DT tx = du;
         const uint32_t rx = 1u + (tbu == tx ? ruu : 0u);
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
@@ -365,10 +393,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
             const uint32_t o = bpk[m] & 0xFFFu;
-            const DT tbm = cell_tb(o);
-            const uint32_t rm =
-                (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
-                kLpRunMask;
+            const DT tbm = CL.get_tb(o);
+            const uint32_t rm = CL.get_pw(o) & kLpRunMask;
             cert |= nd[m] == b && ((bpk[m] & kRevPos) || tbm < tx || (tbm == tx && rm < rx));
           }
           if (hubs) {  // the further blocks' tight in-arcs
@@ -379,11 +405,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               for (int m = 0; m < KP; ++m) {
                 const RT r2 = rec(rxx + m);
                 const uint32_t o = min(r_src(r2) - tmin8, 8u * W);
-                const DT d = cell_d(o);
-                const DT tbm = cell_tb(o);
-                const uint32_t rm =
-                    (uint32_t)(*reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(S.rp) + o) >> 32) &
-                    kLpRunMask;
+                const DT d = CL.get_d(o);
+                const DT tbm = CL.get_tb(o);
+                const uint32_t rm = CL.get_pw(o) & kLpRunMask;
                 cert |= d + r_w(r2) == b &&
                         (r_w(r2) > (DT)0 || tbm < tx || (tbm == tx && rm < rx));
               }
@@ -444,10 +468,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
-        S.d[i] = pres ? bd[e] : kInf;
-        S.tb[i] = pres ? tbx[e] : kInf;
         // pop rank: identity until the sort below fills it in
-        S.rp[i] = pres ? ((unsigned long long)((rank << 20) | runx[e]) << 32) | (rank << 20) : kAbsent2;
+        CL.set(i, pres ? bd[e] : kInf, pres ? rank << 20 : kLpAbsent,
+               pres ? (rank << 20) | runx[e] : kLpAbsent, pres ? tbx[e] : kInf);
         if (pres && sort) S.ord0[rank] = i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
@@ -491,7 +514,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         for (int e = 0; e < EW; ++e) {
           if ((uint32_t)e >= rows_s) continue;  // uniform
           const uint32_t q = (uint32_t)e * 64 + lane;
-          if (q + 1 < n_next) unsorted |= S.d[S.ord0[q]] > S.d[S.ord0[q + 1]];
+          if (q + 1 < n_next) unsorted |= CL.get_d(8 * S.ord0[q]) > CL.get_d(8 * S.ord0[q + 1]);
         }
         const bool in_order = !__ballot(unsorted);
         if (!in_order) {
@@ -509,7 +532,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const uint32_t q = (uint32_t)e * 64 + lane;
           if (q < n_next) {
             cs[e] = S.ord0[q];
-            cd[e] = S.d[cs[e]];
+            cd[e] = CL.get_d(8 * cs[e]);
             mn = fmin(mn, cd[e]);
             mx = fmax(mx, cd[e]);
             if (!F32) nonint |= cd[e] != __builtin_trunc(cd[e]);
@@ -601,9 +624,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             if ((uint32_t)e >= rows_s) continue;
             if ((uint32_t)e * 64 + lane < n_next) {
               const uint32_t q = S.hist[ck[e] >> 9] + cw[e];
-              const uint32_t sl = ck[e] & 511u;
-              const unsigned long long rpw = S.rp[sl];
-              S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
+              CL.set_pop(ck[e] & 511u, q);
             }
           }
           wave_lds_sync();
@@ -630,7 +651,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               v[e] = (el[e] >> bit) & 1u;
             } else {
               const unsigned long long key =
-                  (unsigned long long)__double_as_longlong((double)S.d[el[e] & 511u]);
+                  (unsigned long long)__double_as_longlong((double)CL.get_d(8 * (el[e] & 511u)));
               v[e] = (uint32_t)(key >> bit) & 1u;
             }
             z[e] = __ballot(valid && !v[e]);
@@ -656,12 +677,13 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           wave_lds_sync();
         }
         for (uint32_t q = lane; q < n_next && !counting; q += 64) {  // pop rank q -> cell
-          const uint32_t sl = (cur ? S.ord1 : S.ord0)[q] & 511u;
-          const unsigned long long rpw = S.rp[sl];
-          S.rp[sl] = (rpw & ~(0xFFF00000ull << 32)) | ((unsigned long long)(q << 20) << 32);
+          CL.set_pop((cur ? S.ord1 : S.ord0)[q] & 511u, q);
         }
         wave_lds_sync();
         }  // !in_order
+        io = in_order;
+      } else {
+        io = true;  // at most one tuple (or the last layer): identity pop ranks
       }
       tmin = tn;
       base = nbase;
@@ -677,11 +699,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // leave every cell empty for the next string (a failed string may stop mid-layer)
       wave_lds_sync();
 #pragma unroll 1
-      for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) {
-        S.d[i] = kInf;
-        S.rp[i] = kAbsent2;
-        S.tb[i] = kInf;
-      }
+      for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
       if (lane < (uint32_t)kWords) S.bits[lane] = 0;
       wave_lds_sync();
       wlast = 0;
