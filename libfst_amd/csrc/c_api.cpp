@@ -1222,6 +1222,12 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
   };
   std::shared_ptr<MutableFst> a;
   std::shared_ptr<FrozenFst> b;
+  // a compileString acceptor is snapshotted as its labels alone (the chain route below
+  // needs nothing else); any other lhs as a deep copy
+  std::vector<uint32_t> chain;
+  bool is_chain = false;
+  size_t a_states = 0, a_arcs = 0;
+  bool a_start = false;
   {
     std::shared_lock<std::shared_mutex> g(g_api_mu);
     auto ha = g_mut.get(a_handle);
@@ -1229,27 +1235,30 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
       trace("sp_invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
       return kInvalid;
     }
-    a = std::make_shared<MutableFst>(*ha);  // snapshot (c-api.zig:754)
+    is_chain = as_chain(*ha, &chain);
+    if (!is_chain) a = std::make_shared<MutableFst>(*ha);  // snapshot (c-api.zig:754)
+    a_states = ha->num_states();
+    a_arcs = is_chain ? chain.size() : ha->total_arcs();
+    a_start = ha->start() != kNoState;
     b = g_fst.get(b_handle);                // pin (c-api.zig:759)
     if (!b) {
-      trace("sp_invalid_b", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(), 0);
+      trace("sp_invalid_b", a_handle, b_handle, a_states, a_arcs, 0, 0, us(), 0);
       return kInvalid;
     }
   }
   MutableFst result;
   // compose-shortest-path.zig:30-33: empty checks first, then n.
-  if (a->start() == kNoState || b->start() == kNoState || n == 0) {
+  if (!a_start || b->start() == kNoState || n == 0) {
     // empty result
   } else if (n != 1) {
-    trace("sp_compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(), 0);
+    trace("sp_compose_error", a_handle, b_handle, a_states, a_arcs, 0, 0, us(), 0);
     return kInvalid;
   } else {
     if (!gpu_available()) return kInvalid;
     double kms = 0;
     int rc = -1;
-    std::vector<uint32_t> chain;
-    if (as_chain(*a, &chain)) {  // the batch engines on one string, coalesced with the
-                                 // chain calls of other threads (ChainCombiner)
+    if (is_chain) {  // the batch engines on one string, coalesced with the chain calls of
+                     // other threads (ChainCombiner)
       ChainCall c;
       c.rhs = b;
       c.n = n;
@@ -1273,14 +1282,16 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
       }
     }
     // anything else (a general lhs; a string the batch engines handed back): one general lhs
-    if (rc < 0) rc = run_lazy_single(*a, *b, n, &result, &kms);
+    if (rc < 0) {
+      if (!a) a = std::make_shared<MutableFst>(MutableFst::compile_chain(chain));
+      rc = run_lazy_single(*a, *b, n, &result, &kms);
+    }
     if (rc != 0) {
-      trace("sp_compose_error", a_handle, b_handle, a->num_states(), a->total_arcs(), 0, 0, us(),
-            kms);
+      trace("sp_compose_error", a_handle, b_handle, a_states, a_arcs, 0, 0, us(), kms);
       return kInvalid;
     }
   }
-  trace("sp_ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
+  trace("sp_ok", a_handle, b_handle, a_states, a_arcs, result.num_states(),
         result.total_arcs(), us(), t_last_stats.kernel_ms);
   std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));

@@ -1361,6 +1361,7 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     while (w < want) w <<= 1;
     if (wse) w = std::max<uint32_t>(64, 1u << (31 - __builtin_clz((uint32_t)std::max(1, std::atoi(wse)))));
     p.wstates = w;
+    if ((uint64_t)w * (p.lcap + 1) >= (1ull << 26)) return false;  // the kernel's div_lc range
     p.wn = (uint64_t)w * (p.lcap + 1) * 2;
     p.scap = capped ? std::min<uint32_t>(srange, 2 * w) : srange;
     p.tn = (uint64_t)(p.lcap + 1) * p.scap * 2;  // ids and tuple indices fit 31 bits

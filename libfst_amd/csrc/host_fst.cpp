@@ -189,6 +189,16 @@ MutableFst MutableFst::compile_string(const uint8_t* in, uint32_t in_len, const 
   return f;
 }
 
+MutableFst MutableFst::compile_chain(const std::vector<Label>& labels) {
+  MutableFst f;
+  const uint32_t L = (uint32_t)labels.size();
+  f.add_states((size_t)L + 1);
+  f.set_start(0);
+  f.set_final(L, w_one());
+  for (uint32_t i = 0; i < L; ++i) f.add_arc(i, Arc{labels[i], labels[i], w_one(), i + 1});
+  return f;
+}
+
 bool MutableFst::print_string(bool output_tape, std::vector<uint8_t>* bytes) const {
   StateId cur = start_;
   if (cur == kNoState) return false;

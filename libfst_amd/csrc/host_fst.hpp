@@ -48,6 +48,9 @@ class MutableFst {
   // compileString / compileStringTransducer, src/string.zig:17-50
   static MutableFst compile_string(const uint8_t* in, uint32_t in_len, const uint8_t* out,
                                    uint32_t out_len);
+  // The acceptor of a label chain (what c_api.cpp's as_chain recognises): states 0..L,
+  // arc k = (c, c, One, k + 1), final(L) = One.
+  static MutableFst compile_chain(const std::vector<Label>& labels);
   // printStringFromTape, src/string.zig:64-97.  Returns false for "null".
   bool print_string(bool output_tape, std::vector<uint8_t>* bytes) const;
   // readText, src/io/text.zig:20-115 (OpenFst AT&T text: "src dest il [ol] [w]" arcs,

@@ -34,8 +34,10 @@
 // slots outside the current layer's window (and the null block's padding records) are
 // clamped to slot W, which never holds a tuple.
 //
-// The back record of a tuple is {reverse record of its back arc, slab position of its
-// source}: the batched backtrace walks one dependent 8-B load per arc.
+// The back record of a tuple is the reverse record of its back arc (4 B); the record's
+// source state and the source layer's {slab base, window origin} (one 8-B entry per layer)
+// give the source's slab position: the batched backtrace walks two dependent loads per arc
+// (back record, then the reverse record it reads anyway for the olabel and weight).
 #pragma once
 
 #include <type_traits>
@@ -187,22 +189,31 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       maxL = jb.L;
     }
     maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
-    const uint2* sl = slabs + (size_t)lane * lp.back_cap;
+    // slab: 4-B back records (the reverse record of each tuple's back arc) in its first
+    // half, per layer k {slab base, window origin} of layer k in its second half: the
+    // record's source state gives the source's slab position
+    const uint32_t* sl = reinterpret_cast<const uint32_t*>(slabs + (size_t)lane * lp.back_cap);
+    const uint2* hdr = slabs + (size_t)lane * lp.back_cap + lp.back_cap / 2;
     uint32_t id = jb.id;
     for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
-        const uint2 b = sl[FB(id, lp.back_cap, 60)];
+        const uint32_t b = sl[FB(id, lp.back_cap, 60)];
+        const uint2 h = hdr[k];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
+        uint32_t src8;
         if constexpr (F32) {
-          const uint4 r = rv.rrec32[b.x];
+          const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
           out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
+          src8 = r.x;
         } else {
-          out.out_ol[jb.o + k] = rv.rolab[b.x];
-          out.out_w[jb.o + k] = rv.rrec[b.x].weight;  // times(One, w) == w for w >= +0
+          const RevRec r = rv.rrec[b];
+          out.out_ol[jb.o + k] = rv.rolab[b];
+          out.out_w[jb.o + k] = r.weight;  // times(One, w) == w for w >= +0
+          src8 = r.src;
         }
-        id = b.y;
+        id = h.x + ((src8 >> 3) - h.y);
       }
     }
     if (lane < njobs) {
@@ -234,7 +245,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     item = __builtin_amdgcn_readfirstlane(item);
     if (item >= num_items) break;
     const uint32_t si = __builtin_amdgcn_readfirstlane(lp.items ? lp.items[item] : item);
-    uint2* const back = slabs + (size_t)njobs * lp.back_cap;
+    uint32_t* const back = reinterpret_cast<uint32_t*>(slabs + (size_t)njobs * lp.back_cap);
+    uint2* const hdr = slabs + (size_t)njobs * lp.back_cap + lp.back_cap / 2;
     const uint64_t off0 = in.offsets[si];
     const uint64_t off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off0 >> 32)) << 32) |
                          __builtin_amdgcn_readfirstlane((uint32_t)off0);
@@ -395,6 +407,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // ---- (P3) the next layer's cells (rewriting every row the current one used), back
       // records, and on the last layer the final candidates ----
       const bool last = k + 1 == L;
+      if (lane == 0) hdr[k] = make_uint2(base, tmin);  // layer k: where its sources sit
       const uint32_t rows_w = max(rows_n, (wk + 63) / 64);
       uint32_t lo_slot = kEmptyKey, hi_slot = 0;  // uniform: present slots of the next layer
 #pragma unroll
@@ -416,7 +429,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          back[FB(nbase + i, lp.back_cap, 61)] = make_uint2(bra[e], base + ((bk[e] & 0xFFFu) >> 3));
+          back[FB(nbase + i, lp.back_cap, 61)] = bra[e];
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];

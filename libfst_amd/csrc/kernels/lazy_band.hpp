@@ -104,6 +104,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   const uint32_t S0 = rhs.start;  // every reachable state is >= S0 (arcs go forward)
   const uint32_t SCAP = ws.scap;
   auto wix = [&](uint32_t k_, uint32_t s_) { return (s_ & wmask) * LC + k_; };  // x 2 + f
+  // v / LC for window indices v < 2^26 (the host plan checks WS * LC < 2^26): one 64-bit
+  // multiply instead of a ~35-instruction integer division, exact since 2^38 >= v * LC
+  const uint64_t mlc = ((1ull << 38) + LC - 1) / LC;
+  auto div_lc = [&](uint32_t v_) -> uint32_t { return (uint32_t)(((uint64_t)v_ * mlc) >> 38); };
   auto gix = [&](uint32_t k_, uint32_t s_) { return (s_ - S0) * LC + k_; };     // x 2 + f
   // back pointers: f_src | ds << 1 | local arc << (1 + dbits)
   uint8_t* bk8 = (uint8_t*)bkv;
@@ -323,7 +327,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     const uint32_t pid = uni(cur_base + (uint32_t)__ffsll((long long)cur_bits) - 1);
     cur_bits = uni64(cur_bits & (cur_bits - 1));
     const uint32_t x = uni(pid + kLbRing >= nn ? S.ring[pid & (kLbRing - 1)] : idr[pid & rmask]);
-    const uint32_t sslot = (x >> 1) / LC;
+    const uint32_t sslot = div_lc(x >> 1);
     const uint32_t k = (x >> 1) - sslot * LC;
     const uint32_t s = slo + ((sslot - slo) & wmask);
 #ifdef FSTAMD_BAND_DEBUG
@@ -439,7 +443,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       // (every ~Ws - L states), so the open set is walked rather than counted per pop.
       uint32_t smin = s;
       {
-        auto state_of = [&](uint32_t xw) { return slo + (((xw >> 1) / LC - slo) & wmask); };
+        auto state_of = [&](uint32_t xw) { return slo + ((div_lc(xw >> 1) - slo) & wmask); };
         const uint32_t lo = max(lowp, nn > LS ? nn - LS : 0u);
         for (uint32_t b0 = lo & ~63u; b0 < nn; b0 += 64 * 64) {
           const uint32_t id0 = b0 + lane * 64;
@@ -478,7 +482,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       // clear the leaving states' records (every tuple there is final)
       const uint32_t nclear = (smin - slo) * LC * 2;
       for (uint32_t i = lane; i < nclear; i += 64) {
-        const uint32_t st = slo + i / (LC * 2);
+        const uint32_t st = slo + div_lc(i >> 1);
         const uint32_t r = i - (st - slo) * (LC * 2);
         Rw[4 * (size_t)(2 * ((st & wmask) * LC) + r) + 2] = kLdUntouched;
       }
@@ -529,7 +533,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const bool act = lane < cnt_c;
       const uint32_t tx = act ? S.x[lane] : 0u;
       // the target's tuple index (its state from the window slot: targets lie in the window)
-      const uint32_t tslot = (tx >> 1) / LC;
+      const uint32_t tslot = div_lc(tx >> 1);
       const uint32_t tstate = slo + ((tslot - slo) & wmask);
       const uint32_t tg = 2 * gix((tx >> 1) - tslot * LC, tstate) + (tx & 1);
       const double nd = act ? w_times(dcur, S.w[lane]) : 0.0;

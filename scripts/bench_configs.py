@@ -5,9 +5,8 @@ strings, is bench.py's).  One JSON line per config; CPU time of the oracle resta
   1  compose_frozen_epsilon_dense: one 1^96 string vs eps-dense T=4096 B=12, eager
      compose only (fst_compose_frozen, the whole lattice)
   2  compose_frozen_shortest_path_ambiguous: 64K 1^64 strings, eager and lazy
-  3  compose_frozen_lazy_shortest_path_epsilon_dense: lazy, mixed lengths L 11..251, at
-     T=1,024 here (4,096 strings); the full config (T=65,536, ~17M tuples per string) is
-     measured on 512 strings by scripts/config3_scaling.py
+  3  compose_frozen_lazy_shortest_path_epsilon_dense: lazy, mixed lengths L 11..251, the
+     full rhs T=65,536, 65,536 strings ("3m": the config's 1M)
   4  two-stage tagger -> verbalizer (synthetic stand-ins, libfst_amd/synthetic.py)
   4w the same on the WeText-scale stand-in (libfst_amd/wetext_standin.py)
   5  LogWeight ambiguous chain, 256K strings, lengths 1..64, 10 % dead strings
@@ -116,22 +115,40 @@ def config2(n=65536, L=64):
     return out
 
 
-def config3(T=1024, n=4096):
+def config3(T=65536, n=65536, ncpu=8):
+    """Config 3 at its full rhs (T=65,536), n strings of its length distribution (1M in the
+    config; 65,536 by default, "3m" runs the 1M), lazy.  The first `ncpu` strings are also
+    run by the CPU port on ncpu host threads, timed, and bit-compared with the GPU's."""
     fz = F.Fst.bench_transducer(F.BENCH_EPS_DENSE, T, 12)
     rhs, blob = dev_rhs(fz)
     rng = np.random.default_rng(0x5EED)
     lens = rng.integers(11, 252, n)
     b = bench.DeviceBatch(lens, lambda t: torch.ones(t, dtype=torch.int32), "cuda:0",
-                              arc_factor=4)
+                          arc_factor=4)
     wall, kms = timed_device(b, rhs, F.FST_SEM_LAZY, steps=1)
     st = b.status.cpu().numpy()
-    labels = np.ones(int(lens[:8].sum()), np.uint32)
-    offs = np.concatenate([[0], np.cumsum(lens[:8])]).astype(np.uint64)
-    cr, take = cpu_rate(blob, labels, offs, 0, budget_s=8.0)
-    return {"config": 3, "workload": f"compose_frozen_lazy_shortest_path_epsilon_dense T={T} (full config: T=65536), {n} strings, L uniform 11..251",
-            "strings_per_s": n / wall, "kernel_ms": kms, "ok": int((st == 0).sum()),
-            "overflow": int((st == 4).sum()), "cpu_oracle_strings_per_s": cr, "cpu_sample": take,
-            "cpu_kind": "port, 1 thread"}
+    labels = np.ones(int(lens[:ncpu].sum()), np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:ncpu])]).astype(np.uint64)
+    t0 = time.perf_counter()
+    ref = O.batch_run(blob, labels, offs, 0, 1, ncpu)
+    secs = time.perf_counter() - t0
+    checked = bench.compare_with_ref(b, ref, ncpu)
+    # the work the reference's replay does (its whole product) vs the GPU's (early exit)
+    b.run(rhs, F.FST_SEM_LAZY, 0, torch.cuda.current_stream().cuda_stream, work=True)
+    torch.cuda.synchronize()
+    work = b.work.cpu().numpy().astype(np.int64)
+    return {"config": 3, "workload": f"compose_frozen_lazy_shortest_path_epsilon_dense T={T} B=12, {n} strings, L uniform 11..251 (seed 0x5EED), lazy",
+            "strings_per_s": n / wall, "wall_s": wall, "kernel_ms": kms, "ok": int((st == 0).sum()),
+            "overflow": int((st == 4).sum()), "bit_exact_vs_oracle": checked,
+            "gpu_tuples_per_string": float(work[0::2].mean()),
+            "gpu_relax_per_string": float(work[1::2].mean()),
+            "oracle_tuples_per_string_sample": float(ref.tuples.mean()),
+            "cpu_oracle_strings_per_s": ncpu / secs, "cpu_sample": ncpu,
+            "cpu_kind": f"port, {ncpu} threads (first {ncpu} strings, each bit-compared)"}
+
+
+def config3m():
+    return config3(n=1 << 20)
 
 
 def cpu_pipeline_rate(blobs, labels, offsets, sem, threads=16):
@@ -294,8 +311,19 @@ def main():
     ap.add_argument("--configs", default="1,2,3,4,5")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
+    t_start = time.perf_counter()
+
+    def heartbeat():  # long configs (3m) print nothing for minutes: gpurun needs a sign
+        while True:
+            time.sleep(30)
+            print(f"# still running, {time.perf_counter() - t_start:.0f} s", file=sys.stderr,
+                  flush=True)
+
+    import threading
+    threading.Thread(target=heartbeat, daemon=True).start()
     torch.cuda.set_device(0)
-    fns = {"1": config1, "2": config2, "3": config3, "4": config4, "4w": config4w, "2p": config2p, "5": config5}
+    fns = {"1": config1, "2": config2, "3": config3, "3m": config3m, "4": config4, "4w": config4w,
+           "2p": config2p, "5": config5}
     lines = []
     for c in args.configs.split(","):
         r = fns[c]()
