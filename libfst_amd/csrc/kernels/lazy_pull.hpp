@@ -268,7 +268,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       const uint32_t tn = cmin >= rhs.jump_back ? cmin - rhs.jump_back : 0u;
       const uint64_t hi = min((uint64_t)cmax + rhs.jump_fwd, (uint64_t)rhs.num_states - 1);
       const uint32_t nbase = base + wk;
-      if (hi - tn >= (uint64_t)W || (uint64_t)nbase + (hi - tn + 1) > lp.back_cap) {
+      // (the slab's second half holds one header entry per layer: k < back_cap / 2)
+      if (hi - tn >= (uint64_t)W || (uint64_t)nbase + (hi - tn + 1) > lp.back_cap ||
+          k >= lp.back_cap / 2) {
         fail = kPathOverflow;
         break;
       }

@@ -146,9 +146,15 @@ def lazy_via_rounds(lhs: O.Fst, blob: bytes):
 # above dcur, scanned when the bitmap empties (dcur advances to the smallest valid
 # entry; every valid entry at that distance moves into the bitmap).
 # ---------------------------------------------------------------------------------
-def lazy_via_buckets(labels, rhs: O.Fst, stats=None):
+def lazy_via_buckets(labels, rhs: O.Fst, stats=None, early=False):
     """composeShortestPath(chain(labels), frozen(rhs), 1) for finite weights >= 0 and
-    labels != 0.  Returns the oracle_ffi.chain tuple, None (empty) or "cycle"."""
+    labels != 0.  Returns the oracle_ffi.chain tuple, None (empty) or "cycle".
+
+    early: the band replay's exact early exit (kernels/lazy_band.hpp, DESIGN.md §4.2c;
+    taken only when every final weight is >= 0 or Zero): stop before a pop at distance D
+    once the best total is finite and either D > best total, or D == best total and every
+    tuple with an id <= emax is settled, emax = the largest id on the best tuple's back
+    chain (walked when the next pop passes the last emax)."""
     L = len(labels)
     NS = rhs.num_states
     if rhs.start == O.NO_STATE:
@@ -176,6 +182,20 @@ def lazy_via_buckets(labels, rhs: O.Fst, stats=None):
     dcur = 0.0
     bucket.add(0)
     best = None                       # (total, id, fw)
+    early = early and all(x >= 0 or math.isinf(x) for x in rhs.finals)
+    emax = 0
+    st["early_exit"] = False
+
+    def chain_max(b_id):
+        m, cur = b_id, b_id
+        for _ in range(len(idx_of) + 1):
+            if cur == 0:
+                break
+            back = rec[idx_of[cur]][3]
+            cur = back[0]
+            m = max(m, cur)
+        return m
+
     while True:
         if not bucket:               # advance: scan + compact the future list
             st["advances"] += 1
@@ -184,12 +204,24 @@ def lazy_via_buckets(labels, rhs: O.Fst, stats=None):
             if not live:
                 break
             dcur = min(d for d, _ in live)
+            if early and best is not None and not math.isinf(best[0]) and dcur > best[0]:
+                st["early_exit"] = True
+                break
             future = [(d, t) for (d, t) in live if d != dcur]
             for d, t in live:
                 if d == dcur:
                     bucket.add(rec[t][1])
         st["bucket_max"] = max(st["bucket_max"], len(bucket))
         pid = min(bucket)
+        if (early and best is not None and not math.isinf(best[0]) and dcur == best[0]
+                and pid > emax):
+            live_ids = [rec[t][1] for (d, t) in future if not rec[t][2] and rec[t][0] == d]
+            if not live_ids or min(live_ids) > emax:
+                m = chain_max(best[1])
+                if m <= emax:
+                    st["early_exit"] = True
+                    break
+                emax = m
         bucket.discard(pid)
         st["pops"] += 1
         if stats is not None and "order" in stats:
@@ -205,6 +237,7 @@ def lazy_via_buckets(labels, rhs: O.Fst, stats=None):
             total = dcur + (fw1 + fw2)
             if best is None or total < best[0] or (total == best[0] and pid < best[1]):
                 best = (total, pid, fw1 + fw2)
+                emax = max(emax, pid)
         cands = []                    # (target, il, ol, w) in the reference's phase order
         if k < L:
             cands += [((k + 1, a[3], 0), a[0], a[1], 0.0 + a[2])

@@ -79,3 +79,45 @@ def test_bucket_model_bench_shapes(name, T, L):
     o = st["order"]
     leaf_changes = sum(1 for a, b in zip(o, o[1:]) if a // 64 != b // 64)
     assert leaf_changes <= len(o) // 8
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_early_exit_model_random(block):
+    """The band replay's early exit on the bucket model: same answers as
+    the oracle's whole replay on random tie-heavy epsilon rhs (finals >= 0; any arc
+    direction: the argument does not need forward arcs), with fewer pops on most."""
+    saved = 0
+    for seed in range(block * 300, block * 300 + 300):
+        rng = np.random.default_rng(7700 + seed)
+        rhs = random_rhs(rng, int(rng.integers(1, 20)), int(rng.integers(1, 80)), 3, eps=True,
+                         wmax=2, frac=seed % 3 == 0)
+        labels = [int(x) for x in rng.integers(1, 4, size=int(rng.integers(0, 10)))]
+        blob = O.freeze(rhs)
+        full, early = {}, {}
+        want = oracle_lazy(chain_of(labels), blob)
+        assert M.lazy_via_buckets(labels, rhs, full) == want, seed
+        assert M.lazy_via_buckets(labels, rhs, early, early=True) == want, seed
+        assert early["pops"] <= full["pops"]
+        saved += full["pops"] - early["pops"]
+    assert saved > 0
+
+
+def test_early_exit_model_negative_finals_not_taken():
+    rng = np.random.default_rng(7799)
+    rhs = random_rhs(rng, 12, 50, 3, eps=True, wmax=2)
+    rhs.finals = [-1.0 if not np.isinf(x) else x for x in rhs.finals]
+    st = {}
+    labels = [1, 2, 3, 1]
+    assert M.lazy_via_buckets(labels, rhs, st, early=True) == \
+        oracle_lazy(chain_of(labels), O.freeze(rhs))
+    assert not st["early_exit"]
+
+
+@pytest.mark.parametrize("T,L", [(512, 24), (2048, 40)])
+def test_early_exit_model_eps_dense(T, L):
+    # config 3's shape: the exit comes after ~2 L^2 pops whatever T is
+    rhs = O.gen("eps_dense", T, 12)
+    st = {}
+    got = M.lazy_via_buckets([1] * L, rhs, st, early=True)
+    assert got == oracle_lazy(chain_of([1] * L), O.freeze(rhs))
+    assert st["early_exit"] and st["pops"] < 3 * L * L
