@@ -682,6 +682,123 @@ FstError shard_download(Shard& S, FstBatchResult* out, uint64_t arc_base) {
   return FST_OK;
 }
 
+// Gives the calling thread its current HIP device back when it goes out of scope.
+struct DeviceRestore_ {
+  int dev = -1;
+  DeviceRestore_() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DeviceRestore_() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
+// The same copies without the synchronisation or the offset fix-up, on `stream` (the
+// pipelined host batch: the caller synchronises once at the end).
+bool shard_download_async(Shard& S, FstBatchResult* out, uint64_t arc_base, hipStream_t stream) {
+  const uint32_t num = S.s1 - S.s0;
+  const auto d2h = [stream](void* dst, const void* src, size_t b) {
+    return b == 0 || hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, stream) == hipSuccess;
+  };
+  return d2h(out->status + S.s0, S.st->p, num * 4ull) &&
+         d2h(out->final_weights + S.s0, S.fin->p, num * 8ull) &&
+         d2h(out->path_offsets + S.s0, S.off->p, num * 8ull) &&
+         d2h(out->ilabels + arc_base, S.il->p, S.tot * 4) &&
+         d2h(out->olabels + arc_base, S.ol->p, S.tot * 4) &&
+         d2h(out->weights + arc_base, S.w->p, S.tot * 8);
+}
+
+// One device, one large batch on an rhs without input epsilons (a path has exactly L arcs,
+// so the result is allocated before any shard finishes): the strings run as consecutive
+// sub-shards on one engine, and the download of sub-shard j (a second stream, waiting for
+// j's compaction only) runs while sub-shard j + 1 computes -- round 3's host batch ran its
+// ~1 GB D2H after all the kernels.  Results are identical to the one-shard path.
+FstError run_pipelined(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
+                       uint32_t num, uint32_t n, int semantics, uint32_t parts,
+                       FstBatchResult* out) {
+  if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  DeviceFst* D = b.device(dev);
+  if (!D) return FST_OOM;
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return FST_INVALID_ARG;
+  const hipStream_t stream = E.stream();
+  struct CopyStream {  // the downloads' stream and the compaction events it waits for
+    hipStream_t s = nullptr;
+    std::vector<hipEvent_t> ev;
+    ~CopyStream() {
+      if (s) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+      }
+      for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+  } C;
+  if (hipStreamCreateWithFlags(&C.s, hipStreamNonBlocking) != hipSuccess) return FST_OOM;
+  const uint64_t total = offsets[num] - offsets[0];
+  std::vector<uint64_t> rebased(num + 1);
+  for (uint32_t i = 0; i <= num; ++i) rebased[i] = offsets[i] - offsets[0];
+  DevBuf d_lab(total * 4), d_off((num + 1) * 8ull);
+  if (!d_lab.p || !d_off.p) return FST_OOM;
+  if (total && hipMemcpyAsync(d_lab.p, labels + offsets[0], total * 4, hipMemcpyHostToDevice,
+                              stream) != hipSuccess)
+    return FST_OOM;
+  if (hipMemcpyAsync(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice, stream) !=
+      hipSuccess)
+    return FST_OOM;
+  if (t_prof) t_prof->lap(0);
+  if (!alloc_result(out, num, total)) return FST_OOM;  // paths of L arcs: <= total arcs
+  std::vector<Shard> sh(parts);
+  uint64_t base = 0;
+  for (uint32_t j = 0; j < parts; ++j) {
+    Shard& S = sh[j];
+    S.dev = dev;
+    S.s0 = (uint32_t)((uint64_t)num * j / parts);
+    S.s1 = (uint32_t)((uint64_t)num * (j + 1) / parts);
+    uint32_t ml = 0;
+    for (uint32_t i = S.s0; i < S.s1; ++i) ml = std::max<uint32_t>(ml, (uint32_t)(rebased[i + 1] - rebased[i]));
+    // the sub-shard reads the whole upload: its offsets index the one label array
+    ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p + S.s0, S.s1 - S.s0, ml};
+    HostPaths h;
+    if (FstError e = run_chain_batch_dev(E, *D, in, rebased[S.s1] - rebased[S.s0], n, semantics,
+                                         &h, &S.keep);
+        e != FST_OK)
+      return e;
+    S.stats = t_last_stats;
+    S.E = std::move(E);  // shard_compact runs on the lease's stream
+    const FstError ce = shard_compact(S);
+    E = std::move(S.E);
+    if (ce != FST_OK) return ce;
+    if (base + S.tot > total) return FST_OOM;  // (a path longer than its string: impossible)
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return FST_OOM;
+    C.ev.push_back(ev);
+    if (hipEventRecord(ev, stream) != hipSuccess || hipStreamWaitEvent(C.s, ev, 0) != hipSuccess ||
+        !shard_download_async(S, out, base, C.s))
+      return FST_OOM;
+    S.keep.reset();  // (the path arena: compaction copied what the download needs)
+    base += S.tot;
+  }
+  if (hipStreamSynchronize(C.s) != hipSuccess) return FST_OOM;
+  if (t_prof) t_prof->lap(3);
+  uint64_t acc = 0;
+  for (uint32_t j = 0; j < parts; ++j) {
+    if (acc)
+      for (uint32_t i = sh[j].s0; i < sh[j].s1; ++i) out->path_offsets[i] += acc;
+    acc += sh[j].tot;
+  }
+  out->path_offsets[num] = base;
+  out->total_arcs = base;
+  LaunchStats agg = sh[0].stats;
+  agg.kernel_ms = 0;
+  agg.launches = 0;
+  for (const Shard& S : sh) {
+    agg.kernel_ms += S.stats.kernel_ms;
+    agg.launches += S.stats.launches;
+  }
+  t_last_stats = agg;
+  return FST_OK;
+}
+
 // Runs `compute` (the engines: it fills S.keep and, for pipelines, S.fail) over the shards
 // of a batch and gathers their results into *out.  Shards are contiguous string ranges of
 // equal estimated cost (cost[i]: the work estimate of string i); shard j runs on
@@ -691,15 +808,7 @@ FstError run_sharded(const std::vector<int>& devices, uint32_t nsh, uint32_t num
                      const std::function<FstError(Shard&)>& compute, FstBatchResult* out) {
   // shard 0 runs on the calling thread and switches its current device: give the caller
   // its device back on every return (later calls that use current_device() rely on it)
-  struct DeviceRestore {
-    int dev = -1;
-    DeviceRestore() {
-      if (hipGetDevice(&dev) != hipSuccess) dev = -1;
-    }
-    ~DeviceRestore() {
-      if (dev >= 0) (void)hipSetDevice(dev);
-    }
-  } restore;
+  DeviceRestore_ restore;
   nsh = std::max<uint32_t>(1, std::min<uint32_t>(nsh, std::max<uint32_t>(num, 1)));
   std::vector<Shard> sh(nsh);
   if (nsh == 1) {
@@ -1507,6 +1616,32 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   struct ProfScope {
     ~ProfScope() { t_prof = nullptr; }
   } prof_scope;
+  // one device and a large batch on an rhs without input epsilons: pipelined sub-shards
+  // (FSTAMD_PIPELINE=0 keeps the one-shard path; FSTAMD_PIPELINE=k forces k sub-shards)
+  {
+    const char* pe = std::getenv("FSTAMD_PIPELINE");
+    const int want = pe && *pe ? std::atoi(pe) : -1;
+    uint32_t parts = want > 0 ? (uint32_t)want
+                              : (uint32_t)std::min<uint64_t>(8, num_strings / (1u << 17));
+    parts = std::min<uint32_t>(parts, std::max<uint32_t>(num_strings, 1));
+    const bool single = devices.size() == 1 && nsh == 1;
+    if (single && want != 0 && parts >= 2) {
+      DeviceFst* D = nullptr;
+      if (hipSetDevice(devices[0]) == hipSuccess) D = b->device(devices[0]);
+      if (D && !D->has_eps) {
+        DeviceRestore_ restore;
+        const FstError e = run_pipelined(devices[0], *b, labels, offsets, num_strings, n,
+                                         semantics, parts, out);
+        if (e != FST_OK) {
+          fst_batch_result_free(out);
+          return e;
+        }
+        prof.lap(5);
+        prof.print("fst_compose_frozen_shortest_path_batch (pipelined)");
+        return FST_OK;
+      }
+    }
+  }
   std::vector<double> cost(nsh > 1 ? num_strings : 0);
   for (size_t i = 0; i < cost.size(); ++i) cost[i] = b->chain_cost(offsets[i + 1] - offsets[i]);
   const FstError e = run_sharded(

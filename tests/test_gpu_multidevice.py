@@ -237,3 +237,36 @@ def test_bench_two_ranks_one_gpu(mode):
     assert line["config"]["global_batch"] == 8192
     assert line["config"]["strings_per_gpu"] == 4096
     assert line["checked_vs_oracle"] == 256 and line["value"] > 0
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_pipelined_host_batch(monkeypatch, sem):
+    # the one-device pipelined host batch (sub-shards, each download overlapping the next
+    # compute): the same result as the one-shard path and the oracle, with dead strings,
+    # empty strings and label-0 strings in the mix
+    rng = np.random.default_rng(4242)
+    blob = O.freeze(O.gen("ambiguous", 300, 12))
+    rhs = load_blob(blob)
+    seqs = []
+    for i in range(2000):
+        L = int(rng.integers(0, 40))
+        s = [1] * L
+        if L and i % 7 == 0:
+            s[int(rng.integers(0, L))] = 2     # dies
+        if L and i % 13 == 0:
+            s[int(rng.integers(0, L))] = 0     # lhs epsilon
+        seqs.append(s)
+    labels, offsets = csr(seqs)
+    monkeypatch.setenv("FSTAMD_PIPELINE", "0")
+    one = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+    for parts in ("3", "7"):
+        monkeypatch.setenv("FSTAMD_PIPELINE", parts)
+        got = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+        for k in ("status", "offsets", "ilabels", "olabels"):
+            assert np.array_equal(getattr(got, k), getattr(one, k)), (parts, k)
+        assert np.array_equal(bits(got.weights), bits(one.weights))
+        assert np.array_equal(bits(got.finals), bits(one.finals))
+    ref = O.batch_run(blob, labels, offsets, 0 if sem == LAZY else 1, 1, 8)
+    assert np.array_equal(one.status, expected_status(ref))
+    assert np.array_equal(one.olabels, ref.olabels)
+    assert np.array_equal(bits(one.weights), bits(ref.weights))
