@@ -1,15 +1,15 @@
 #!/bin/bash
 # Profile of the band replay (config 3, kernels/lazy_band.hpp) on the GPU box: the
 # rocprofv3 kernel trace, the HBM traffic passes (FETCH_SIZE, WRITE_SIZE: separate passes)
-# and two SQ instruction-mix passes, on 4,096 strings of config 3's length distribution
-# against the eps-dense rhs at T=4,096 (one launch of lazy_band_kernel, ~15 s).
+# and two SQ instruction-mix passes, on N (default 8,192) strings of config 3's length
+# distribution against the eps-dense rhs at T (default the full 65,536).
 # usage: scripts/profile_band.sh [outdir]   (outdir under gpurun_out/)
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 out=${1:-gpurun_out/prof_band}
 mkdir -p "$out"
 export TMPDIR=/tmp FSTAMD_LAZY_TINY=0
-C="scripts/config3_scaling.py --ts 4096 --n 4096 --cpu-max-t 0"
+C="scripts/config3_scaling.py --ts ${T:-65536} --n ${N:-8192} --cpu-max-t 0"
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
 P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM"
 scripts/gpu_session.sh \

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.." || exit 1
 out=${1:-gpurun_out/sq}; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
-B="bench.py --steps 2 --warmup 1 --no-cpu --lazy-batch 0 --no-varied --no-e2e --batch 65536 $*"
+B="bench.py --steps 2 --warmup 1 --no-cpu --lazy-batch 0 --no-varied --no-e2e --no-f64 --scaling weak --batch 65536 $*"
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
 P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH"
 scripts/gpu_session.sh \
