@@ -11,6 +11,10 @@
 //
 // usage: concurrent_calls [--threads 32] [--calls 1000] [--len 64] [--rhs ambiguous|eps_dense]
 //                         [--transducer-len 4096] [--varied] [--free-midway]
+//                         [--rhs-file BLOB --strings-file CSR]
+// --rhs-file / --strings-file: a frozen blob (fst_batch_load) and the strings to call it on
+// (u32 count, u64 offsets[count + 1], u32 labels = byte + 1), e.g. the WeText-scale tagger
+// stand-in and its utterances (scripts/concurrent_calls_bench.py --wetext).
 // prints one JSON line: calls/s, mismatches, invalid results.
 #include <atomic>
 #include <chrono>
@@ -38,7 +42,7 @@ bool same(double a, double b) { return std::memcmp(&a, &b, 8) == 0; }
 int main(int argc, char** argv) {
   int threads = 32, calls = 1000, len = 64, T = 4096;
   bool varied = false, free_midway = false;
-  std::string kind = "ambiguous";
+  std::string kind = "ambiguous", rhs_file, strings_file;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&] { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
@@ -49,21 +53,46 @@ int main(int argc, char** argv) {
     else if (a == "--rhs") kind = next();
     else if (a == "--varied") varied = true;
     else if (a == "--free-midway") free_midway = true;
+    else if (a == "--rhs-file") rhs_file = next();
+    else if (a == "--strings-file") strings_file = next();
     else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
     }
   }
-  const FstHandle rhs = fst_bench_transducer(kind == "eps_dense" ? 1 : 0, T, 12);
+  const FstHandle rhs = rhs_file.empty() ? fst_bench_transducer(kind == "eps_dense" ? 1 : 0, T, 12)
+                                          : fst_batch_load(rhs_file.c_str());
   if (rhs == FST_INVALID_HANDLE) return 2;
-  // the distinct strings: bytes 0 (label 1), lengths 1..len when varied, some dead (byte 1)
-  const int distinct = varied ? 64 : 1;
-  std::vector<std::vector<uint8_t>> texts(distinct);
-  for (int d = 0; d < distinct; ++d) {
-    const int L = varied ? 1 + (d * 37) % len : len;
-    texts[d].assign(L, 0);
-    if (varied && d % 10 == 3) texts[d][L / 2] = 1;  // label 2: no rhs arc (empty result)
+  std::vector<std::vector<uint8_t>> texts;
+  if (!strings_file.empty()) {  // the caller's strings (labels = byte + 1)
+    FILE* f = std::fopen(strings_file.c_str(), "rb");
+    if (!f) return 2;
+    uint32_t num = 0;
+    bool ok = std::fread(&num, 4, 1, f) == 1;
+    std::vector<uint64_t> off(num + 1);
+    ok = ok && std::fread(off.data(), 8, num + 1, f) == num + 1;
+    std::vector<uint32_t> lab(ok ? off[num] : 0);
+    ok = ok && std::fread(lab.data(), 4, lab.size(), f) == lab.size();
+    std::fclose(f);
+    if (!ok || num == 0) return 2;
+    texts.resize(num);
+    for (uint32_t d = 0; d < num; ++d)
+      for (uint64_t k = off[d]; k < off[d + 1]; ++k) {
+        if (lab[k] == 0 || lab[k] > 256) return 2;  // not a byte string
+        texts[d].push_back((uint8_t)(lab[k] - 1));
+      }
+    kind = "file";
+  } else {
+    // the distinct strings: bytes 0 (label 1), lengths 1..len when varied, some dead (byte 1)
+    const int nd = varied ? 64 : 1;
+    texts.resize(nd);
+    for (int d = 0; d < nd; ++d) {
+      const int L = varied ? 1 + (d * 37) % len : len;
+      texts[d].assign(L, 0);
+      if (varied && d % 10 == 3) texts[d][L / 2] = 1;  // label 2: no rhs arc (empty result)
+    }
   }
+  const int distinct = (int)texts.size();
   // expected answers from the batch entry (lazy semantics, like the single call)
   std::vector<uint32_t> labels;
   std::vector<uint64_t> offs{0};

@@ -36,7 +36,12 @@ def main():
     ap.add_argument("--transducer-len", type=int, default=4096)
     ap.add_argument("--rhs", default="ambiguous")
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--wetext", action="store_true",
+                    help="the WeText-scale tagger stand-in and 4,096 of its utterances "
+                         "(libfst_amd/wetext_standin.py) instead of a bench rhs")
     a = ap.parse_args()
+    if a.wetext:
+        return wetext(a)
     for t in [int(x) for x in a.threads.split(",")]:
         r = subprocess.run([TOOL, "--threads", str(t), "--calls", str(a.calls), "--len", str(a.len),
                             "--transducer-len", str(a.transducer_len), "--rhs", a.rhs],
@@ -61,6 +66,37 @@ def main():
                       "rhs": a.rhs, "transducer_len": a.transducer_len,
                       "kind": "port (oracle/fst_oracle.c -O3, lazy composeShortestPath per "
                               "string, no C-ABI handle overhead)"}), flush=True)
+
+
+def wetext(a):
+    """Concurrent single calls on realistic utterances: the WeText-scale tagger stand-in
+    (0.43 M states) and its utterances, every result checked against the batch entry; the
+    CPU port on nproc threads over the same utterances beside it."""
+    import tempfile
+    from libfst_amd import wetext_standin as W
+    tag = W.tagger()
+    blob = W.freeze_blob(tag)
+    labels, offsets = W.utterances(np.random.default_rng(11), 4096, tag)
+    d = tempfile.mkdtemp()
+    bpath, spath = os.path.join(d, "tagger.fst"), os.path.join(d, "utt.bin")
+    open(bpath, "wb").write(blob)
+    with open(spath, "wb") as f:
+        f.write(np.uint32(len(offsets) - 1).tobytes())
+        f.write(offsets.astype(np.uint64).tobytes())
+        f.write(labels.astype(np.uint32).tobytes())
+    for t in [int(x) for x in a.threads.split(",")]:
+        r = subprocess.run([TOOL, "--threads", str(t), "--calls", str(a.calls), "--rhs-file", bpath,
+                            "--strings-file", spath], capture_output=True, text=True, timeout=600)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        line["rc"] = r.returncode
+        line["rhs"] = "WeText-scale tagger stand-in (0.43 M states), 4,096 utterances"
+        print(json.dumps(line), flush=True)
+    nth = bench.nproc()
+    secs, _ = O.batch_time(blob, labels, offsets, 0, nth)
+    print(json.dumps({"cpu_port_calls_per_s": (len(offsets) - 1) / secs, "threads": nth,
+                      "strings": len(offsets) - 1, "rhs": "WeText-scale tagger stand-in",
+                      "kind": "port (oracle/fst_oracle.c -O3, lazy composeShortestPath per "
+                              "utterance, no C-ABI handle overhead)"}), flush=True)
 
 
 if __name__ == "__main__":
