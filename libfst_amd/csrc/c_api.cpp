@@ -661,13 +661,8 @@ bool alloc_result(FstBatchResult* out, uint32_t num, uint64_t tot) {
 FstError shard_download(Shard& S, FstBatchResult* out, uint64_t arc_base) {
   const uint32_t num = S.s1 - S.s0;
   const hipStream_t stream = S.E.stream();
-  // FSTAMD_D2H_NOCU=1: the copies into the pinned result as DeviceToDeviceNoCU (the DMA
-  // engines, no compute units; the pinned pages are device-addressable) -- a blit copy
-  // kernel waits for CU slots that persistent engine kernels hold (round 3's streaming try)
-  static const hipMemcpyKind kind =
-      std::getenv("FSTAMD_D2H_NOCU") ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
   const auto d2h = [stream](void* dst, const void* src, size_t b) {
-    return b == 0 || hipMemcpyAsync(dst, src, b, kind, stream) == hipSuccess;
+    return b == 0 || hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, stream) == hipSuccess;
   };
   if (!(d2h(out->status + S.s0, S.st->p, num * 4ull) &&
         d2h(out->final_weights + S.s0, S.fin->p, num * 8ull) &&

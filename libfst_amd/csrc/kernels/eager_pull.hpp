@@ -341,33 +341,16 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t f = kEmptyKey;
         DT b = kInf;
         uint32_t c = kEmptyKey;
-#ifdef FSTAMD_P_KEY64
-        if constexpr (F32) {
-          // (distance, key) as one 64-bit key: the bits of a float >= +0 order as its value,
-          // so one 64-bit min per in-arc gives the distance and the tight key together
-          unsigned long long best = ~0ull;
+        // (one 64-bit min of (distance bits, key) per in-arc instead of fmin + the tight
+        // pass: 25 fewer VALU per unrolled row, same 41.4 ms per 1M metric strings, round 4)
 #pragma unroll
-          for (int m = 0; m < KP; ++m) {
-            pull_candidate<W>(S, rr[m], tmin8, pk[m], nd[m], rw[m]);
-            f = min(f, pk[m]);
-            const unsigned long long key =
-                ((unsigned long long)__float_as_uint((float)nd[m]) << 32) | pk[m];
-            best = key < best ? key : best;
-          }
-          b = (DT)__uint_as_float((uint32_t)(best >> 32));
-          c = (uint32_t)best;
-        } else
-#endif
-        {
-#pragma unroll
-          for (int m = 0; m < KP; ++m) {
-            pull_candidate<W>(S, rr[m], tmin8, pk[m], nd[m], rw[m]);
-            f = min(f, pk[m]);
-            b = fmin(b, nd[m]);
-          }
-#pragma unroll
-          for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
+        for (int m = 0; m < KP; ++m) {
+          pull_candidate<W>(S, rr[m], tmin8, pk[m], nd[m], rw[m]);
+          f = min(f, pk[m]);
+          b = fmin(b, nd[m]);
         }
+#pragma unroll
+        for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
         if (want_work) {
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
