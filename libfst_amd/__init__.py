@@ -8,4 +8,5 @@ from .fst import (  # noqa: F401
     FST_NO_STATE, FST_PATH_CYCLE, FST_PATH_EMPTY, FST_PATH_ERROR_N, FST_PATH_OK,
     FST_PATH_OUTPUT_FULL, FST_PATH_OVERFLOW, FST_PATH_UNSUPPORTED, FST_SEM_EAGER, FST_SEM_LAZY,
     Fst, MutableFst, compose_frozen, compose_frozen_shortest_path,
-    compose_frozen_shortest_path_batch, last_launch_stats, lib, pipeline_batch, shortest_path)
+    coalescer_state, compose_frozen_shortest_path_batch, last_launch_stats, lib, pipeline_batch,
+    shortest_path)
