@@ -734,21 +734,73 @@ FstError run_pipelined(int dev, FrozenFst& b, const uint32_t* labels, const uint
   for (uint32_t i = 0; i <= num; ++i) rebased[i] = offsets[i] - offsets[0];
   DevBuf d_lab(total * 4), d_off((num + 1) * 8ull);
   if (!d_lab.p || !d_off.p) return FST_OOM;
-  if (total && hipMemcpyAsync(d_lab.p, labels + offsets[0], total * 4, hipMemcpyHostToDevice,
-                              stream) != hipSuccess)
-    return FST_OOM;
   if (hipMemcpyAsync(d_off.p, rebased.data(), (num + 1) * 8ull, hipMemcpyHostToDevice, stream) !=
       hipSuccess)
     return FST_OOM;
+  std::vector<Shard> sh(parts);
+  for (uint32_t j = 0; j < parts; ++j) {
+    sh[j].dev = dev;
+    sh[j].s0 = (uint32_t)((uint64_t)num * j / parts);
+    sh[j].s1 = (uint32_t)((uint64_t)num * (j + 1) / parts);
+  }
+  // The labels go up per sub-shard on a thread and stream of their own (a pageable source
+  // is staged through pinned memory on the copying thread), so sub-shard j + 1's upload
+  // runs while sub-shard j computes; the engine's stream waits on each upload's event.
+  struct Uploader {
+    hipStream_t s = nullptr;
+    std::vector<hipEvent_t> ev;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t ready = 0;
+    bool failed = false;
+    std::thread th;
+    ~Uploader() {
+      if (th.joinable()) th.join();
+      if (s) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+      }
+      for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+  } U;
+  if (hipStreamCreateWithFlags(&U.s, hipStreamNonBlocking) != hipSuccess) return FST_OOM;
+  U.ev.assign(parts, nullptr);
+  for (uint32_t j = 0; j < parts; ++j)
+    if (hipEventCreateWithFlags(&U.ev[j], hipEventDisableTiming) != hipSuccess) return FST_OOM;
+  U.th = std::thread([&, dev] {
+    bool ok = hipSetDevice(dev) == hipSuccess;
+    for (uint32_t j = 0; j < parts; ++j) {
+      const uint64_t a = rebased[sh[j].s0], z = rebased[sh[j].s1];
+      ok = ok && (z == a || hipMemcpyAsync((uint32_t*)d_lab.p + a, labels + offsets[0] + a,
+                                           (z - a) * 4, hipMemcpyHostToDevice, U.s) == hipSuccess);
+      ok = ok && hipEventRecord(U.ev[j], U.s) == hipSuccess;
+      std::lock_guard<std::mutex> g(U.mu);
+      if (!ok) {
+        U.failed = true;
+        U.cv.notify_all();
+        return;
+      }
+      U.ready = j + 1;
+      U.cv.notify_all();
+    }
+  });
   if (t_prof) t_prof->lap(0);
   if (!alloc_result(out, num, total)) return FST_OOM;  // paths of L arcs: <= total arcs
-  std::vector<Shard> sh(parts);
+  // every return below first waits for the downloads in flight: on an error the caller
+  // frees the result, whose pinned pages must not be written after that
+  struct SyncOnExit {
+    hipStream_t s;
+    ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+  } sync_copies{C.s};
   uint64_t base = 0;
   for (uint32_t j = 0; j < parts; ++j) {
     Shard& S = sh[j];
-    S.dev = dev;
-    S.s0 = (uint32_t)((uint64_t)num * j / parts);
-    S.s1 = (uint32_t)((uint64_t)num * (j + 1) / parts);
+    {
+      std::unique_lock<std::mutex> g(U.mu);
+      U.cv.wait(g, [&] { return U.failed || U.ready > j; });
+      if (U.failed) return FST_OOM;
+    }
+    if (hipStreamWaitEvent(stream, U.ev[j], 0) != hipSuccess) return FST_OOM;
     uint32_t ml = 0;
     for (uint32_t i = S.s0; i < S.s1; ++i) ml = std::max<uint32_t>(ml, (uint32_t)(rebased[i + 1] - rebased[i]));
     // the sub-shard reads the whole upload: its offsets index the one label array
