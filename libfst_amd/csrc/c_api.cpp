@@ -1038,7 +1038,7 @@ FstError run_chain_batch_dev(DeviceEngine::Lease& E, DeviceFst& D, const ChainIn
 // fst_compose_frozen_shortest_path on a compileString lhs is one chain string.  Calls that
 // arrive while a batch is in flight are combined (flat combining): the first caller of an
 // idle device becomes a leader, takes every queued call (grouped by rhs and n), runs them
-// as one batch on an engine lease and hands each caller its path; up to kChainLeaders
+// as one batch on an engine lease and hands each caller its path; up to chain_leaders()
 // batches run at once (separate engines and streams).  A lone caller runs its own string
 // with no added latency; N concurrent callers share launches and host <-> device trips, so
 // calls/s grows with N (the reference scales calls over threads, README.md:68-82).
@@ -1065,7 +1065,14 @@ struct ChainCombiner {
   std::deque<ChainCall*> q;
   int leaders = 0;
 };
-constexpr int kChainLeaders = 2;
+// leaders at once (each on its own engine lease); FSTAMD_CHAIN_LEADERS overrides (A/B)
+int chain_leaders() {
+  static const int n = [] {
+    const char* e = std::getenv("FSTAMD_CHAIN_LEADERS");
+    return e && std::atoi(e) > 0 ? std::atoi(e) : 2;
+  }();
+  return n;
+}
 constexpr size_t kChainMaxBatch = 1u << 16;
 
 ChainCombiner& chain_combiner(int dev) {
@@ -1136,7 +1143,7 @@ FstError coalesced_chain_call(int dev, ChainCall* c) {
   // a call leads when a leader slot is free and no leader has taken it yet; a slot is only
   // ever taken here, by the thread itself under the lock, and given back by the same thread
   // after its batch, so slots can be neither lost nor duplicated (round-3 ADVICE)
-  c->cv.wait(lk, [&] { return c->done || (!c->taken && C.leaders < kChainLeaders); });
+  c->cv.wait(lk, [&] { return c->done || (!c->taken && C.leaders < chain_leaders()); });
   if (c->done) return c->err;
   ++C.leaders;
   // this call first, then the oldest queued ones
@@ -1148,7 +1155,7 @@ FstError coalesced_chain_call(int dev, ChainCall* c) {
   C.q.erase(C.q.begin(), C.q.begin() + take);
   for (ChainCall* x : batch) x->taken = true;
   // a second free slot: let the oldest remaining caller lead a batch beside this one
-  if (!C.q.empty() && C.leaders < kChainLeaders) C.q.front()->cv.notify_one();
+  if (!C.q.empty() && C.leaders < chain_leaders()) C.q.front()->cv.notify_one();
   lk.unlock();
   run_chain_calls(dev, batch);
   lk.lock();

@@ -42,10 +42,10 @@ const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
   return pull_f32(rhs, max_len) && !std::getenv("FSTAMD_P_F64") ? pull_kernel_for<true>(rhs.rev)
                                                                  : pull_kernel_for<false>(rhs.rev);
 }
-// Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 4 with f32 cells (10.2 KB)
-// when every distance is an integer below 2^24.
+// Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 5 with f32 cells (7.4 KB;
+// round 3: 4 at 10.2 KB) when every distance is an integer below 2^24.
 #ifndef FSTAMD_LP_WAVES_F32  // A/B builds
-#define FSTAMD_LP_WAVES_F32 4
+#define FSTAMD_LP_WAVES_F32 5
 #endif
 constexpr int kLazyPullWaves = 3;
 template <int KP, bool F32>
@@ -273,7 +273,8 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
 }
 
 bool lazy_pull_f32(const DeviceFst& rhs, uint32_t max_len) {
-  return pull_f32(rhs, max_len) && !std::getenv("FSTAMD_LP_F64");
+  // (the f32 cells keep d - tb <= the largest arc weight in 8 bits, kernels/lazy_pull.hpp)
+  return pull_f32(rhs, max_len) && rhs.int_wmax <= kLpF32WMax && !std::getenv("FSTAMD_LP_F64");
 }
 
 int lazy_pull_waves_per_cu(const DeviceFst& rhs, uint32_t max_len) {

@@ -44,7 +44,13 @@ namespace fstamd {
 constexpr uint32_t kLpAbsent = 0xFFF00000u;  // rank words of a slot that holds no tuple
 constexpr uint32_t kLpRunMask = 0xFFFu;      // run (<= 4095 layers) below the pop rank
 constexpr uint32_t kLpMaxLen = 4095;
-constexpr int kLpBins = 256;  // counting sort of the pop order: integer keys d - dmin < 256
+// counting sort of the pop order: integer keys d - dmin below this (f64 cells: 256; f32
+// cells: 128, so that 5 waves' LDS fits a CU)
+template <typename DT>
+constexpr int lp_bins() { return sizeof(DT) == 4 ? 128 : 256; }
+// f32 cells keep d - tb (the first toucher's distance) in 8 bits of the pop word: the lazy
+// pull takes f32 cells only when every arc weight is at most this
+constexpr double kLpF32WMax = 255.0;
 constexpr int kLpChase = 15;  // backtraces batched per wave (<= kChaseBatch: slabs)
 
 // DT: the cells' distance storage.  double in general; float when every distance is an
@@ -74,24 +80,41 @@ struct LazyPullCells {  // f64 distances: d, {idw, pw}, tb
     *w = (*w & kLpRunMask) | (q << 20);
   }
 };
-// f32 distances (exact: integers below 2^24): {d, idw} and {pw, tb} as two 8-B arrays, so
-// the merge reads one 8-B word per in-arc (as tier P) and the certificate one per source
+// f32 distances (exact: integers below 2^24): {d, idw} (8 B) and one 4-B pop word
+// pw = pop rank << 20 | (d - tb) << 12 | run, so the merge reads one 8-B word per in-arc
+// (as tier P).  d - tb lies in [0, the largest arc weight]: the first toucher u* pops no
+// later than a tight in-neighbour (d(u*) <= d), and d <= d(u*) + w; the start's tb = -1
+// gives 1.  5 waves' cells, sort and jobs fit a CU's LDS (7.4 KB per wave).
+constexpr uint32_t kLpDeltaShift = 12, kLpDeltaMask = 0xFFu;
 template <int W>
 struct LazyPullCells<W, float> {
   uint2 a[W + 1];                  // {f32 bits of d, idw}
-  uint2 b[W + 1];                  // {pw, f32 bits of tb}
+  uint32_t b[W + 1];               // pw
   __device__ __forceinline__ uint2 get_a(uint32_t o) const { return *(const uint2*)((const char*)a + o); }
-  __device__ __forceinline__ uint2 get_b(uint32_t o) const { return *(const uint2*)((const char*)b + o); }
   __device__ __forceinline__ float get_d(uint32_t o) const { return __uint_as_float(get_a(o).x); }
   __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return get_a(o).y; }
-  __device__ __forceinline__ uint32_t get_pw(uint32_t o) const { return get_b(o).x; }
-  __device__ __forceinline__ float get_tb(uint32_t o) const { return __uint_as_float(get_b(o).y); }
+  __device__ __forceinline__ uint32_t get_pw(uint32_t o) const {
+    return *(const uint32_t*)((const char*)b + (o >> 1));
+  }
+  // d - tb of the cell's tuple
+  __device__ __forceinline__ uint32_t get_delta(uint32_t o) const {
+    return (get_pw(o) >> kLpDeltaShift) & kLpDeltaMask;
+  }
+  __device__ __forceinline__ float get_tb(uint32_t o) const {
+    return get_d(o) - (float)get_delta(o);
+  }
+  // pw carries the run in its low 12 bits; tb enters as d - delta
   __device__ __forceinline__ void set(uint32_t i, float dd, uint32_t idw, uint32_t pw, float t) {
     a[i] = make_uint2(__float_as_uint(dd), idw);
-    b[i] = make_uint2(pw, __float_as_uint(t));
+    b[i] = pw < kLpAbsent ? pw | ((uint32_t)(dd - t) << kLpDeltaShift) : pw;
+  }
+  // the same with delta already known (pw | delta << 12)
+  __device__ __forceinline__ void set_packed(uint32_t i, float dd, uint32_t idw, uint32_t pwd) {
+    a[i] = make_uint2(__float_as_uint(dd), idw);
+    b[i] = pwd;
   }
   __device__ __forceinline__ void set_pop(uint32_t i, uint32_t q) {
-    b[i].x = (b[i].x & kLpRunMask) | (q << 20);
+    b[i] = (b[i] & 0xFFFFFu) | (q << 20);
   }
 };
 
@@ -100,17 +123,18 @@ struct LazyPullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys p << 3 | j < 8 W
   LazyPullCells<W, DT> c;
   uint32_t ord0[W];                // (key << 9 |) slot in id order
-  // P1-P3 and the split sort use {bits, pre, ord1}; the counting sort overlays {mask,
-  // hist} on them (bits lies under mask, which the counting sort leaves all zero)
+  // P1-P3 use {bits, pre}; the sorts (P4, after P3 read pre) overlay the split sort's
+  // second buffer ord1 or the counting sort's {mask, hist} on them.  bits must be all zero
+  // when P1 starts: the counting sort leaves mask zero, the split sort re-zeroes bits.
   union {
     struct {
       unsigned long long bits[kWords];
       uint4 pre[kWords];
-      uint32_t ord1[W];            // split sort: the other buffer
     };
+    uint32_t ord1[W];              // split sort: the other buffer
     struct {
-      unsigned long long mask[kLpBins];  // lanes of the current 64-chunk holding key b
-      uint32_t hist[kLpBins];            // running count of key b, then its prefix
+      unsigned long long mask[lp_bins<DT>()];  // lanes of the current 64-chunk holding key b
+      uint32_t hist[lp_bins<DT>()];            // running count of key b, then its prefix
     };
   };
   unsigned long long best;
@@ -281,6 +305,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // ---- (P1) pull merge per target: first toucher, distance, back-pointer, C ----
       uint32_t fst[EW], bk[EW], bra[EW], runx[EW];
       DT bd[EW], tbx[EW];
+      // f32 cells: the distance (an integer below 2^24) and d - tb (<= 255) share one word,
+      // the run sits in fst's low 17 bits (P3 reads only fst >> 17): 3 words per row live
+      // across P2 instead of 6 (5 waves per SIMD)
+      uint32_t bdp[EW];
       bool uncert = false;
 #pragma unroll
       for (int e = 0; e < EW; ++e) {
@@ -290,6 +318,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         bd[e] = kInf;
         tbx[e] = kInf;
         runx[e] = 0;
+        bdp[e] = 0;
         if ((uint32_t)e >= rows_n) continue;  // uniform
         const uint32_t i = (uint32_t)e * 64 + lane;
         const uint32_t t = tn + i;
@@ -375,13 +404,23 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
         const uint32_t ou = pres ? (ff & 0xFFFu) : 8u * W;
         const DT du = CL.get_d(ou);
-        const DT tbu = CL.get_tb(ou);
-        const uint32_t ruu = CL.get_pw(ou) & kLpRunMask;
+        const uint32_t pwu = CL.get_pw(ou);
+        const uint32_t ruu = pwu & kLpRunMask;
         // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
         // round trip: its certificate alone usually settles C
         const uint32_t ob = pres ? (c & 0xFFFu) : 8u * W;
-        const DT tbb = CL.get_tb(ob);
-        const uint32_t rbb = CL.get_pw(ob) & kLpRunMask;
+        const uint32_t pwb = CL.get_pw(ob);
+        const uint32_t rbb = pwb & kLpRunMask;
+        DT tbu, tbb;
+        if constexpr (F32) {
+          // tb = d - delta; the back source of a 0-weight back arc is at d(x) = b (a
+          // positive-weight one certifies x by itself, so its tb is never decisive)
+          tbu = du - (DT)((pwu >> kLpDeltaShift) & kLpDeltaMask);
+          tbb = b - (DT)((pwb >> kLpDeltaShift) & kLpDeltaMask);
+        } else {
+          tbu = CL.get_tb(ou);
+          tbb = CL.get_tb(ob);
+        }
         const DT tx = du;
         const uint32_t rx = 1u + (tbu == tx ? ruu : 0u);
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
@@ -405,8 +444,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
             const uint32_t o = bpk[m] & 0xFFFu;
-            const DT tbm = CL.get_tb(o);
-            const uint32_t rm = CL.get_pw(o) & kLpRunMask;
+            const uint32_t pwm = CL.get_pw(o);
+            // (f32: a tight 0-weight source sits at b; any other in-arc's tb is not used)
+            DT tbm;
+            if constexpr (F32) tbm = b - (DT)((pwm >> kLpDeltaShift) & kLpDeltaMask);
+            else tbm = CL.get_tb(o);
+            const uint32_t rm = pwm & kLpRunMask;
             cert |= nd[m] == b && ((bpk[m] & kRevPos) || tbm < tx || (tbm == tx && rm < rx));
           }
           if (hubs) {  // the further blocks' tight in-arcs
@@ -427,12 +470,17 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           }
           uncert |= !cert;
         }
-        fst[e] = ff;
-        bd[e] = b;
         bk[e] = c;
         bra[e] = ra;
-        tbx[e] = tx;
-        runx[e] = rx;
+        if constexpr (F32) {
+          fst[e] = ff < kLpAbsent ? (ff & ~0x1FFFFu) | rx : ff;
+          bdp[e] = ff < kLpAbsent ? (uint32_t)b | ((uint32_t)(b - tx) << 24) : 0u;
+        } else {
+          fst[e] = ff;
+          bd[e] = b;
+          tbx[e] = tx;
+          runx[e] = rx;
+        }
         if (pres) {
           const uint32_t key = ff >> 17;  // pop rank << 3 | j
           atomicOr(&S.bits[key >> 6], 1ull << (key & 63u));
@@ -482,8 +530,18 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
         // pop rank: identity until the sort below fills it in
-        CL.set(i, pres ? bd[e] : kInf, pres ? rank << 20 : kLpAbsent,
-               pres ? (rank << 20) | runx[e] : kLpAbsent, pres ? tbx[e] : kInf);
+        DT dx;
+        if constexpr (F32) {
+          dx = pres ? (DT)(bdp[e] & 0xFFFFFFu) : kInf;
+          CL.set_packed(i, dx, pres ? rank << 20 : kLpAbsent,
+                        pres ? (rank << 20) | ((bdp[e] >> 24) << kLpDeltaShift) |
+                                   (fst[e] & kLpRunMask)
+                             : kLpAbsent);
+        } else {
+          dx = bd[e];
+          CL.set(i, pres ? bd[e] : kInf, pres ? rank << 20 : kLpAbsent,
+                 pres ? (rank << 20) | runx[e] : kLpAbsent, pres ? tbx[e] : kInf);
+        }
         if (pres && sort) S.ord0[rank] = i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
@@ -496,7 +554,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 72)];
             if (!w_is_zero(fw2)) {
-              const unsigned long long kk = okey((double)bd[e] + fw2);
+              const unsigned long long kk = okey((double)dx + fw2);
               const uint32_t pp = (rank << 9) | i;
               if (kk < mykey || (kk == mykey && pp < myp)) {
                 mykey = kk;
@@ -578,7 +636,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #ifdef FSTAMD_LP_SPLIT_ONLY  // A/B: the split sort for every layer
         const bool counting = false;
 #else
-        const bool counting = ik && mx - mn < (DT)kLpBins;
+        const bool counting = ik && mx - mn < (DT)lp_bins<DT>();
 #endif
         unsigned long long vary;
         if (ik) {
@@ -594,7 +652,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           // it in the chunk; hist[b] carries the count from earlier chunks.  One wave's
           // LDS operations complete in order, so the fences below separate the steps.
 #pragma unroll
-          for (int b = 0; b < kLpBins / 64; ++b) {
+          for (int b = 0; b < lp_bins<DT>() / 64; ++b) {
             S.mask[b * 64 + lane] = 0;
             S.hist[b * 64 + lane] = 0;
           }
@@ -692,6 +750,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         for (uint32_t q = lane; q < n_next && !counting; q += 64) {  // pop rank q -> cell
           CL.set_pop((cur ? S.ord1 : S.ord0)[q] & 511u, q);
         }
+        wave_lds_sync();
+        if (!counting && lane < (uint32_t)kWords) S.bits[lane] = 0;  // (ord1 overlays bits)
         wave_lds_sync();
         }  // !in_order
         io = in_order;
