@@ -81,11 +81,12 @@ struct LazyPullCells {  // f64 distances: d, {idw, pw}, tb
   }
 };
 // f32 distances (exact: integers below 2^24): {d, idw} (8 B) and one 4-B pop word
-// pw = pop rank << 20 | (d - tb) << 12 | run, so the merge reads one 8-B word per in-arc
+// pw = pop rank << 20 | (255 - (d - tb)) << 12 | run, so the merge reads one 8-B word per in-arc
 // (as tier P).  d - tb lies in [0, the largest arc weight]: the first toucher u* pops no
 // later than a tight in-neighbour (d(u*) <= d), and d <= d(u*) + w; the start's tb = -1
 // gives 1.  5 waves' cells, sort and jobs fit a CU's LDS (7.4 KB per wave).
-constexpr uint32_t kLpDeltaShift = 12, kLpDeltaMask = 0xFFu;
+// the pop word of an f32 cell: pop rank << 20 | cf << 12 | run, cf = 255 - (d - tb)
+constexpr uint32_t kLpCfShift = 12, kLpCfMask = 0xFFu, kLpCkeyMask = 0xFFFFFu;
 template <int W>
 struct LazyPullCells<W, float> {
   uint2 a[W + 1];                  // {f32 bits of d, idw}
@@ -98,7 +99,7 @@ struct LazyPullCells<W, float> {
   }
   // d - tb of the cell's tuple
   __device__ __forceinline__ uint32_t get_delta(uint32_t o) const {
-    return (get_pw(o) >> kLpDeltaShift) & kLpDeltaMask;
+    return kLpCfMask - ((get_pw(o) >> kLpCfShift) & kLpCfMask);
   }
   __device__ __forceinline__ float get_tb(uint32_t o) const {
     return get_d(o) - (float)get_delta(o);
@@ -106,7 +107,7 @@ struct LazyPullCells<W, float> {
   // pw carries the run in its low 12 bits; tb enters as d - delta
   __device__ __forceinline__ void set(uint32_t i, float dd, uint32_t idw, uint32_t pw, float t) {
     a[i] = make_uint2(__float_as_uint(dd), idw);
-    b[i] = pw < kLpAbsent ? pw | ((uint32_t)(dd - t) << kLpDeltaShift) : pw;
+    b[i] = pw < kLpAbsent ? pw | ((kLpCfMask - (uint32_t)(dd - t)) << kLpCfShift) : pw;
   }
   // the same with delta already known (pw | delta << 12)
   __device__ __forceinline__ void set_packed(uint32_t i, float dd, uint32_t idw, uint32_t pwd) {
@@ -410,25 +411,34 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         // round trip: its certificate alone usually settles C
         const uint32_t ob = pres ? (c & 0xFFFu) : 8u * W;
         const uint32_t pwb = CL.get_pw(ob);
-        const uint32_t rbb = pwb & kLpRunMask;
-        DT tbu, tbb;
-        if constexpr (F32) {
-          // tb = d - delta; the back source of a 0-weight back arc is at d(x) = b (a
-          // positive-weight one certifies x by itself, so its tb is never decisive)
-          tbu = du - (DT)((pwu >> kLpDeltaShift) & kLpDeltaMask);
-          tbb = b - (DT)((pwb >> kLpDeltaShift) & kLpDeltaMask);
-        } else {
-          tbu = CL.get_tb(ou);
-          tbb = CL.get_tb(ob);
-        }
         const DT tx = du;
-        const uint32_t rx = 1u + (tbu == tx ? ruu : 0u);
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
         // source certified by (tb, run).  The back arc is tight, so its own certificate
         // (positive weight: kRevPos in its key, or its source's (tb, run)) is sufficient;
         // the loop over every tight in-arc runs only for rows where some lane is left
-        // without one
-        const bool fast = !pres || (c & kRevPos) || tbb < tx || (tbb == tx && rbb < rx);
+        // without one.
+        // f32 cells: a tight 0-weight source u sits at d(u) = b, so tb(u) < tb(x) iff
+        // d(u) - tb(u) > b - tb(x): with the cell field cf = 255 - (d - tb), (tb, run)(u) <
+        // (tb, run)(x) is one integer compare of (cf << 12 | run), the pop word's low 20
+        // bits (a positive-weight in-arc certifies by itself, so its field never decides)
+        uint32_t rx, ckx = 0;
+        DT tbu = 0;
+        bool fast;
+        if constexpr (F32) {
+          rx = 1u + (((pwu >> kLpCfShift) & kLpCfMask) == kLpCfMask ? ruu : 0u);  // tb(u*) == d(u*)
+          ckx = ((kLpCfMask - (uint32_t)(b - du)) << kLpCfShift) | rx;
+          fast = !pres || (c & kRevPos) || (pwb & kLpCkeyMask) < ckx;
+        } else {
+          tbu = CL.get_tb(ou);
+          rx = 1u + (tbu == tx ? ruu : 0u);
+          const DT tbb = CL.get_tb(ob);
+          const uint32_t rbb = pwb & kLpRunMask;
+          fast = !pres || (c & kRevPos) || tbb < tx || (tbb == tx && rbb < rx);
+        }
+        auto certifies = [&](uint32_t pw_src, DT tb_src) -> bool {  // a tight 0-weight source
+          if constexpr (F32) return (pw_src & kLpCkeyMask) < ckx;
+          else return tb_src < tx || (tb_src == tx && (pw_src & kLpRunMask) < rx);
+        };
 #ifdef FSTAMD_LP_NOCERT  // timing experiment only: no certificate check
         if (false) {
 #elif defined(FSTAMD_LP_FULLCERT)  // A/B: the full loop on every row that needs it
@@ -444,13 +454,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
             const uint32_t o = bpk[m] & 0xFFFu;
-            const uint32_t pwm = CL.get_pw(o);
-            // (f32: a tight 0-weight source sits at b; any other in-arc's tb is not used)
-            DT tbm;
-            if constexpr (F32) tbm = b - (DT)((pwm >> kLpDeltaShift) & kLpDeltaMask);
-            else tbm = CL.get_tb(o);
-            const uint32_t rm = pwm & kLpRunMask;
-            cert |= nd[m] == b && ((bpk[m] & kRevPos) || tbm < tx || (tbm == tx && rm < rx));
+            DT tbm = 0;
+            if constexpr (!F32) tbm = CL.get_tb(o);
+            cert |= nd[m] == b && ((bpk[m] & kRevPos) || certifies(CL.get_pw(o), tbm));
           }
           if (hubs) {  // the further blocks' tight in-arcs
             for (uint32_t x = 1;; ++x) {
@@ -461,10 +467,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                 const RT r2 = rec(rxx + m);
                 const uint32_t o = min(r_src(r2) - tmin8, 8u * W);
                 const DT d = CL.get_d(o);
-                const DT tbm = CL.get_tb(o);
-                const uint32_t rm = CL.get_pw(o) & kLpRunMask;
-                cert |= d + r_w(r2) == b &&
-                        (r_w(r2) > (DT)0 || tbm < tx || (tbm == tx && rm < rx));
+                DT tbm = 0;
+                if constexpr (!F32) tbm = CL.get_tb(o);
+                cert |= d + r_w(r2) == b && (r_w(r2) > (DT)0 || certifies(CL.get_pw(o), tbm));
               }
             }
           }
@@ -474,7 +479,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         bra[e] = ra;
         if constexpr (F32) {
           fst[e] = ff < kLpAbsent ? (ff & ~0x1FFFFu) | rx : ff;
-          bdp[e] = ff < kLpAbsent ? (uint32_t)b | ((uint32_t)(b - tx) << 24) : 0u;
+          bdp[e] = ff < kLpAbsent ? (uint32_t)b | ((ckx >> kLpCfShift) << 24) : 0u;
         } else {
           fst[e] = ff;
           bd[e] = b;
@@ -534,7 +539,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if constexpr (F32) {
           dx = pres ? (DT)(bdp[e] & 0xFFFFFFu) : kInf;
           CL.set_packed(i, dx, pres ? rank << 20 : kLpAbsent,
-                        pres ? (rank << 20) | ((bdp[e] >> 24) << kLpDeltaShift) |
+                        pres ? (rank << 20) | ((bdp[e] >> 24) << kLpCfShift) |
                                    (fst[e] & kLpRunMask)
                              : kLpAbsent);
         } else {

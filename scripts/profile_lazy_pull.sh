@@ -8,7 +8,7 @@ out=${1:-gpurun_out/prof_lp}
 mkdir -p "$out"
 export TMPDIR=/tmp
 B="bench.py --semantics lazy --steps 5 --warmup 2 --no-cpu --lazy-batch 0 --no-varied --no-e2e --no-f64"
-S="bench.py --semantics lazy --steps 2 --warmup 1 --no-cpu --lazy-batch 0 --no-varied --no-e2e --batch 65536"
+S="bench.py --semantics lazy --steps 2 --warmup 1 --no-cpu --lazy-batch 0 --no-varied --no-e2e --no-f64 --global-batch 65536"
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
 P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM"
 scripts/gpu_session.sh \
