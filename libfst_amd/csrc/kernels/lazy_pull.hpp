@@ -123,7 +123,7 @@ template <int W, typename DT>
 struct LazyPullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys p << 3 | j < 8 W
   LazyPullCells<W, DT> c;
-  uint32_t ord0[W];                // (key << 9 |) slot in id order
+  uint32_t ord0[W];                // (key << 9 |) slot in id order (f32 cells: first d)
   // P1-P3 use {bits, pre}; the sorts (P4, after P3 read pre) overlay the split sort's
   // second buffer ord1 or the counting sort's {mask, hist} on them.  bits must be all zero
   // when P1 starts: the counting sort leaves mask zero, the split sort re-zeroes bits.
@@ -547,7 +547,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           CL.set(i, pres ? bd[e] : kInf, pres ? rank << 20 : kLpAbsent,
                  pres ? (rank << 20) | runx[e] : kLpAbsent, pres ? tbx[e] : kInf);
         }
-        if (pres && sort) S.ord0[rank] = i;
+        // (f32 cells: the distance's bits, ordered as the non-negative distances are; P4
+        // rebuilds the slots from the cells' id-rank words when the layer needs its sort)
+        if (pres && sort) S.ord0[rank] = F32 ? __float_as_uint((float)dx) : i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -590,10 +592,24 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         for (int e = 0; e < EW; ++e) {
           if ((uint32_t)e >= rows_s) continue;  // uniform
           const uint32_t q = (uint32_t)e * 64 + lane;
-          if (q + 1 < n_next) unsorted |= CL.get_d(8 * S.ord0[q]) > CL.get_d(8 * S.ord0[q + 1]);
+          if (q + 1 < n_next) {
+            if constexpr (F32) unsorted |= S.ord0[q] > S.ord0[q + 1];
+            else unsorted |= CL.get_d(8 * S.ord0[q]) > CL.get_d(8 * S.ord0[q + 1]);
+          }
         }
         const bool in_order = !__ballot(unsorted);
         if (!in_order) {
+        if constexpr (F32) {  // the id order's slots, from the cells' id ranks
+          wave_lds_sync();
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {
+            if ((uint32_t)e >= rows_n) continue;  // uniform
+            const uint32_t i = (uint32_t)e * 64 + lane;
+            const uint32_t iw = CL.get_idw(8 * i);
+            if (iw < kLpAbsent) S.ord0[iw >> 20] = i;
+          }
+          wave_lds_sync();
+        }
         // keys: integer distances with d - dmin < 2^23 (ik) sort by d - dmin, others by
         // their f64 bit patterns; dmin / dmax over the layer, then key << 9 | slot in ord0
         DT mn = kInf, mx = -kInf;
