@@ -87,7 +87,12 @@ struct RevView {
   // the weight, olabel}; only when every arc weight is an integer in [0, 2^24) (exact in
   // f32; DeviceFst::int_wmax), else null
   const uint4* rrec32;
+  // [nblocks * kp] the records in 8 B: {src, y | weight}, only when every arc weight is an
+  // integer in [0, kRec8WMax] (it sits in y's low 3 bits, below the byte offset the keys OR
+  // in), else null
+  const uint2* rrec8;
 };
+constexpr double kRec8WMax = 7.0;
 
 struct DeviceFst {
   int dev = 0;
@@ -118,7 +123,7 @@ struct DeviceFst {
   // ... and one whose 128-tuple LDS size handed on over a third of a batch starts at 256
   mutable std::atomic<int> tiny_lazy_256{0}, tiny_eager_256{0};
   RevView rev{};
-  void* rev_bufs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  void* rev_bufs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a
   // breadth-first renumbering of an rhs with scattered ids (device_engine.hip
   // bfs_renumbering).  Every device view (RhsView, RevView) uses it; results do not.

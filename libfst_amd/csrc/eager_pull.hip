@@ -17,10 +17,11 @@ namespace {
 // metric: 5 waves 20.3 M strings/s, 4 waves 18.5 M, 6 waves 19.8 M with spills);
 // 8-record blocks need 4.
 
-template <int KP, int WV, bool F32>
+// RK: the records the kernel reads -- 0 RevRec (f64 cells), 1 rrec32, 2 rrec8 (f32 cells)
+template <int KP, int WV, int RK>
 const void* pull_kernel_ptr(bool direct) {
-  return direct ? (const void*)eager_pull_kernel<kPullRows, KP, true, WV, F32>
-                : (const void*)eager_pull_kernel<kPullRows, KP, false, WV, F32>;
+  return direct ? (const void*)eager_pull_kernel<kPullRows, KP, true, WV, RK>
+                : (const void*)eager_pull_kernel<kPullRows, KP, false, WV, RK>;
 }
 #ifndef FSTAMD_PULL_WAVES_SMALL  // A/B builds: waves per SIMD for blocks of <= 5 records
 #define FSTAMD_PULL_WAVES_SMALL 5
@@ -28,19 +29,26 @@ const void* pull_kernel_ptr(bool direct) {
 #ifndef FSTAMD_PULL_WAVES_F32  // A/B builds: the same with f32 cells (8-B cells, f32 merge)
 #define FSTAMD_PULL_WAVES_F32 6
 #endif
-template <bool F32>
+// ... and with the 8-B records: 7 waves (3 VGPRs spilled outside the layer loop) measured
+// 37.1 ms per 1M metric strings, 6 waves 37.7 ms, 8 waves (10 spilled) 38.9 ms
+#ifndef FSTAMD_PULL_WAVES_R8
+#define FSTAMD_PULL_WAVES_R8 7
+#endif
+template <int RK>
 const void* pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
-  constexpr int wv = F32 ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
+  constexpr int wv = RK == 2 ? FSTAMD_PULL_WAVES_R8 : RK ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
   switch (rv.kp) {
-    case 4: return pull_kernel_ptr<4, wv, F32>(dir);
-    case 5: return pull_kernel_ptr<5, wv, F32>(dir);
-    default: return pull_kernel_ptr<8, 4, F32>(dir);
+    case 4: return pull_kernel_ptr<4, wv, RK>(dir);
+    case 5: return pull_kernel_ptr<5, wv, RK>(dir);
+    default: return pull_kernel_ptr<8, 4, RK>(dir);
   }
 }
+// the 8-B records when the rhs has them (every weight an integer <= kRec8WMax)
+bool use_rec8(const RevView& rv) { return rv.rrec8 && !std::getenv("FSTAMD_NO_REC8"); }
 const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
-  return pull_f32(rhs, max_len) && !std::getenv("FSTAMD_P_F64") ? pull_kernel_for<true>(rhs.rev)
-                                                                 : pull_kernel_for<false>(rhs.rev);
+  if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64")) return pull_kernel_for<0>(rhs.rev);
+  return use_rec8(rhs.rev) ? pull_kernel_for<2>(rhs.rev) : pull_kernel_for<1>(rhs.rev);
 }
 // Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 5 with f32 cells (7.4 KB;
 // round 3: 4 at 10.2 KB) when every distance is an integer below 2^24.
@@ -48,25 +56,25 @@ const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
 #define FSTAMD_LP_WAVES_F32 5
 #endif
 constexpr int kLazyPullWaves = 3;
-template <int KP, bool F32>
+template <int KP, int RK>
 const void* lazy_pull_ptr(bool direct) {
-  constexpr int wv = (F32 && KP <= 5) ? FSTAMD_LP_WAVES_F32 : kLazyPullWaves;  // 8-record
-                                                                           // blocks spill at 4
-  return direct ? (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, F32>
-                : (const void*)lazy_pull_kernel<kPullRows, KP, false, wv, F32>;
+  constexpr int wv = (RK && KP <= 5) ? FSTAMD_LP_WAVES_F32 : kLazyPullWaves;  // 8-record
+                                                                          // blocks spill at 4
+  return direct ? (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, RK>
+                : (const void*)lazy_pull_kernel<kPullRows, KP, false, wv, RK>;
 }
-template <bool F32>
+template <int RK>
 const void* lazy_pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
   switch (rv.kp) {
-    case 4: return lazy_pull_ptr<4, F32>(dir);
-    case 5: return lazy_pull_ptr<5, F32>(dir);
-    default: return lazy_pull_ptr<8, F32>(dir);
+    case 4: return lazy_pull_ptr<4, RK>(dir);
+    case 5: return lazy_pull_ptr<5, RK>(dir);
+    default: return lazy_pull_ptr<8, RK>(dir);
   }
 }
 const void* lazy_pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
-  return lazy_pull_f32(rhs, max_len) ? lazy_pull_kernel_for<true>(rhs.rev)
-                                     : lazy_pull_kernel_for<false>(rhs.rev);
+  if (!lazy_pull_f32(rhs, max_len)) return lazy_pull_kernel_for<0>(rhs.rev);
+  return use_rec8(rhs.rev) ? lazy_pull_kernel_for<2>(rhs.rev) : lazy_pull_kernel_for<1>(rhs.rev);
 }
 }  // namespace
 
@@ -220,6 +228,12 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     else d->int_wmax = std::max(d->int_wmax, w);
   }
   std::vector<uint4> rrec32;
+  std::vector<uint2> rrec8;
+  if (d->int_wmax >= 0.0 && d->int_wmax <= kRec8WMax) {
+    rrec8.resize(rrec.size());
+    for (size_t r = 0; r < rrec.size(); ++r)
+      rrec8[r] = make_uint2(rrec[r].src, rrec[r].y | (uint32_t)rrec[r].weight);
+  }
   if (d->int_wmax >= 0.0) {
     rrec32.resize(rrec.size());
     for (size_t r = 0; r < rrec.size(); ++r) {
@@ -240,13 +254,14 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       !up(1, gtab.data(), gtab.size() * sizeof(uint4)) ||
       !up(2, rrec.data(), rrec.size() * sizeof(RevRec)) ||
       !up(3, rolab.data(), rolab.size() * sizeof(uint32_t)) ||
-      (!rrec32.empty() && !up(4, rrec32.data(), rrec32.size() * sizeof(uint4)))) {
+      (!rrec32.empty() && !up(4, rrec32.data(), rrec32.size() * sizeof(uint4))) ||
+      (!rrec8.empty() && !up(5, rrec8.data(), rrec8.size() * sizeof(uint2)))) {
     free_reverse_mirror(d);
     return false;
   }
   d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
-                   direct ? 1u : 0u, (const uint4*)d->rev_bufs[4]};
+                   direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5]};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;

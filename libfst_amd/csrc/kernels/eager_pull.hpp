@@ -109,6 +109,21 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const 
   rank_word = c.y;
   nd = __uint_as_float(c.x) + __uint_as_float(r.z);
 }
+// The same on the 8-B records {src, y | weight} (RevView::rrec8): the weight, an integer
+// <= 7, sits in y's low 3 bits, below the byte offset (a multiple of 8), so it rides in the
+// key's bits that never decide a comparison; y's bits 3..7 are zero, so the weight is
+// y's low byte
+__device__ __forceinline__ float rec8_weight(uint32_t y) { return (float)(y & 0xFFu); }
+template <int W>
+__device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const uint2& r,
+                                               uint32_t tmin8, uint32_t& pk, float& nd,
+                                               uint32_t& rank_word) {
+  const uint32_t off = min(r.x - tmin8, 8u * W);
+  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
+  pk = c.y | r.y | off;
+  rank_word = c.y;
+  nd = __uint_as_float(c.x) + rec8_weight(r.y);
+}
 
 // The in-arc group of target t for input label `lab`: the index of its first record and
 // its block count (nb = 0: no in-arc with that label).  rspan is padded past the last
@@ -145,17 +160,21 @@ __device__ __forceinline__ void pull_group(const RevView& rv, uint32_t lab, uint
 // DIRECT (RevView::direct): block 0 of target t is records [t * KP, t * KP + KP), loaded
 // together with rspan[t] (which then only confirms the label); otherwise the group is
 // looked up first (pull_group) and its records loaded after.
-// F32: cells and merge in f32, records from RevView::rrec32 -- chosen by the host when every
-// distance of the launch is an integer below 2^24 (pull_f32: integer arc weights, max_len *
-// max weight < 2^24), where every f32 sum, min and compare equals the f64 one.  Strings
-// longer than in.max_len (a caller's wrong bound) are handed on, so the bound always holds.
-template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, bool F32 = false>
+// RK (records): 0 RevRec, f64 cells; 1 and 2 (F32): cells and merge in f32, records from
+// RevView::rrec32 (1) or the 8-B RevView::rrec8 (2, weights <= 7) -- chosen by the host when
+// every distance of the launch is an integer below 2^24 (pull_f32: integer arc weights,
+// max_len * max weight < 2^24), where every f32 sum, min and compare equals the f64 one.
+// Strings longer than in.max_len (a caller's wrong bound) are handed on, so the bound
+// always holds.
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, int RK = 0>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
 eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                   unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
+  constexpr bool F32 = RK != 0;
   using DT = typename std::conditional<F32, float, double>::type;
-  using RT = typename std::conditional<F32, uint4, RevRec>::type;
+  using RT = typename std::conditional<RK == 2, uint2,
+                                       typename std::conditional<F32, uint4, RevRec>::type>::type;
   constexpr int kWords = PullLds<W, F32>::kWords;
   static_assert(KP <= 16, "m is 4 bits of the key");
   static_assert(W < 512, "8 * slot is 12 bits of the key, ranks 9 bits");
@@ -172,7 +191,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     }
   };
   auto rec = [&](uint32_t r) -> RT {
-    if constexpr (F32) return rv.rrec32[r];
+    if constexpr (RK == 2) return rv.rrec8[r];
+    else if constexpr (F32) return rv.rrec32[r];
     else return rv.rrec[r];
   };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
@@ -202,7 +222,12 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint2 h = hdr[k];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
-        if constexpr (F32) {
+        if constexpr (RK == 2) {
+          const uint2 r = rv.rrec8[b];
+          out.out_ol[jb.o + k] = rv.rolab[b];
+          out.out_w[jb.o + k] = (double)rec8_weight(r.y);  // exact: the f64 weight
+          src8 = r.x;
+        } else if constexpr (F32) {
           const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
           out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
@@ -332,7 +357,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         RT rr[KP];
         // one base address, the records at immediate offsets
         const RT* R;
-        if constexpr (F32) R = rv.rrec32 + rec0;
+        if constexpr (RK == 2) R = rv.rrec8 + rec0;
+        else if constexpr (F32) R = rv.rrec32 + rec0;
         else R = rv.rrec + rec0;
 #pragma unroll
         for (int m = 0; m < KP; ++m) rr[m] = R[m];

@@ -143,18 +143,24 @@ struct LazyPullLds {
   ChaseJob job[kLpChase];
 };
 
-template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, bool F32>
+// RK: the records, as in eager_pull_kernel (0 RevRec, 1 rrec32, 2 rrec8)
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, int RK>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
 lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                  unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
+  constexpr bool F32 = RK != 0;
   // DT: the distance type of cells and of the merge's arithmetic (f32: exact for the
   // integer distances below 2^24 the host checked)
   using DT = typename std::conditional<F32, float, double>::type;
-  // records: RevRec, or with f32 cells RevView::rrec32 {src, y, f32 weight, olabel}
-  using RT = typename std::conditional<F32, uint4, RevRec>::type;
+  // records: RevRec, or with f32 cells RevView::rrec32 {src, y, f32 weight, olabel} or
+  // RevView::rrec8 {src, y | weight}.  The keys carry y: with rrec8 the weight sits in their
+  // low 3 bits, so a cell offset taken from a key is masked with 0xFF8
+  using RT = typename std::conditional<RK == 2, uint2,
+                                       typename std::conditional<F32, uint4, RevRec>::type>::type;
   auto rec = [&](uint32_t r) -> RT {
-    if constexpr (F32) return rv.rrec32[r];
+    if constexpr (RK == 2) return rv.rrec8[r];
+    else if constexpr (F32) return rv.rrec32[r];
     else return rv.rrec[r];
   };
   auto r_src = [](const RT& r) -> uint32_t {
@@ -162,7 +168,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     else return r.src;
   };
   auto r_w = [](const RT& r) -> DT {
-    if constexpr (F32) return __uint_as_float(r.z);
+    if constexpr (RK == 2) return rec8_weight(r.y);
+    else if constexpr (F32) return __uint_as_float(r.z);
     else return r.weight;
   };
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
@@ -202,7 +209,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint2 h = hdr[k];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
-        if constexpr (F32) {
+        if constexpr (RK == 2) {
+          const uint2 r = rv.rrec8[b];
+          out.out_ol[jb.o + k] = rv.rolab[b];
+          out.out_w[jb.o + k] = (double)rec8_weight(r.y);  // exact: the f64 weight
+          src8 = r.x;
+        } else if constexpr (F32) {
           const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
           out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
@@ -345,7 +357,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         RT rr[KP];
         // one base address, the records at immediate offsets
         const RT* R;
-        if constexpr (F32) R = rv.rrec32 + rec0;
+        if constexpr (RK == 2) R = rv.rrec8 + rec0;
+        else if constexpr (F32) R = rv.rrec32 + rec0;
         else R = rv.rrec + rec0;
 #pragma unroll
         for (int m = 0; m < KP; ++m) rr[m] = R[m];
@@ -403,13 +416,13 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         const bool pres = ff < kLpAbsent;
         // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
-        const uint32_t ou = pres ? (ff & 0xFFFu) : 8u * W;
+        const uint32_t ou = pres ? (ff & 0xFF8u) : 8u * W;
         const DT du = CL.get_d(ou);
         const uint32_t pwu = CL.get_pw(ou);
         const uint32_t ruu = pwu & kLpRunMask;
         // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
         // round trip: its certificate alone usually settles C
-        const uint32_t ob = pres ? (c & 0xFFFu) : 8u * W;
+        const uint32_t ob = pres ? (c & 0xFF8u) : 8u * W;
         const uint32_t pwb = CL.get_pw(ob);
         const DT tx = du;
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
@@ -453,7 +466,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #endif
 #pragma unroll
           for (int m = 0; m < KP; ++m) {
-            const uint32_t o = bpk[m] & 0xFFFu;
+            const uint32_t o = bpk[m] & 0xFF8u;
             DT tbm = 0;
             if constexpr (!F32) tbm = CL.get_tb(o);
             cert |= nd[m] == b && ((bpk[m] & kRevPos) || certifies(CL.get_pw(o), tbm));

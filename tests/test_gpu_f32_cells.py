@@ -117,3 +117,18 @@ def test_understated_max_len_hands_longer_strings_on(sem):
         assert np.array_equal(ol[g], ref.olabels[a:b]), i
         assert np.array_equal(bits(w[g]), bits(ref.weights[a:b])), i
         assert bits(fin[i:i + 1])[0] == bits(ref.finals[i:i + 1])[0], i
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+@pytest.mark.parametrize("wmax", [7, 8])
+def test_record_widths_at_the_rec8_bound(sem, wmax, monkeypatch):
+    # integer weights <= 7 take the 8-B records (RevView::rrec8: the weight in y's low 3
+    # bits, riding in the candidate keys); 8 takes the 16-B rrec32.  Both, and the 16-B
+    # records forced (FSTAMD_NO_REC8), give the oracle's bits -- ties on purpose (half the
+    # weights are wmax, finals 0..4)
+    rng = np.random.default_rng(80 + wmax)
+    blob = O.freeze(banded_int_rhs(rng, 180, wmax))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 50)))] for _ in range(300)]
+    check(blob, *csr(seqs), sem)
+    monkeypatch.setenv("FSTAMD_NO_REC8", "1")
+    check(blob, *csr(seqs), sem)
