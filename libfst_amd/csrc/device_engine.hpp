@@ -91,6 +91,10 @@ struct RevView {
   // integer in [0, kRec8WMax] (it sits in y's low 3 bits, below the byte offset the keys OR
   // in), else null
   const uint2* rrec8;
+  // direct layout: rspan split for the row loads, {ilabel, nblocks} per state (8 B) and
+  // the record of its block 1 (read only for states with more than one block)
+  const uint2* rlab;
+  const uint32_t* rxrec;
 };
 constexpr double kRec8WMax = 7.0;
 
@@ -123,7 +127,7 @@ struct DeviceFst {
   // ... and one whose 128-tuple LDS size handed on over a third of a batch starts at 256
   mutable std::atomic<int> tiny_lazy_256{0}, tiny_eager_256{0};
   RevView rev{};
-  void* rev_bufs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  void* rev_bufs[8] = {};
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a
   // breadth-first renumbering of an rhs with scattered ids (device_engine.hip
   // bfs_renumbering).  Every device view (RhsView, RevView) uses it; results do not.

@@ -227,6 +227,16 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     if (!(w >= 0.0) || w != __builtin_trunc(w) || w >= 16777216.0) d->int_wmax = -1.0;
     else d->int_wmax = std::max(d->int_wmax, w);
   }
+  std::vector<uint2> rlab;
+  std::vector<uint32_t> rxrec;
+  if (direct) {
+    rlab.resize(rspan.size());
+    rxrec.resize(rspan.size());
+    for (size_t t = 0; t < rspan.size(); ++t) {
+      rlab[t] = make_uint2(rspan[t].z, rspan[t].y);
+      rxrec[t] = rspan[t].x;
+    }
+  }
   std::vector<uint4> rrec32;
   std::vector<uint2> rrec8;
   if (d->int_wmax >= 0.0 && d->int_wmax <= kRec8WMax) {
@@ -255,13 +265,16 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       !up(2, rrec.data(), rrec.size() * sizeof(RevRec)) ||
       !up(3, rolab.data(), rolab.size() * sizeof(uint32_t)) ||
       (!rrec32.empty() && !up(4, rrec32.data(), rrec32.size() * sizeof(uint4))) ||
-      (!rrec8.empty() && !up(5, rrec8.data(), rrec8.size() * sizeof(uint2)))) {
+      (!rrec8.empty() && !up(5, rrec8.data(), rrec8.size() * sizeof(uint2))) ||
+      (direct && (!up(6, rlab.data(), rlab.size() * sizeof(uint2)) ||
+                  !up(7, rxrec.data(), rxrec.size() * sizeof(uint32_t))))) {
     free_reverse_mirror(d);
     return false;
   }
   d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
-                   direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5]};
+                   direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5],
+                   (const uint2*)d->rev_bufs[6], (const uint32_t*)d->rev_bufs[7]};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;

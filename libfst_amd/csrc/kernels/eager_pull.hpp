@@ -342,15 +342,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rec0, nb, xrec = 0;
         uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
-          const uint4 rs = rv.rspan[t];
+          const uint2 rs = rv.rlab[t];  // {ilabel, nblocks}
           // block 0 holds the arcs of another label: shifting the window origin by 2^31
           // sends every source of the row past slot W (8 * state < 2^30), so the row
           // merges to "no tuple" with no per-result selects
-          const bool hit = rs.z == lab && lab < kSpanMixed;
+          const bool hit = rs.x == lab && lab < kSpanMixed;
           tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;
           rec0 = t * KP;
           nb = hit ? rs.y : 0u;
-          xrec = rs.x;
         } else {
           pull_group(rv, lab, t, rec0, nb);
         }
@@ -384,6 +383,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t ra = rec0 + ((c >> 13) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
+          if constexpr (DIRECT) xrec = nb > 1 ? rv.rxrec[t] : 0u;
           for (uint32_t x = 1;; ++x) {
             const bool act = nb > x;
             if (!__ballot(act)) break;

@@ -338,12 +338,11 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rec0, nb, xrec = 0;
         uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
-          const uint4 rs = rv.rspan[t];
-          const bool hit = rs.z == lab && lab < kSpanMixed;
+          const uint2 rs = rv.rlab[t];  // {ilabel, nblocks}
+          const bool hit = rs.x == lab && lab < kSpanMixed;
           tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;  // no in-arc of this label (tier P)
           rec0 = t * KP;
           nb = hit ? rs.y : 0u;
-          xrec = rs.x;
         } else {
           pull_group(rv, lab, t, rec0, nb);
         }
@@ -394,6 +393,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? bpk[m] : kEmptyKey);
         uint32_t ra = rec0 + ((c >> 13) & 15u);
         if (hubs) {  // the further blocks: first toucher, distance, back-pointer
+          // (block 1's record, loaded here: a branch before the row's record loads would
+          // hold them behind the label load)
+          if constexpr (DIRECT) xrec = nb > 1 ? rv.rxrec[t] : 0u;
           for (uint32_t x = 1;; ++x) {
             if (!__ballot(nb > x)) break;
             const uint32_t rxx = block_rec(x);
