@@ -524,6 +524,13 @@ static hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyK
   return hipStreamSynchronize(stream);
 }
 
+// Test knob: caps a persistent kernel's grid, so that each wave takes many strings and
+// keeps chase jobs pending across them (tests/test_gpu_lazy_pull.py, test_gpu_eager_pull.py)
+static uint32_t grid_cap(const char* env) {
+  const char* g = std::getenv(env);
+  return g && std::atoi(g) > 0 ? (uint32_t)std::atoi(g) : 0xFFFFFFFFu;
+}
+
 __global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_count,
                                     const int32_t* status, int32_t code, uint32_t* list,
                                     uint32_t* count);
@@ -650,6 +657,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     if (use_p) {
       grid_p = (uint32_t)std::min<uint64_t>((uint64_t)pull_waves_per_cu(rhs, in.max_len) * num_cus_,
                                             in.num_strings);
+      grid_p = std::min<uint32_t>(grid_p, grid_cap("FSTAMD_P_GRID"));
       while (grid_p > 1 && (uint64_t)grid_p * kChaseBatch * back_cap_w * 8 > (24ull << 30))
         grid_p /= 2;
       grid_p = std::max<uint32_t>(grid_p, 1);
@@ -1098,6 +1106,7 @@ hipError_t DeviceEngine::run_lazy_pull(const DeviceFst& rhs, const ChainInput& i
       (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * kPullW, 1u << 22);
   uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)lazy_pull_waves_per_cu(rhs, in.max_len) * num_cus_,
                                                in.num_strings);
+  grid = std::min<uint32_t>(grid, grid_cap("FSTAMD_LP_GRID"));
   while (grid > 1 && (uint64_t)grid * kChaseBatch * back_cap * 8 > (24ull << 30)) grid /= 2;
   grid = std::max<uint32_t>(grid, 1);
   uint2* back = (uint2*)scratch(kLpBack, (size_t)grid * kChaseBatch * back_cap * 8);

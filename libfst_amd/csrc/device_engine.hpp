@@ -95,6 +95,7 @@ struct RevView {
   // the record of its block 1 (read only for states with more than one block)
   const uint2* rlab;
   const uint32_t* rxrec;
+  uint32_t nrec;  // records (nblocks * kp)
 };
 constexpr double kRec8WMax = 7.0;
 

@@ -274,7 +274,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
                    direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5],
-                   (const uint2*)d->rev_bufs[6], (const uint32_t*)d->rev_bufs[7]};
+                   (const uint2*)d->rev_bufs[6], (const uint32_t*)d->rev_bufs[7],
+                   (uint32_t)(nblocks * kp)};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;

@@ -218,7 +218,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
-        const uint32_t b = sl[FB(id, lp.back_cap, 60)];
+        const uint32_t b = FB(sl[FB(id, lp.back_cap, 60)], rv.nrec, 63);
         const uint2 h = hdr[k];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;

@@ -205,7 +205,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
-        const uint32_t b = sl[FB(id, lp.back_cap, 70)];
+        const uint32_t b = FB(sl[FB(id, lp.back_cap, 70)], rv.nrec, 73);
         const uint2 h = hdr[k];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
@@ -719,12 +719,22 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             }
             wave_lds_sync();
           }
-          // exclusive prefix of the counts: lane l holds keys 4l .. 4l+3
-          const uint4 h = reinterpret_cast<const uint4*>(S.hist)[lane];
-          const uint32_t s4 = h.x + h.y + h.z + h.w;
-          const uint32_t ex = wave_incl_scan_dpp(s4) - s4;
-          reinterpret_cast<uint4*>(S.hist)[lane] =
-              make_uint4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
+          // exclusive prefix of the counts: lane l holds keys 4l .. 4l+3 (256 bins) or
+          // 2l, 2l+1 (128 bins, f32 cells) -- never past hist, which ends the union: the
+          // pending chase jobs follow it
+          static_assert(lp_bins<DT>() == 256 || lp_bins<DT>() == 128, "bins per lane");
+          if constexpr (lp_bins<DT>() == 256) {
+            const uint4 h = reinterpret_cast<const uint4*>(S.hist)[lane];
+            const uint32_t s4 = h.x + h.y + h.z + h.w;
+            const uint32_t ex = wave_incl_scan_dpp(s4) - s4;
+            reinterpret_cast<uint4*>(S.hist)[lane] =
+                make_uint4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
+          } else {
+            const uint2 h = reinterpret_cast<const uint2*>(S.hist)[lane];
+            const uint32_t s2 = h.x + h.y;
+            const uint32_t ex = wave_incl_scan_dpp(s2) - s2;
+            reinterpret_cast<uint2*>(S.hist)[lane] = make_uint2(ex, ex + h.x);
+          }
           wave_lds_sync();
 #pragma unroll
           for (int e = 0; e < EW; ++e) {  // pop rank -> the cell's high word

@@ -157,3 +157,15 @@ def test_wide_rhs_hands_strings_on(only_p):
     seqs = [[int(x) for x in rng.integers(1, 5, int(rng.integers(0, 14)))] for _ in range(64)]
     got, took = run_p(blob, seqs, expect_all=False)
     assert np.all((got.status[~took] == F.FST_PATH_OVERFLOW))
+
+
+@pytest.mark.parametrize("wmax", [3, 200])
+def test_many_strings_per_wave(only_p, wmax, monkeypatch):
+    # FSTAMD_P_GRID=3: three waves take every string (16 back slabs each, chased in
+    # batches), 8-B records (wmax 3) and 16-B ones (200)
+    monkeypatch.setenv("FSTAMD_P_GRID", "3")
+    rng = np.random.default_rng(4500 + wmax)
+    f = random_rhs(rng, 120, 500, 3, eps=False, wmax=wmax)
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 40)))] for _ in range(500)]
+    got, took = run_p(O.freeze(f), seqs, expect_all=False)
+    assert took.mean() > 0.5, took.mean()

@@ -172,3 +172,24 @@ def test_random_wide_layers(only_lp, seed):
     blob = O.freeze(f)
     seqs = [[int(x) for x in rng.integers(1, 3, int(rng.integers(0, 30)))] for _ in range(96)]
     run_lp(blob, seqs, expect_all=False)
+
+
+@pytest.mark.parametrize("sem_case", ["ties", "counting", "wide"])
+def test_many_strings_per_wave(only_lp, sem_case, monkeypatch):
+    # FSTAMD_LP_GRID=3: three waves take every string, so each wave holds up to 14 pending
+    # chase jobs (LazyPullLds::job, after the sort buffers) while it sorts later strings'
+    # layers -- a sort that wrote past its buffers would corrupt them (round 4: the f32
+    # cells' 128-bin counting sort wrote a 256-bin prefix)
+    monkeypatch.setenv("FSTAMD_LP_GRID", "3")
+    rng = np.random.default_rng(4242)
+    if sem_case == "ties":
+        f = random_rhs(rng, 40, 160, 3, eps=False, wmax=2)
+        seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 16)))] for _ in range(400)]
+    elif sem_case == "counting":
+        f = scaled_ambiguous(300, 1)
+        seqs = [[1] * int(L) for L in rng.integers(1, 70, 200)]
+    else:
+        f = scaled_ambiguous(300, 40)
+        seqs = [[1] * int(L) for L in rng.integers(1, 70, 200)]
+    got, took = run_lp(O.freeze(f), seqs, expect_all=False)
+    assert took.mean() > 0.5, took.mean()
