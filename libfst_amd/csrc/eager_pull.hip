@@ -246,12 +246,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   }
   if (d->int_wmax >= 0.0) {
     rrec32.resize(rrec.size());
-    for (size_t r = 0; r < rrec.size(); ++r) {
-      const float wf = (float)rrec[r].weight;  // exact: an integer below 2^24
-      uint32_t wb;
-      std::memcpy(&wb, &wf, 4);
-      rrec32[r] = make_uint4(rrec[r].src, rrec[r].y, wb, rolab[r]);
-    }
+    for (size_t r = 0; r < rrec.size(); ++r)  // the weight: an integer below 2^24
+      rrec32[r] = make_uint4(rrec[r].src, rrec[r].y, (uint32_t)rrec[r].weight, rolab[r]);
   }
   auto up = [&](int i, const void* src_p, size_t bytes) -> bool {
     if (bytes == 0) bytes = 16;

@@ -50,6 +50,21 @@
 namespace fstamd {
 
 constexpr uint32_t kPullAbsent = 0xFFFF0000u;  // rank word of a slot that holds no tuple
+// integer cells (the F32 kernels: every distance an integer below 2^24): the distance of a
+// slot with no tuple.  Far above every real distance, and a weight below 2^24 added to it
+// stays below 2^31, so a candidate from such a slot never wins and never wraps
+constexpr uint32_t kDistAbsent = 0x7F000000u;
+// +inf of the cells' distance type
+template <typename DT>
+__device__ __forceinline__ DT dist_inf() {
+  if constexpr (sizeof(DT) == 4) return (DT)kDistAbsent;
+  else return (DT)__builtin_huge_val();
+}
+template <typename DT>
+__device__ __forceinline__ DT dist_min(DT a, DT b) {
+  if constexpr (sizeof(DT) == 4) return min(a, b);
+  else return fmin(a, b);
+}
 
 
 template <int W, bool F32 = false>
@@ -66,12 +81,13 @@ struct PullLds {
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
 };
-// f32 cells (every distance an integer below 2^24, exact): one 8-B cell {f32 distance,
-// rank word} per slot, read by one ds_read_b64 per in-arc; 4.3 KB instead of 6.9 KB
+// integer cells (every distance an integer below 2^24; round 3 kept them as f32, round 4 as
+// u32, whose add takes the 8-B record's weight byte as an SDWA operand): one 8-B cell
+// {distance, rank word} per slot, read by one ds_read_b64 per in-arc; 4.3 KB instead of 6.9 KB
 template <int W>
 struct PullLds<W, true> {
   static constexpr int kWords = W * 8 / 64;
-  uint2 cell[W + 1];               // {f32 bits of the distance (+inf: no tuple), rank << 20}
+  uint2 cell[W + 1];               // {distance (kDistAbsent: no tuple), rank << 20}
   unsigned long long bits[kWords];
   uint4 pre[kWords];
   unsigned long long best;
@@ -97,32 +113,32 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec
   // stays +inf
   nd = d + r.weight;
 }
-// The same on f32 cells and the f32 record copy {src, y, f32 weight, olabel}: the sum of
-// two integers below 2^24 is exact, so it equals the f64 one.
+// The same on integer cells and the integer record copy {src, y, weight, olabel}: the
+// distances are integers below 2^24, so the u32 sum, min and compare equal the f64 ones.
 template <int W>
 __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const uint4& r,
-                                               uint32_t tmin8, uint32_t& pk, float& nd,
+                                               uint32_t tmin8, uint32_t& pk, uint32_t& nd,
                                                uint32_t& rank_word) {
   const uint32_t off = min(r.x - tmin8, 8u * W);
   const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
   pk = c.y | r.y | off;
   rank_word = c.y;
-  nd = __uint_as_float(c.x) + __uint_as_float(r.z);
+  nd = c.x + r.z;
 }
 // The same on the 8-B records {src, y | weight} (RevView::rrec8): the weight, an integer
 // <= 7, sits in y's low 3 bits, below the byte offset (a multiple of 8), so it rides in the
 // key's bits that never decide a comparison; y's bits 3..7 are zero, so the weight is
 // y's low byte
-__device__ __forceinline__ float rec8_weight(uint32_t y) { return (float)(y & 0xFFu); }
+__device__ __forceinline__ uint32_t rec8_weight(uint32_t y) { return y & 0xFFu; }
 template <int W>
 __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const uint2& r,
-                                               uint32_t tmin8, uint32_t& pk, float& nd,
+                                               uint32_t tmin8, uint32_t& pk, uint32_t& nd,
                                                uint32_t& rank_word) {
   const uint32_t off = min(r.x - tmin8, 8u * W);
   const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
   pk = c.y | r.y | off;
   rank_word = c.y;
-  nd = __uint_as_float(c.x) + rec8_weight(r.y);
+  nd = c.x + rec8_weight(r.y);  // (one v_add_u32 with a byte-0 SDWA operand)
 }
 
 // The in-arc group of target t for input label `lab`: the index of its first record and
@@ -172,7 +188,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                   unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
   constexpr bool F32 = RK != 0;
-  using DT = typename std::conditional<F32, float, double>::type;
+  using DT = typename std::conditional<F32, uint32_t, double>::type;  // (F32: integer cells)
   using RT = typename std::conditional<RK == 2, uint2,
                                        typename std::conditional<F32, uint4, RevRec>::type>::type;
   constexpr int kWords = PullLds<W, F32>::kWords;
@@ -180,11 +196,11 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   static_assert(W < 512, "8 * slot is 12 bits of the key, ranks 9 bits");
   __shared__ PullLds<W, F32> S;
   const uint32_t lane = threadIdx.x;
-  const DT kInf = (DT)__builtin_huge_val();
+  const DT kInf = dist_inf<DT>();
   // a cell: {distance, rank word}
   auto set_cell = [&](uint32_t i, DT d, uint32_t rw) {
     if constexpr (F32) {
-      S.cell[i] = make_uint2(__float_as_uint(d), rw);
+      S.cell[i] = make_uint2(d, rw);
     } else {
       S.d[i] = d;
       S.rk[i] = rw;
@@ -230,7 +246,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         } else if constexpr (F32) {
           const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
-          out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)r.z;  // exact: the f64 weight
           src8 = r.x;
         } else {
           const RevRec r = rv.rrec[b];
@@ -372,7 +388,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         for (int m = 0; m < KP; ++m) {
           pull_candidate<W>(S, rr[m], tmin8, pk[m], nd[m], rw[m]);
           f = min(f, pk[m]);
-          b = fmin(b, nd[m]);
+          b = dist_min(b, nd[m]);
         }
 #pragma unroll
         for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);

@@ -168,8 +168,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     else return r.src;
   };
   auto r_w = [](const RT& r) -> DT {
-    if constexpr (RK == 2) return rec8_weight(r.y);
-    else if constexpr (F32) return __uint_as_float(r.z);
+    if constexpr (RK == 2) return (float)rec8_weight(r.y);
+    else if constexpr (F32) return (float)r.z;  // (rrec32 holds the integer weight)
     else return r.weight;
   };
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
@@ -217,7 +217,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         } else if constexpr (F32) {
           const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
-          out.out_w[jb.o + k] = (double)__uint_as_float(r.z);  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)r.z;  // exact: the f64 weight
           src8 = r.x;
         } else {
           const RevRec r = rv.rrec[b];
