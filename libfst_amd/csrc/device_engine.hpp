@@ -96,6 +96,10 @@ struct RevView {
   const uint2* rlab;
   const uint32_t* rxrec;
   uint32_t nrec;  // records (nblocks * kp)
+  // [nblocks * kp] tier P's 4-B records (eager_pull.hip: the source as 8 * (target - source)
+  // + rbias8 in the high half, the key bits and weight in the low half), else null
+  const uint32_t* rrec4;
+  uint32_t rbias8;
 };
 constexpr double kRec8WMax = 7.0;
 
@@ -128,7 +132,7 @@ struct DeviceFst {
   // ... and one whose 128-tuple LDS size handed on over a third of a batch starts at 256
   mutable std::atomic<int> tiny_lazy_256{0}, tiny_eager_256{0};
   RevView rev{};
-  void* rev_bufs[8] = {};
+  void* rev_bufs[9] = {};
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a
   // breadth-first renumbering of an rhs with scattered ids (device_engine.hip
   // bfs_renumbering).  Every device view (RhsView, RevView) uses it; results do not.

@@ -37,7 +37,7 @@ const void* pull_kernel_ptr(bool direct) {
 template <int RK>
 const void* pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
-  constexpr int wv = RK == 2 ? FSTAMD_PULL_WAVES_R8 : RK ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
+  constexpr int wv = RK >= 2 ? FSTAMD_PULL_WAVES_R8 : RK ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
   switch (rv.kp) {
     case 4: return pull_kernel_ptr<4, wv, RK>(dir);
     case 5: return pull_kernel_ptr<5, wv, RK>(dir);
@@ -48,6 +48,8 @@ const void* pull_kernel_for(const RevView& rv) {
 bool use_rec8(const RevView& rv) { return rv.rrec8 && !std::getenv("FSTAMD_NO_REC8"); }
 const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
   if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64")) return pull_kernel_for<0>(rhs.rev);
+  if (rhs.rev.rrec4 && use_rec8(rhs.rev) && !std::getenv("FSTAMD_NO_REC4"))
+    return pull_kernel_for<3>(rhs.rev);
   return use_rec8(rhs.rev) ? pull_kernel_for<2>(rhs.rev) : pull_kernel_for<1>(rhs.rev);
 }
 // Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 5 with f32 cells (7.4 KB;
@@ -176,6 +178,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   if (nblocks * kp * sizeof(RevRec) > (4ull << 30) || nblocks * kp >= 0xFFFFFFFFull) return true;
 
   std::vector<RevRec> rrec(nblocks * kp, RevRec{0xFFFFFFF8u, 0u, 0.0});  // padding
+  std::vector<uint32_t> rtgt(nblocks * kp, 0u);  // each record's target state (rrec4)
   std::vector<uint32_t> rolab(nblocks * kp, 0u);
   // padded by kPullW entries: a window row may run past the last state
   std::vector<uint4> rspan((size_t)ns + kPullW, make_uint4(0u, 0u, kSpanNone, 0u));
@@ -210,6 +213,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
                             ((uint32_t)jpos[a] << 17) | (m << 13) | (pa[a].weight > 0.0 ? kRevPos : 0u),
                             pa[a].weight};
         rolab[slot] = pa[a].olabel;
+        rtgt[slot] = t;
       }
       blk += nb - (direct ? 1 : 0);
     }
@@ -244,6 +248,36 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     for (size_t r = 0; r < rrec.size(); ++r)
       rrec8[r] = make_uint2(rrec[r].src, rrec[r].y | (uint32_t)rrec[r].weight);
   }
+  // 4-B records for tier P: {8 * (t - source + bias) << 16 | j << 13 | m << 9 | pos << 8 |
+  // weight} -- the source as an offset from the target (every arc stays within the rhs's
+  // jump range), the key bits in the low half.  Padding: 0xFFFF0000 (an offset past every
+  // window).  Only with the 8-B records' weights (integers <= 7) and offsets below 2^13.
+  std::vector<uint32_t> rrec4;
+  uint32_t rbias8 = 0;
+  if (!rrec8.empty()) {
+    int64_t dlo = 0, dhi = 0;
+    for (size_t r = 0; r < rrec.size(); ++r) {
+      if (rrec[r].src == 0xFFFFFFF8u) continue;
+      const int64_t dl = (int64_t)rtgt[r] - (int64_t)(rrec[r].src >> 3);
+      dlo = std::min(dlo, dl);
+      dhi = std::max(dhi, dl);
+    }
+    if ((dhi - dlo) * 8 < 0xFFF0) {
+      rbias8 = (uint32_t)(-dlo * 8);
+      rrec4.resize(rrec.size());
+      for (size_t r = 0; r < rrec.size(); ++r) {
+        const uint32_t y = rrec[r].y;
+        const uint32_t low = (((y >> 17) & 7u) << 13) | (((y >> 13) & 15u) << 9) |
+                             (((y >> 12) & 1u) << 8) | (uint32_t)rrec[r].weight;
+        if (rrec[r].src == 0xFFFFFFF8u) {
+          rrec4[r] = 0xFFFF0000u;
+        } else {
+          const int64_t dl = (int64_t)rtgt[r] - (int64_t)(rrec[r].src >> 3);
+          rrec4[r] = ((uint32_t)((dl - dlo) * 8) << 16) | low;
+        }
+      }
+    }
+  }
   if (d->int_wmax >= 0.0) {
     rrec32.resize(rrec.size());
     for (size_t r = 0; r < rrec.size(); ++r)  // the weight: an integer below 2^24
@@ -263,7 +297,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       (!rrec32.empty() && !up(4, rrec32.data(), rrec32.size() * sizeof(uint4))) ||
       (!rrec8.empty() && !up(5, rrec8.data(), rrec8.size() * sizeof(uint2))) ||
       (direct && (!up(6, rlab.data(), rlab.size() * sizeof(uint2)) ||
-                  !up(7, rxrec.data(), rxrec.size() * sizeof(uint32_t))))) {
+                  !up(7, rxrec.data(), rxrec.size() * sizeof(uint32_t)))) ||
+      (!rrec4.empty() && !up(8, rrec4.data(), rrec4.size() * sizeof(uint32_t)))) {
     free_reverse_mirror(d);
     return false;
   }
@@ -271,7 +306,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
                    direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5],
                    (const uint2*)d->rev_bufs[6], (const uint32_t*)d->rev_bufs[7],
-                   (uint32_t)(nblocks * kp)};
+                   (uint32_t)(nblocks * kp), (const uint32_t*)d->rev_bufs[8], rbias8};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;

@@ -141,6 +141,23 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const 
   nd = c.x + rec8_weight(r.y);  // (one v_add_u32 with a byte-0 SDWA operand)
 }
 
+// The same on tier P's 4-B records (RevView::rrec4, RK 3): base8 = 8 * (target - window
+// origin) + rbias8 for this lane, the record's high half = 8 * (target - source) + rbias8,
+// so their difference is the source's cell offset (a wrap or a padding record's 0xFFFF
+// lands past slot W); the key keeps the record's low half (j << 13 | m << 9 | pos << 8 |
+// weight) under the rank word (rank << 16), and the weight is its low byte.  Each of the
+// three steps is one VALU with an SDWA operand, as with the 8-B records.
+template <int W>
+__device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const uint32_t& r,
+                                               uint32_t base8, uint32_t& pk, uint32_t& nd,
+                                               uint32_t& rank_word) {
+  const uint32_t off = min(base8 - (r >> 16), 8u * W);
+  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
+  pk = c.y | (r & 0xFFFFu);
+  rank_word = c.y;
+  nd = c.x + (r & 0xFFu);
+}
+
 // The in-arc group of target t for input label `lab`: the index of its first record and
 // its block count (nb = 0: no in-arc with that label).  rspan is padded past the last
 // state, so t may run past the window (such targets have no in-arc from the layer).
@@ -189,8 +206,15 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   constexpr int W = 64 * EW;
   constexpr bool F32 = RK != 0;
   using DT = typename std::conditional<F32, uint32_t, double>::type;  // (F32: integer cells)
-  using RT = typename std::conditional<RK == 2, uint2,
-                                       typename std::conditional<F32, uint4, RevRec>::type>::type;
+  using RT = typename std::conditional<
+      RK == 3, uint32_t,
+      typename std::conditional<RK == 2, uint2,
+                                typename std::conditional<F32, uint4, RevRec>::type>::type>::type;
+  // key layout: rank word rank << 20 over y = j << 17 | m << 13 (RK 3: rank << 16 over
+  // j << 13 | m << 9): the first key (rank << 3 | j) and m sit at these shifts
+  constexpr uint32_t kRankShift = RK == 3 ? 16 : 20;
+  constexpr uint32_t kFirstShift = kRankShift - 3;
+  constexpr uint32_t kMShift = kFirstShift - 4;
   constexpr int kWords = PullLds<W, F32>::kWords;
   static_assert(KP <= 16, "m is 4 bits of the key");
   static_assert(W < 512, "8 * slot is 12 bits of the key, ranks 9 bits");
@@ -207,7 +231,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     }
   };
   auto rec = [&](uint32_t r) -> RT {
-    if constexpr (RK == 2) return rv.rrec8[r];
+    if constexpr (RK == 3) return rv.rrec4[r];
+    else if constexpr (RK == 2) return rv.rrec8[r];
     else if constexpr (F32) return rv.rrec32[r];
     else return rv.rrec[r];
   };
@@ -231,6 +256,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     const uint32_t* sl = reinterpret_cast<const uint32_t*>(slabs + (size_t)lane * lp.back_cap);
     const uint2* hdr = slabs + (size_t)lane * lp.back_cap + lp.back_cap / 2;
     uint32_t id = jb.id;
+    uint32_t tcur = jb.pad;  // RK 3: the state of the tuple at slab position id
     for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
@@ -238,7 +264,13 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint2 h = hdr[k];
         out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
-        if constexpr (RK == 2) {
+        if constexpr (RK == 3) {
+          const uint32_t r = rv.rrec4[b];
+          out.out_ol[jb.o + k] = rv.rolab[b];
+          out.out_w[jb.o + k] = (double)(r & 0xFFu);  // exact: the f64 weight
+          tcur -= (uint32_t)(((int32_t)(r >> 16) - (int32_t)rv.rbias8) >> 3);  // the source
+          src8 = tcur << 3;
+        } else if constexpr (RK == 2) {
           const uint2 r = rv.rrec8[b];
           out.out_ol[jb.o + k] = rv.rolab[b];
           out.out_w[jb.o + k] = (double)rec8_weight(r.y);  // exact: the f64 weight
@@ -369,10 +401,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         } else {
           pull_group(rv, lab, t, rec0, nb);
         }
+        // RK 3: the records hold the source relative to the target, so the lane's base is
+        // 8 * (t - window origin) + rbias8 (the 2^31 shift of a miss applies the same)
+        if constexpr (RK == 3) tmin8 = (t << 3) - (tmin << 3) + rv.rbias8 + (tmin8 - (tmin << 3));
         RT rr[KP];
         // one base address, the records at immediate offsets
         const RT* R;
-        if constexpr (RK == 2) R = rv.rrec8 + rec0;
+        if constexpr (RK == 3) R = rv.rrec4 + rec0;
+        else if constexpr (RK == 2) R = rv.rrec8 + rec0;
         else if constexpr (F32) R = rv.rrec32 + rec0;
         else R = rv.rrec + rec0;
 #pragma unroll
@@ -396,7 +432,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
         }
-        uint32_t ra = rec0 + ((c >> 13) & 15u);
+        uint32_t ra = rec0 + ((c >> kMShift) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
           if constexpr (DIRECT) xrec = nb > 1 ? rv.rxrec[t] : 0u;
@@ -427,7 +463,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         bk[e] = c;
         bra[e] = ra;
         if (f < kPullAbsent) {  // a tuple: mark its first key (rank << 3 | j)
-          const uint32_t key = f >> 17;
+          const uint32_t key = f >> kFirstShift;
           atomicOr(&S.bits[key >> 6], 1ull << (key & 63u));
         }
       }
@@ -463,12 +499,12 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const bool pres = (uint32_t)e < rows_n && fst[e] < kPullAbsent;
         uint32_t rank = 0;
         if ((uint32_t)e < rows_n) {
-          const uint32_t key = pres ? fst[e] >> 17 : 0u;
+          const uint32_t key = pres ? fst[e] >> kFirstShift : 0u;
           const uint4 p = S.pre[key >> 6];
           const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
           rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
         }
-        set_cell(i, pres ? bd[e] : kInf, pres ? rank << 20 : kPullAbsent);
+        set_cell(i, pres ? bd[e] : kInf, pres ? rank << kRankShift : kPullAbsent);
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -534,6 +570,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       j.si = si;
       j.L = L;
       j.id = base + (bp & 511u);  // shortest-path.zig:109-136 starts at the best final
+      j.pad = tmin + (bp & 511u);  // (its state: RK 3's records hold sources relative to it)
       j.tuples = tuples;
       j.relax = relax;
       j.o = o;
