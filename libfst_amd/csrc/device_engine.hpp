@@ -91,10 +91,11 @@ struct RevView {
   // integer in [0, kRec8WMax] (it sits in y's low 3 bits, below the byte offset the keys OR
   // in), else null
   const uint2* rrec8;
-  // direct layout: rspan split for the row loads, {ilabel, nblocks} per state (8 B) and
-  // the record of its block 1 (read only for states with more than one block)
-  const uint2* rlab;
-  const uint32_t* rxrec;
+  // direct layout: rspan split for the row loads, ilabel | min(nblocks, 255) << 24 per
+  // state (4 B; labels below 2^24) and {the record of its block 1, nblocks} (read only for
+  // states with more than one block)
+  const uint32_t* rlab;
+  const uint2* rxrec;
   uint32_t nrec;  // records (nblocks * kp)
   // [nblocks * kp] tier P's 4-B records (eager_pull.hip: the source as 8 * (target - source)
   // + rbias8 in the high half, the key bits and weight in the low half), else null

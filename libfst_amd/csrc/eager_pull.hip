@@ -171,7 +171,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   // target row instead of two).  Further blocks follow the direct region.
   bool direct = !std::getenv("FSTAMD_PULL_INDIRECT");
   for (size_t g = 0; g < groups.size() && direct; ++g)
-    if ((g > 0 && groups[g].t == groups[g - 1].t) || groups[g].label >= kSpanMixed) direct = false;
+    if ((g > 0 && groups[g].t == groups[g - 1].t) || groups[g].label >= (1u << 24)) direct = false;
   const uint64_t ndirect = direct ? (uint64_t)ns + kPullW : 0;  // rows may run past the last state
   uint64_t nblocks = direct ? ndirect : 1;  // indirect: block 0 is the null block
   for (const Group& g : groups) nblocks += (g.n + kp - 1) / kp - (direct ? 1 : 0);
@@ -231,14 +231,16 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     if (!(w >= 0.0) || w != __builtin_trunc(w) || w >= 16777216.0) d->int_wmax = -1.0;
     else d->int_wmax = std::max(d->int_wmax, w);
   }
-  std::vector<uint2> rlab;
-  std::vector<uint32_t> rxrec;
+  // direct layout: per state one 4-B row word ilabel | min(nblocks, 255) << 24 (labels
+  // below 2^24, else the layout is indirect), and {block 1's record, nblocks} for hub rows
+  std::vector<uint32_t> rlab;
+  std::vector<uint2> rxrec;
   if (direct) {
     rlab.resize(rspan.size());
     rxrec.resize(rspan.size());
     for (size_t t = 0; t < rspan.size(); ++t) {
-      rlab[t] = make_uint2(rspan[t].z, rspan[t].y);
-      rxrec[t] = rspan[t].x;
+      rlab[t] = (rspan[t].z & 0xFFFFFFu) | (std::min<uint32_t>(rspan[t].y, 255u) << 24);
+      rxrec[t] = make_uint2(rspan[t].x, rspan[t].y);
     }
   }
   std::vector<uint4> rrec32;
@@ -296,8 +298,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       !up(3, rolab.data(), rolab.size() * sizeof(uint32_t)) ||
       (!rrec32.empty() && !up(4, rrec32.data(), rrec32.size() * sizeof(uint4))) ||
       (!rrec8.empty() && !up(5, rrec8.data(), rrec8.size() * sizeof(uint2))) ||
-      (direct && (!up(6, rlab.data(), rlab.size() * sizeof(uint2)) ||
-                  !up(7, rxrec.data(), rxrec.size() * sizeof(uint32_t)))) ||
+      (direct && (!up(6, rlab.data(), rlab.size() * sizeof(uint32_t)) ||
+                  !up(7, rxrec.data(), rxrec.size() * sizeof(uint2)))) ||
       (!rrec4.empty() && !up(8, rrec4.data(), rrec4.size() * sizeof(uint32_t)))) {
     free_reverse_mirror(d);
     return false;
@@ -305,7 +307,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   d->rev = RevView{(const uint4*)d->rev_bufs[0], (const uint4*)d->rev_bufs[1],
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
                    direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5],
-                   (const uint2*)d->rev_bufs[6], (const uint32_t*)d->rev_bufs[7],
+                   (const uint32_t*)d->rev_bufs[6], (const uint2*)d->rev_bufs[7],
                    (uint32_t)(nblocks * kp), (const uint32_t*)d->rev_bufs[8], rbias8};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");

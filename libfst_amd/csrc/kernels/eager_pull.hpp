@@ -390,14 +390,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rec0, nb, xrec = 0;
         uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
-          const uint2 rs = rv.rlab[t];  // {ilabel, nblocks}
+          const uint32_t rs = rv.rlab[t];  // ilabel | min(nblocks, 255) << 24
           // block 0 holds the arcs of another label: shifting the window origin by 2^31
           // sends every source of the row past slot W (8 * state < 2^30), so the row
           // merges to "no tuple" with no per-result selects
-          const bool hit = rs.x == lab && lab < kSpanMixed;
+          const bool hit = (rs & 0xFFFFFFu) == lab && lab < kSpanMixed;
           tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;
           rec0 = t * KP;
-          nb = hit ? rs.y : 0u;
+          nb = hit ? rs >> 24 : 0u;
         } else {
           pull_group(rv, lab, t, rec0, nb);
         }
@@ -435,7 +435,11 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t ra = rec0 + ((c >> kMShift) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
-          if constexpr (DIRECT) xrec = nb > 1 ? rv.rxrec[t] : 0u;
+          if constexpr (DIRECT) {  // block 1's record; the true count past 255 blocks
+            const uint2 xr = nb > 1 ? rv.rxrec[t] : make_uint2(0u, nb);
+            xrec = xr.x;
+            nb = xr.y;
+          }
           for (uint32_t x = 1;; ++x) {
             const bool act = nb > x;
             if (!__ballot(act)) break;

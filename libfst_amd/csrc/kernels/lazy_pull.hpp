@@ -338,11 +338,11 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rec0, nb, xrec = 0;
         uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
-          const uint2 rs = rv.rlab[t];  // {ilabel, nblocks}
-          const bool hit = rs.x == lab && lab < kSpanMixed;
+          const uint32_t rs = rv.rlab[t];  // ilabel | min(nblocks, 255) << 24
+          const bool hit = (rs & 0xFFFFFFu) == lab && lab < kSpanMixed;
           tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;  // no in-arc of this label (tier P)
           rec0 = t * KP;
-          nb = hit ? rs.y : 0u;
+          nb = hit ? rs >> 24 : 0u;
         } else {
           pull_group(rv, lab, t, rec0, nb);
         }
@@ -395,7 +395,11 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if (hubs) {  // the further blocks: first toucher, distance, back-pointer
           // (block 1's record, loaded here: a branch before the row's record loads would
           // hold them behind the label load)
-          if constexpr (DIRECT) xrec = nb > 1 ? rv.rxrec[t] : 0u;
+          if constexpr (DIRECT) {  // block 1's record; the true count past 255 blocks
+            const uint2 xr = nb > 1 ? rv.rxrec[t] : make_uint2(0u, nb);
+            xrec = xr.x;
+            nb = xr.y;
+          }
           for (uint32_t x = 1;; ++x) {
             if (!__ballot(nb > x)) break;
             const uint32_t rxx = block_rec(x);
