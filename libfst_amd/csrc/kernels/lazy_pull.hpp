@@ -182,6 +182,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #endif
   const uint32_t lane = threadIdx.x;
   const DT kInf = (DT)__builtin_huge_val();
+  // min of two distances >= +0 (no NaN: finite weights): on f32, the integer min of the
+  // bit patterns (one v_min_u32, no NaN quieting of the operands)
+  auto lp_dmin = [](DT x, DT y) -> DT {
+    if constexpr (F32) return __uint_as_float(min(__float_as_uint(x), __float_as_uint(y)));
+    else return fmin(x, y);
+  };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;
 
@@ -372,7 +378,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             nd[m] = CL.get_d(o) + r_w(rr[m]);  // times(d, w) for finite w >= 0 (:108)
             bpk[m] = CL.get_idw(o) | rr[m].y | o;
             ff = min(ff, bpk[m]);
-            b = fmin(b, nd[m]);
+            b = lp_dmin(b, nd[m]);
           }
         } else {
 #pragma unroll
@@ -381,7 +387,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             nd[m] = CL.get_d(o) + r_w(rr[m]);
             bpk[m] = CL.get_idw(o) | rr[m].y | o;
             ff = min(ff, (CL.get_pw(o) & kLpAbsent) | rr[m].y | o);
-            b = fmin(b, nd[m]);
+            b = lp_dmin(b, nd[m]);
           }
         }
         if (want_work) {  // (one uniform branch per row; an absent source's key >= kLpAbsent)
@@ -454,6 +460,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const uint32_t rbb = pwb & kLpRunMask;
           fast = !pres || (c & kRevPos) || tbb < tx || (tbb == tx && rbb < rx);
         }
+        // the lanes whose back arc does not certify them, as SALU ANDs of compare masks (a
+        // ballot of the OR-ed predicate costs two VALU to materialise it)
+        auto lanes_without = [](bool pr, uint32_t cc, uint32_t pwbb, uint32_t ck,
+                                bool fst_) -> unsigned long long {
+          if constexpr (F32)
+            return __ballot(pr) & ~__ballot((cc & kRevPos) != 0u) &
+                   ~__ballot((pwbb & kLpCkeyMask) < ck);
+          else return __ballot(!fst_);
+        };
         auto certifies = [&](uint32_t pw_src, DT tb_src) -> bool {  // a tight 0-weight source
           if constexpr (F32) return (pw_src & kLpCkeyMask) < ckx;
           else return tb_src < tx || (tb_src == tx && (pw_src & kLpRunMask) < rx);
@@ -463,7 +478,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #elif defined(FSTAMD_LP_FULLCERT)  // A/B: the full loop on every row that needs it
         if (check_c && __ballot(pres && (!(c & kRevPos) || nb > 1))) {
 #else
-        if (check_c && __ballot(!fast)) {
+        if (check_c && lanes_without(pres, c, pwb, ckx, fast)) {
 #endif
 #ifdef FSTAMD_LP_FULLCERT
           bool cert = !pres || (c & kRevPos);
