@@ -363,15 +363,17 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // ---- window of the next layer: every target of a state in [cmin, cmax] lies in
       // [cmin - jump_back, cmax + jump_fwd] (RhsView) ----
       const uint32_t tn = cmin >= rhs.jump_back ? cmin - rhs.jump_back : 0u;
-      const uint64_t hi = min((uint64_t)cmax + rhs.jump_fwd, (uint64_t)rhs.num_states - 1);
+      // (32-bit: the pull tiers take rhs of fewer than 2^27 states, so cmax + jump_fwd
+      // cannot wrap, and the compares stay scalar -- u64 ones went to the VALU)
+      const uint32_t hi = min(cmax + rhs.jump_fwd, rhs.num_states - 1);
       const uint32_t nbase = base + wk;
       // (the slab's second half holds one header entry per layer: k < back_cap / 2)
-      if (hi - tn >= (uint64_t)W || (uint64_t)nbase + (hi - tn + 1) > lp.back_cap ||
+      if (hi - tn >= (uint32_t)W || nbase + (hi - tn + 1) > lp.back_cap ||
           k >= lp.back_cap / 2) {
         fail = kPathOverflow;  // the push tiers take the string
         break;
       }
-      const uint32_t wn = (uint32_t)(hi - tn) + 1;
+      const uint32_t wn = hi - tn + 1;
       const uint32_t rows_n = (wn + 63) / 64;
 
       // ---- (P1) pull: every target slot of the window merges its in-arcs ----
