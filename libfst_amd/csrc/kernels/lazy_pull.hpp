@@ -430,13 +430,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         const bool pres = ff < kLpAbsent;
         // the first toucher's cell: tb(x) = d(u*), run(x) = 1 + run(u*) if tb(u*) == tb(x)
-        const uint32_t ou = pres ? (ff & 0xFF8u) : 8u * W;
+        // (no select for absent lanes: their keys' offsets are in-bounds LDS addresses too,
+        // and nothing they read is used)
+        const uint32_t ou = ff & 0xFF8u;
         const DT du = CL.get_d(ou);
         const uint32_t pwu = CL.get_pw(ou);
         const uint32_t ruu = pwu & kLpRunMask;
         // the back-pointer source's cell (a tight in-neighbour), read in the same LDS
         // round trip: its certificate alone usually settles C
-        const uint32_t ob = pres ? (c & 0xFF8u) : 8u * W;
+        const uint32_t ob = c & 0xFF8u;
         const uint32_t pwb = CL.get_pw(ob);
         const DT tx = du;
         // C: a tight in-arc of positive weight pops before x; else a tight 0-weight
@@ -514,8 +516,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         bk[e] = c;
         bra[e] = ra;
         if constexpr (F32) {
-          fst[e] = ff < kLpAbsent ? (ff & ~0x1FFFFu) | rx : ff;
-          bdp[e] = ff < kLpAbsent ? (uint32_t)b | ((ckx >> kLpCfShift) << 24) : 0u;
+          // (an absent lane keeps ff's high bits, >= kLpAbsent; its bdp is never read)
+          fst[e] = (ff & ~0x1FFFFu) | rx;
+          bdp[e] = (uint32_t)b | ((ckx >> kLpCfShift) << 24);
         } else {
           fst[e] = ff;
           bd[e] = b;
