@@ -95,6 +95,20 @@ struct PullLds<W, true> {
   ChaseJob job[kChaseBatch];
 };
 
+// The back key: the smallest key among the tight candidates (nd == b), as selects then a
+// tree of 3-input mins (v_min3_u32) -- the running min(c, tight ? key : ~0) compiles to a
+// compare, a min and a select per candidate (the lazy pull uses it)
+template <int KP, typename DT>
+__device__ __forceinline__ uint32_t tight_min(const DT (&nd)[KP], DT b, const uint32_t (&pk)[KP]) {
+  uint32_t t[KP];
+#pragma unroll
+  for (int m = 0; m < KP; ++m) t[m] = nd[m] == b ? pk[m] : 0xFFFFFFFFu;
+  uint32_t c = t[0];
+#pragma unroll
+  for (int m = 1; m < KP; m += 2) c = m + 1 < KP ? min(min(c, t[m]), t[m + 1]) : min(c, t[m]);
+  return c;
+}
+
 // One in-arc record against the current layer's cells: its candidate key and distance.
 template <int W>
 __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec& r,
@@ -428,6 +442,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           f = min(f, pk[m]);
           b = dist_min(b, nd[m]);
         }
+        // (tight_min's select-then-min3 tree measured 0.5 % slower here, 0.6 % faster in
+        // the lazy pull)
 #pragma unroll
         for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
         if (want_work) {

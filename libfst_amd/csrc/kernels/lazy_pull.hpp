@@ -396,9 +396,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(bpk[m] < kLpAbsent));
         }
-        uint32_t c = kEmptyKey;
-#pragma unroll
-        for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? bpk[m] : kEmptyKey);
+        uint32_t c = tight_min<KP>(nd, b, bpk);
         uint32_t ra = rec0 + ((c >> 13) & 15u);
         if (hubs) {  // the further blocks: first toucher, distance, back-pointer
           // (block 1's record, loaded here: a branch before the row's record loads would
