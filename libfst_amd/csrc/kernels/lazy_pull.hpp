@@ -525,7 +525,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         if (pres) {
           const uint32_t key = ff >> 17;  // pop rank << 3 | j
-          atomicOr(&S.bits[key >> 6], 1ull << (key & 63u));
+          // (a 32-bit OR into the word's half: ~4 lanes of a row share an address instead
+          // of ~8, and same-address LDS atomics serialise -- they were all of the kernel's
+          // LDS conflict cycles)
+          atomicOr(reinterpret_cast<uint32_t*>(S.bits) + (key >> 5), 1u << (key & 31u));
         }
       }
       wave_lds_sync();
