@@ -541,7 +541,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       const uint32_t inc = wave_incl_scan_dpp(pc);
       const uint32_t n_next = __builtin_amdgcn_readlane(inc, 63);
       if (lane < nw) {
-        S.pre[lane] = make_uint4(inc - pc, 0u, (uint32_t)word, (uint32_t)(word >> 32));
+        // per 32-bit half: {popcount of the keys before it, its bits}, so P3's lookup is one
+        // 32-bit mask and count
+        S.pre[lane] = make_uint4(inc - pc, (uint32_t)word,
+                                 inc - pc + (uint32_t)__popc((uint32_t)word), (uint32_t)(word >> 32));
         S.bits[lane] = 0;
       }
       wave_lds_sync();
@@ -570,9 +573,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rank = 0;
         if ((uint32_t)e < rows_n) {
           const uint32_t key = pres ? fst[e] >> 17 : 0u;
-          const uint4 p = S.pre[key >> 6];
-          const unsigned long long w64 = ((unsigned long long)p.w << 32) | p.z;
-          rank = p.x + (uint32_t)__popcll(w64 & ((1ull << (key & 63u)) - 1ull));
+          const uint2 p = reinterpret_cast<const uint2*>(S.pre)[key >> 5];
+          rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
         }
         // pop rank: identity until the sort below fills it in
         DT dx;
