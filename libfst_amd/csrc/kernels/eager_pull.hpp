@@ -109,6 +109,14 @@ __device__ __forceinline__ uint32_t tight_min(const DT (&nd)[KP], DT b, const ui
   return c;
 }
 
+// A load at a 32-bit byte offset from a kernel-argument base: global_load's SGPR-base +
+// VGPR-offset form, no 64-bit address arithmetic per lane (the caller guarantees the
+// offset fits: tables of < 4 GB)
+template <typename T>
+__device__ __forceinline__ const T* at_byte(const T* base, uint32_t byte_off) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 // One in-arc record against the current layer's cells: its candidate key and distance.
 template <int W>
 __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec& r,
@@ -406,7 +414,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rec0, nb, xrec = 0;
         uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
-          const uint32_t rs = rv.rlab[t];  // ilabel | min(nblocks, 255) << 24
+          const uint32_t rs = *at_byte(rv.rlab, t * 4u);  // ilabel | min(nblocks, 255) << 24
           // block 0 holds the arcs of another label: shifting the window origin by 2^31
           // sends every source of the row past slot W (8 * state < 2^30), so the row
           // merges to "no tuple" with no per-result selects
@@ -423,8 +431,9 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         RT rr[KP];
         // one base address, the records at immediate offsets
         const RT* R;
-        if constexpr (RK == 3) R = rv.rrec4 + rec0;
-        else if constexpr (RK == 2) R = rv.rrec8 + rec0;
+        // (RK 2, 3: the byte offset in 32 bits -- fewer than 2^28 records, eager_pull.hip)
+        if constexpr (RK == 3) R = at_byte(rv.rrec4, rec0 * 4u);
+        else if constexpr (RK == 2) R = at_byte(rv.rrec8, rec0 * 8u);
         else if constexpr (F32) R = rv.rrec32 + rec0;
         else R = rv.rrec + rec0;
 #pragma unroll

@@ -346,7 +346,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rec0, nb, xrec = 0;
         uint32_t tmin8 = tmin << 3;
         if constexpr (DIRECT) {
-          const uint32_t rs = rv.rlab[t];  // ilabel | min(nblocks, 255) << 24
+          const uint32_t rs = *at_byte(rv.rlab, t * 4u);  // ilabel | min(nblocks, 255) << 24
           const bool hit = (rs & 0xFFFFFFu) == lab && lab < kSpanMixed;
           tmin8 = hit ? tmin8 : tmin8 + 0x80000000u;  // no in-arc of this label (tier P)
           rec0 = t * KP;
@@ -364,7 +364,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         RT rr[KP];
         // one base address, the records at immediate offsets
         const RT* R;
-        if constexpr (RK == 2) R = rv.rrec8 + rec0;
+        if constexpr (RK == 2) R = at_byte(rv.rrec8, rec0 * 8u);  // (32-bit byte offset)
         else if constexpr (F32) R = rv.rrec32 + rec0;
         else R = rv.rrec + rec0;
 #pragma unroll
