@@ -540,14 +540,16 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const uint2 p = reinterpret_cast<const uint2*>(S.pre)[key >> 5];
           rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
         }
-        set_cell(i, pres ? bd[e] : kInf, pres ? rank << kRankShift : kPullAbsent);
+        // (an absent slot keeps its merged distance, +inf or >= kDistAbsent: no select; the
+        // rank word alone marks it absent)
+        set_cell(i, bd[e], pres ? rank << kRankShift : kPullAbsent);
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          back[FB(nbase + i, lp.back_cap, 61)] = bra[e];
+          *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 61) * 4u)) = bra[e];
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];

@@ -598,7 +598,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          back[FB(nbase + i, lp.back_cap, 71)] = bra[e];
+          *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 71) * 4u)) = bra[e];
           if (last) {  // best final: lexmin (total, id) (compose-shortest-path.zig:165-179)
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 72)];
