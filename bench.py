@@ -39,41 +39,44 @@ CLOCK_GHZ = 2.4
 VALU_PEAK_GCYC = SIMDS * CLOCK_GHZ   # G SIMD-cycles/s
 # Measured HBM traffic of the metric kernel: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 # over this same command (scripts/profile_bench.sh), reduced by scripts/pmc_summary.py.
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+TRAFFIC_FILES = {1: os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                 0: os.path.join(REPO, "profiles", "pmc_traffic_lazy.json")}
 # SQ instruction mix of the metric kernel (scripts/sq_counters.sh + sq_summary.py --json):
 # the kernel's real bound is VALU issue, not bytes
-ISSUE_FILE = os.path.join(REPO, "profiles", "sq_issue.json")
+ISSUE_FILES = {1: os.path.join(REPO, "profiles", "sq_issue.json"),
+               0: os.path.join(REPO, "profiles", "sq_issue_lazy.json")}
 L2_PEAK_GBS = 34500.0  # MI355X aggregate L2 (MI355X_MICROARCH.md "L2 (per XCD)")
 
 
 EAGER_KERNEL = "eager_pull_kernel"     # tier P, takes every metric string
 LAZY_KERNEL = "lazy_pull_kernel"
+KERNELS = {1: EAGER_KERNEL, 0: LAZY_KERNEL}
 
 
 def measured_traffic(args, sem):
     """Per-launch HBM bytes from the committed PMC summary (metric config only), else None.
     The summary must name the kernel this run times (a stale file gives None)."""
-    if sem != F.FST_SEM_EAGER or (args.len, args.transducer_len, args.branches) != (64, 4096, 12):
+    if (args.len, args.transducer_len, args.branches) != (64, 4096, 12):
         return None, None
     try:
-        t = json.load(open(TRAFFIC_FILE))
+        t = json.load(open(TRAFFIC_FILES[sem]))
     except (OSError, ValueError):
         return None, None
-    if t.get("kernel") != EAGER_KERNEL:
+    if t.get("kernel") != KERNELS[sem]:
         return None, None
-    return t["traffic_per_string"] * args.batch, t.get("source", TRAFFIC_FILE)
+    return t["traffic_per_string"] * args.batch, t.get("source", TRAFFIC_FILES[sem])
 
 
 def issue_profile(args, sem):
     """SQ instruction mix of the eager metric kernel (committed summary of rocprofv3 --pmc
     SQ_* passes over this command at 65,536 strings), or None for another workload."""
-    if sem != F.FST_SEM_EAGER or (args.len, args.transducer_len, args.branches) != (64, 4096, 12):
+    if (args.len, args.transducer_len, args.branches) != (64, 4096, 12):
         return None
     try:
-        t = json.load(open(ISSUE_FILE))
+        t = json.load(open(ISSUE_FILES[sem]))
     except (OSError, ValueError):
         return None
-    if t.get("kernel") != EAGER_KERNEL:
+    if t.get("kernel") != KERNELS[sem]:
         return None
     return t
 
@@ -116,7 +119,7 @@ def roofline_block(args, sem, avg_k_ms, balg, work, lengths, plen, traffic, traf
                     "valu_busy_cycles_per_string": busy_cyc,
                     "salu_insts_per_string": ps.get("SQ_INSTS_SALU"),
                     "lds_insts_per_string": ps.get("SQ_INSTS_LDS"),
-                    "issue_source": sq.get("source", ISSUE_FILE)})
+                    "issue_source": sq.get("source", ISSUE_FILES[sem])})
     elif hbm is not None:
         blk.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": hbm["frac"]})
@@ -132,7 +135,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+    p.add_argument("--scaling", choices=["strong", "weak"], default="weak",
                    help="strong: --global-batch strings per step split over the ranks (the "
                         "metric's batch=1M at 1/2/4/8 GPUs); weak: --batch strings per rank")
     p.add_argument("--global-batch", type=int, default=1 << 20,
@@ -151,7 +154,8 @@ def parse():
     p.add_argument("--no-varied", dest="varied", action="store_false",
                    help="skip the varied batch (lengths 1..len, 10%% dead strings)")
     p.add_argument("--no-e2e", dest="e2e", action="store_false",
-                   help="skip the end-to-end host-API rate (H2D + kernels + D2H)")
+                   help="profiling runs only: skip the host-entry headline (value is then the "
+                        "kernel-resident rate, and the line says so)")
     p.add_argument("--lazy-batch", type=int, default=-1,
                    help="also time the lazy engine on this many metric strings "
                         "(-1 = the eager batch size, 0 = off)")
@@ -383,33 +387,92 @@ def leg(batch, rhs, sem, dev_index, world, total_per_step, blob, env=None, steps
             "checked_vs_oracle": check_sample(batch, blob, sem)}
 
 
-def end_to_end(args, rhs, sem, dev_index, steps=3, warmup=1):
-    """The host batch entry fst_compose_frozen_shortest_path_batch on the metric batch: host
-    labels in, H2D, kernels, device CSR compaction, D2H into pooled pinned host arrays,
-    results out (SURVEY 8(d) wall time).  Per-GPU rate of one process."""
-    L, B = args.len, args.batch
-    labels = np.ones(B * L, np.uint32)
-    offsets = np.arange(B + 1, dtype=np.uint64) * L
+def host_timed(rhs, sem, dev_index, labels, offsets, steps, warmup, world):
+    """Timed steps of the host batch entry fst_compose_frozen_shortest_path_batch: host
+    labels in, H2D, kernels, D2H into the library's pinned result arrays, result out --
+    SURVEY 8(d)'s wall time (bench/optimize-bench.zig:416-453 times the whole call).
+    Barrier + synchronize on both sides, max over ranks.  Returns the last step's result."""
+    def run():
+        return F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, dev_index)
     for _ in range(warmup):
-        r = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, dev_index)
+        r = run()
         del r
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kms = []
+    r = None
     t0 = time.perf_counter()
     for _ in range(steps):
-        r = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, dev_index)
-        assert r.status[0] == F.FST_PATH_OK and int(r.offsets[-1]) == B * L
-        del r
+        r = None          # the previous result goes back to the pinned pool first
+        r = run()
+        kms.append(F.last_launch_stats().kernel_ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return {"value": B * steps / el, "unit": "strings/s", "ms_per_call": el / steps * 1e3,
-            "calls": steps, "strings_per_call": B,
-            "bytes_in_per_call": int(labels.nbytes + offsets.nbytes),
-            "note": "fst_compose_frozen_shortest_path_batch: host arrays -> H2D -> kernels -> "
-                    "device CSR compaction -> D2H (pinned) -> result, one GPU"}
+    if world > 1:
+        el = max_over_ranks(el, dev_index)
+    return el, kms, r
+
+
+def check_host_result(r, labels, offsets, blob_bytes, sem, n=256):
+    """Bit-compares the first n strings of a host BatchResult with the oracle (checker)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ffi as O  # checker only
+
+    n = min(n, len(offsets) - 1)
+    offs = np.asarray(offsets[: n + 1], np.uint64)
+    ref = O.batch_run(blob_bytes, np.asarray(labels[: int(offs[-1])], np.uint32), offs,
+                      1 if sem == F.FST_SEM_EAGER else 0, 1, 1)
+    exp = np.where(ref.empty == 1, F.FST_PATH_EMPTY, F.FST_PATH_OK)
+    assert np.all(ref.status == O.OR_OK) and np.array_equal(r.status[:n], exp), "status"
+    a, b = int(r.offsets[0]), int(r.offsets[n])
+    assert np.array_equal(r.offsets[: n + 1] - r.offsets[0], ref.offsets), "path offsets"
+    assert np.array_equal(r.ilabels[a:b], ref.ilabels), "ilabels"
+    assert np.array_equal(r.olabels[a:b], ref.olabels), "olabels"
+    assert np.array_equal(r.weights[a:b].view(np.uint64), ref.weights.view(np.uint64)), "w"
+    ok = exp == F.FST_PATH_OK
+    assert np.array_equal(r.finals[:n][ok].view(np.uint64), ref.finals[ok].view(np.uint64))
+    return int(n)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start torchrun with N ranks (one per GPU) as
+    a CHILD process -- before this process touches the GPU, never exec -- and hand back its
+    exit code.  Its ranks inherit stdout, so rank 0's JSON line is this command's output."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port",
+           str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if os.environ.get("FSTAMD_BENCH_DRY_LAUNCH"):  # tests (CPU): the command only
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    # rank topology first, before anything touches the GPU (launch_ranks runs a child)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one GPU per rank; ranks beyond the visible devices share them (gloo tests only)
@@ -440,32 +503,55 @@ def main():
         buf = torch.frombuffer(bytearray(blob_host), dtype=torch.uint8).to(dev)
     rhs = D.adopt_on_device(buf, local)
     del buf
+    blob_check = blob_host if blob_host is not None else D.blob_bytes(
+        F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, args.transducer_len, args.branches))
 
     L = args.len
     lengths = np.full(args.batch, L, np.int64)
-    batch = DeviceBatch(lengths, lambda t: torch.ones(t, dtype=torch.int32), dev)
-    el, kms, st = timed(batch, rhs, sem, local, args.steps, args.warmup, world)
 
-    # correctness of the last timed step: every metric string has one answer, and a fixed
-    # sample is bit-compared with the oracle
+    # ---- headline: the host entry, host arrays in and out (SURVEY 8(d) wall time) ----
+    h_labels = np.ones(args.batch * L, np.uint32)          # the caller's (pageable) arrays
+    h_offsets = np.arange(args.batch + 1, dtype=np.uint64) * L
+    if args.e2e:
+        el, hkms, res = host_timed(rhs, sem, local, h_labels, h_offsets, args.steps,
+                                   args.warmup, world)
+        assert np.all(res.status == F.FST_PATH_OK), np.unique(res.status, return_counts=True)
+        assert int(res.offsets[-1]) == args.batch * L
+        checked = check_host_result(res, h_labels, h_offsets, blob_check, sem)
+        del res
+
+    # ---- kernel-only: the same strings device-resident (fst_device_compose_shortest_path) --
+    batch = DeviceBatch(lengths, lambda t: torch.ones(t, dtype=torch.int32), dev)
+    kel, kms, st = timed(batch, rhs, sem, local, args.steps, args.warmup, world)
     status = batch.status.cpu().numpy()
     plen = batch.plen.cpu().numpy().astype(np.int64)
     assert np.all(status == F.FST_PATH_OK), np.unique(status, return_counts=True)
     assert np.all(plen == L)
-    blob_check = blob_host if blob_host is not None else D.blob_bytes(
-        F.Fst.bench_transducer(F.BENCH_AMBIGUOUS, args.transducer_len, args.branches))
-    checked = check_sample(batch, blob_check, sem)
+    kchecked = check_sample(batch, blob_check, sem)
     # one untimed run with the per-string work counters (B_alg of the roofline)
     batch.run(rhs, sem, local, torch.cuda.current_stream().cuda_stream, work=True)
     torch.cuda.synchronize()
     work = batch.work.cpu().numpy().astype(np.int64)
-
-    total_strings = total_per_step * args.steps
-    value = total_strings / el
     avg_k = float(np.mean(kms))
     balg = b_alg_bytes(work, lengths, plen)   # bytes per launch on this rank
+    if not args.e2e:  # (profiling runs) the headline falls back to the kernel-resident rate
+        el, hkms, checked = kel, kms, kchecked
+    value = total_per_step * args.steps / el
+    extra = {"value_kernel": total_per_step * args.steps / kel,
+             "kernel_resident": {
+                 "value": total_per_step * args.steps / kel,
+                 "ms_per_step": kel / args.steps * 1e3, "kernel_ms": avg_k,
+                 "checked_vs_oracle": kchecked,
+                 "note": "fst_device_compose_shortest_path on device-resident labels/outputs: "
+                         "kernels only, no host copies (the roofline's kernel)"},
+             "end_to_end": None if not args.e2e else {"ms_per_call": el / args.steps * 1e3,
+                            "kernel_ms_per_call": float(np.mean(hkms)),
+                            "bytes_in_per_call": int(h_labels.nbytes + h_offsets.nbytes),
+                            "note": "the headline: fst_compose_frozen_shortest_path_batch, "
+                                    "pageable host labels in, pinned host result out (the "
+                                    "streamed batch: labels staged into the result while the "
+                                    "kernel reads them, paths copied out by the kernel)"}}
 
-    extra = {}
     if args.varied:
         rng = np.random.default_rng(1234 + rank)
         vl = rng.integers(1, L + 1, size=args.batch)
@@ -495,14 +581,23 @@ def main():
         extra["lazy"] = {"value": lazy_total * 3 / lel, "kernel_ms": float(np.mean(lk)),
                          "batch": args.lazy_batch,
                          "checked_vs_oracle": check_sample(lb, blob_check, F.FST_SEM_LAZY),
-                         "note": "fst_compose_frozen_shortest_path semantics (lazy_pull_kernel, exact vs the oracle)"}
+                         "note": "fst_compose_frozen_shortest_path semantics (lazy_pull_kernel, "
+                                 "exact vs the oracle), device-resident"}
+        if args.lazy_batch == args.batch:
+            lb.run(rhs, F.FST_SEM_LAZY, local, torch.cuda.current_stream().cuda_stream, work=True)
+            torch.cuda.synchronize()
+            lwork = lb.work.cpu().numpy().astype(np.int64)
+            lplen = lb.plen.cpu().numpy().astype(np.int64)
+            extra["lazy"]["roofline"] = roofline_block(
+                args, F.FST_SEM_LAZY, float(np.mean(lk)), b_alg_bytes(lwork, lengths, lplen),
+                lwork, lengths, lplen, None, None)
         del lb
         if rank == 0 and not args.no_cpu and world == 1:  # the CPU port beside it (~3 s)
             extra["lazy"]["cpu_baseline"] = cpu_baseline(args, blob_check, 0, seconds=3.0)
 
     if args.f64:
-        # the f64-cell rates beside the headline: the f32 cells above hold only because the
-        # metric's weights are small integers; fractional grammar weights take f64 cells
+        # the f64-cell rates beside the headline: the integer cells above hold only because
+        # the metric's weights are small integers; fractional grammar weights take f64 cells
         E, Lz = F.FST_SEM_EAGER, F.FST_SEM_LAZY
         extra["f64_cells"] = {
             "eager": leg(batch, rhs, E, local, world, total_per_step, blob_check,
@@ -510,24 +605,16 @@ def main():
             "lazy": leg(batch, rhs, Lz, local, world, total_per_step, blob_check,
                         {"FSTAMD_LP_F64": "1"}),
             "note": "same metric batch and rhs, the pull kernels forced to f64 cells "
-                    "(FSTAMD_P_F64 / FSTAMD_LP_F64)"}
+                    "(FSTAMD_P_F64 / FSTAMD_LP_F64), device-resident"}
         fr = fractional_ambiguous(args.transducer_len, args.branches)
         fr_blob = D.blob_bytes(fr)
         extra["fractional_weights"] = {
             "eager": leg(batch, fr, E, local, world, total_per_step, fr_blob),
             "lazy": leg(batch, fr, Lz, local, world, total_per_step, fr_blob),
             "rhs": f"ambiguous chain T={args.transducer_len} B={args.branches}, every arc "
-                   "weight + 0.5 (f64 cells)"}
+                   "weight + 0.5 (f64 cells), device-resident"}
         del fr
-
-    if args.e2e:
-        del batch
-        torch.cuda.empty_cache()
-        extra["end_to_end"] = end_to_end(args, rhs, sem, local)
-        if world > 1:  # every rank ran its own; report the slowest as the job's rate
-            ms = max_over_ranks(extra["end_to_end"]["ms_per_call"], local)
-            extra["end_to_end"]["ms_per_call"] = ms
-            extra["end_to_end"]["value"] = total_per_step / (ms * 1e-3)
+    del batch
 
     if rank == 0:
         traffic, traffic_src = measured_traffic(args, sem)
@@ -546,12 +633,15 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             # results and the CPU port are f64; on this integer-weight rhs the pull tiers
-            # keep the cells' distances in f32, exact (every distance an integer < 2^24),
-            # so every output bit equals the f64 computation (checked_vs_oracle)
+            # keep the cells' distances as exact integers (every distance < 2^24), so every
+            # output bit equals the f64 computation (checked_vs_oracle)
             "dtype": "f64",
-            "cell_dtype": "f32 (exact: integer weights, max_len * max weight < 2^24)",
+            "cell_dtype": "u32 (exact: integer weights, max_len * max weight < 2^24)",
             "data": "synthetic (reference bench generators: 1^64 repeat acceptors, "
                     "ambiguous-chain rhs)",
+            "timed": ("host entry: pageable host labels in -> kernels -> host result "
+                      "(SURVEY 8(d) wall time); kernel-only rate in value_kernel") if args.e2e
+                     else "kernel-resident only (--no-e2e profiling run)",
             "config": {"workload": "compose_frozen_shortest_path_ambiguous",
                        "semantics": args.semantics, "len": L,
                        "transducer_len": args.transducer_len, "branches": args.branches,

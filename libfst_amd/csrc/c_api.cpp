@@ -269,6 +269,12 @@ void pin_release(void* p) {
     (void)hipHostFree(p);
   }
 }
+bool pin_is_pinned(const void* p) {  // a pooled block from hipHostMalloc (device-mapped)
+  PinPool& P = pin_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  auto it = P.live.find(const_cast<void*>(p));
+  return it != P.live.end() && it->second.second;
+}
 void pin_pool_clear() {
   PinPool& P = pin_pool();
   std::lock_guard<std::mutex> g(P.mu);
@@ -738,6 +744,12 @@ FstError run_pipelined(int dev, FrozenFst& b, const uint32_t* labels, const uint
       hipSuccess)
     return FST_OOM;
   std::vector<Shard> sh(parts);
+  // every return drains the engine stream before the buffers its kernels use (d_lab, d_off,
+  // the sub-shards' outputs: declared above, destroyed after this) go back to the pool
+  struct SyncEngine {
+    hipStream_t s;
+    ~SyncEngine() { (void)hipStreamSynchronize(s); }
+  } sync_engine{stream};
   for (uint32_t j = 0; j < parts; ++j) {
     sh[j].dev = dev;
     sh[j].s0 = (uint32_t)((uint64_t)num * j / parts);
@@ -843,6 +855,194 @@ FstError run_pipelined(int dev, FrozenFst& b, const uint32_t* labels, const uint
     agg.launches += S.stats.launches;
   }
   t_last_stats = agg;
+  return FST_OK;
+}
+
+// ---- The streamed host batch --------------------------------------------------------
+// One device, an rhs without input epsilons whose first tier is a pull tier (the metric's
+// case: DeviceEngine::pull_first).  Every path then has exactly L arcs, so string i's path
+// can sit at its own label offsets (BatchOutDev::slots) and the result's CSR offsets are
+// the rebased input offsets.  The host arrays ARE the kernel's I/O:
+//  * host threads copy the caller's labels into result.ilabels (pinned, device-mapped) in
+//    chunks of whole 128-B lines and publish how many are in place (`ready`, a host-coherent
+//    word); the pull tier reads each string's labels from there once they are (on an OK
+//    path il[k] = label k: the ilabels are the answer already);
+//  * the pull tier copies each finished path's olabels and weights into the result with
+//    whole-line stores as it goes (copy_out_paths), so there is no D2H of paths at all;
+//  * statuses and final weights (12 B per string) come down once, after the last tier;
+//  * strings the pull tier handed on are finished by the later tiers in the device arena
+//    (same slots) and downloaded after them; strings without a path are compacted out.
+// Returns FST_PATH_UNSUPPORTED (an int, not an FstError) when the mode does not apply; the
+// caller then takes the pipelined path.
+constexpr int kStreamNotApplicable = -1;
+constexpr uint64_t kStreamChunk = 1ull << 18;  // labels per staging chunk (1 MB, whole lines)
+
+struct ReadyWord {  // the `ready` count: host-coherent, device-mapped, one per thread
+  unsigned long long* p = nullptr;
+  ReadyWord() {
+    void* q = nullptr;
+    if (hipHostMalloc(&q, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess)
+      p = (unsigned long long*)q;
+  }
+  // (never freed: thread exit may come after the runtime's teardown)
+};
+
+int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
+                 uint32_t num, uint32_t n, int semantics, FstBatchResult* out) {
+  if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  DeviceFst* D = b.device(dev);
+  if (!D) return FST_OOM;
+  if (D->has_eps || !DeviceEngine::pull_first(*D, semantics)) return kStreamNotApplicable;
+  thread_local ReadyWord ready_word;
+  // (a plain pointer: the staging threads must publish to THIS thread's word, and a
+  // thread_local named inside their lambda would be their own)
+  unsigned long long* const ready = ready_word.p;
+  if (!ready) return kStreamNotApplicable;
+  const uint64_t base0 = offsets[0], total = offsets[num] - base0;
+  if (!alloc_result(out, num, total)) return FST_OOM;
+  if (!pin_is_pinned(out->ilabels) || !pin_is_pinned(out->olabels) ||
+      !pin_is_pinned(out->weights) || !pin_is_pinned(out->path_offsets)) {
+    fst_batch_result_free(out);
+    return kStreamNotApplicable;
+  }
+  uint64_t* const poff = out->path_offsets;
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < num; ++i) {
+    poff[i] = offsets[i] - base0;
+    max_len = std::max<uint32_t>(max_len, (uint32_t)(offsets[i + 1] - offsets[i]));
+  }
+  poff[num] = total;
+  const uint32_t* src = labels ? labels + base0 : nullptr;
+
+  // ---- label staging: chunk c = labels [c * kStreamChunk, ...), threads round robin,
+  // `ready` advanced over the finished prefix (in order) ----
+  const uint64_t nchunks = (total + kStreamChunk - 1) / kStreamChunk;
+  struct Stager {
+    std::mutex mu;
+    std::vector<uint8_t> done;
+    uint64_t next = 0;
+  } St;
+  St.done.assign(nchunks, 0);
+  auto stage = [&](uint64_t c) {
+    const uint64_t a = c * kStreamChunk, z = std::min(total, a + kStreamChunk);
+    std::memcpy(out->ilabels + a, src + a, (z - a) * 4);
+    std::lock_guard<std::mutex> g(St.mu);
+    St.done[c] = 1;
+    while (St.next < nchunks && St.done[St.next]) ++St.next;
+    __atomic_store_n(ready, std::min(total, St.next * kStreamChunk), __ATOMIC_RELEASE);
+  };
+  struct Threads {  // joined on every return (declared after what they use)
+    std::vector<std::thread> th;
+    ~Threads() {
+      for (auto& t : th) t.join();
+    }
+  } Th;
+  __atomic_store_n(ready, 0ull, __ATOMIC_RELEASE);
+  if (nchunks <= 1) {
+    if (nchunks) stage(0);
+  } else {
+    stage(0);  // the first waves start at once
+    const uint64_t T = std::min<uint64_t>(4, nchunks - 1);
+    for (uint64_t t = 0; t < T; ++t)
+      Th.th.emplace_back([&stage, t, T, nchunks] {
+        for (uint64_t c = 1 + t; c < nchunks; c += T) stage(c);
+      });
+  }
+
+  // ---- the engines: device inputs, outputs at fixed slots, the pull tier's copy-out ----
+  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
+  if (!E) return FST_INVALID_ARG;
+  const hipStream_t stream = E.stream();
+  DevBuf d_off((num + 1) * 8ull), d_first(std::max<size_t>(num, 1) * 4ull);
+  DevOut o(num, std::max<uint64_t>(total, 1));
+  if (!d_off.p || !d_first.p || !o.ok()) return FST_OOM;
+  struct SyncEngine {  // every return: the kernels are done with the result and the buffers
+    hipStream_t s;
+    ~SyncEngine() { (void)hipStreamSynchronize(s); }
+  } sync_engine{stream};
+  if (hipMemcpyAsync(d_off.p, poff, (num + 1) * 8ull, hipMemcpyHostToDevice, stream) !=
+      hipSuccess)
+    return FST_OOM;
+  ChainInput in{out->ilabels, (const uint64_t*)d_off.p, num, max_len, ready};
+  BatchOutDev v = o.v;
+  v.slots = (const uint64_t*)d_off.p;
+  v.host_ol = out->olabels;
+  v.host_w = out->weights;
+  // A/B knobs (timing only: FSTAMD_STREAM_AB=1 drops the copy-out -- the paths then stay on
+  // the device, results incomplete; =2 stages every label to a device buffer first)
+  const char* ab = std::getenv("FSTAMD_STREAM_AB");
+  std::unique_ptr<DevBuf> d_lab;
+  if (ab && std::atoi(ab) & 1) v.host_ol = nullptr, v.host_w = nullptr;
+  if (ab && std::atoi(ab) & 2) {
+    Th.~Threads();
+    new (&Th) Threads();
+    d_lab = std::make_unique<DevBuf>(std::max<uint64_t>(total, 1) * 4);
+    if (!d_lab->p || (total && hipMemcpyAsync(d_lab->p, out->ilabels, total * 4,
+                                              hipMemcpyHostToDevice, stream) != hipSuccess))
+      return FST_OOM;
+    in.labels = (const uint32_t*)d_lab->p;
+    in.ready = nullptr;
+  }
+  v.first_status = (int32_t*)d_first.p;
+  if (t_prof) t_prof->lap(0);
+  LaunchStats st;
+  if (E->run_chain(*D, in, n, semantics, v, stream, &st) != hipSuccess) return FST_OOM;
+  t_last_stats = st;
+  PinnedVec<int32_t> first(num);
+  if ((num && (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost,
+                              stream) != hipSuccess ||
+               hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost,
+                              stream) != hipSuccess ||
+               hipMemcpyAsync(first.data(), d_first.p, num * 4ull, hipMemcpyDeviceToHost,
+                              stream) != hipSuccess)) ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return FST_OOM;
+  if (t_prof) t_prof->lap(2);
+
+  // ---- fix-ups: paths the later tiers wrote (device arena, same slots), then the CSR ----
+  uint64_t nfix = 0, nbad = 0;
+  for (uint32_t i = 0; i < num; ++i) {
+    nbad += out->status[i] != kPathOk;
+    nfix += out->status[i] == kPathOk && first[i] != kPathOk;
+  }
+  if (nfix) {
+    const auto d2h = [&](void* dst, const void* s, size_t bytes) {
+      return bytes == 0 ||
+             hipMemcpyAsync(dst, s, bytes, hipMemcpyDeviceToHost, stream) == hipSuccess;
+    };
+    bool ok = true;
+    if (nfix <= 4096) {
+      for (uint32_t i = 0; i < num && ok; ++i)
+        if (out->status[i] == kPathOk && first[i] != kPathOk) {
+          const uint64_t a = poff[i], L = poff[i + 1] - a;
+          ok = d2h(out->olabels + a, (uint32_t*)o.ol.p + a, L * 4) &&
+               d2h(out->weights + a, (double*)o.w.p + a, L * 8);
+        }
+    } else {  // many: the whole arena (the pull tier's paths are in it too)
+      ok = d2h(out->olabels, o.ol.p, total * 4) && d2h(out->weights, o.w.p, total * 8);
+    }
+    if (!ok || hipStreamSynchronize(stream) != hipSuccess) return FST_OOM;
+  }
+  if (nbad) {  // drop the slots of strings without a path (in order, moving left)
+    uint64_t dst = 0;
+    for (uint32_t i = 0; i < num; ++i) {
+      const uint64_t a = poff[i], L = poff[i + 1] - a;
+      poff[i] = dst;
+      if (out->status[i] != kPathOk) continue;
+      if (dst != a) {
+        std::memmove(out->ilabels + dst, out->ilabels + a, L * 4);
+        std::memmove(out->olabels + dst, out->olabels + a, L * 4);
+        std::memmove(out->weights + dst, out->weights + a, L * 8);
+      }
+      dst += L;
+    }
+    poff[num] = dst;
+  }
+  out->total_arcs = poff[num];
+  if (t_prof) {
+    t_prof->runs = (int)st.launches;
+    t_prof->lap(3);
+  }
   return FST_OK;
 }
 
@@ -1670,6 +1870,24 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   struct ProfScope {
     ~ProfScope() { t_prof = nullptr; }
   } prof_scope;
+  // one device, an rhs without input epsilons and a pull tier first: the streamed batch
+  // (FSTAMD_STREAM=0 turns it off)
+  if (devices.size() == 1 && nsh == 1 && num_strings > 0) {
+    const char* se = std::getenv("FSTAMD_STREAM");
+    if (!(se && std::strcmp(se, "0") == 0)) {
+      DeviceRestore_ restore;
+      const int e = run_streamed(devices[0], *b, labels, offsets, num_strings, n, semantics, out);
+      if (e != kStreamNotApplicable) {
+        if (e != FST_OK) {
+          fst_batch_result_free(out);
+          return (FstError)e;
+        }
+        prof.lap(5);
+        prof.print("fst_compose_frozen_shortest_path_batch (streamed)");
+        return FST_OK;
+      }
+    }
+  }
   // one device and a large batch on an rhs without input epsilons: pipelined sub-shards
   // (FSTAMD_PIPELINE=0 keeps the one-shard path; FSTAMD_PIPELINE=k forces k sub-shards)
   {
@@ -1680,10 +1898,11 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
     parts = std::min<uint32_t>(parts, std::max<uint32_t>(num_strings, 1));
     const bool single = devices.size() == 1 && nsh == 1;
     if (single && want != 0 && parts >= 2) {
+      // (before hipSetDevice: every path out of this block gives the caller its device back)
+      DeviceRestore_ restore;
       DeviceFst* D = nullptr;
       if (hipSetDevice(devices[0]) == hipSuccess) D = b->device(devices[0]);
       if (D && !D->has_eps) {
-        DeviceRestore_ restore;
         const FstError e = run_pipelined(devices[0], *b, labels, offsets, num_strings, n,
                                          semantics, parts, out);
         if (e != FST_OK) {

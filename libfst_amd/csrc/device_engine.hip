@@ -544,10 +544,28 @@ static hipError_t finish_stats(hipEvent_t e0, hipEvent_t e1, LaunchStats* stats)
   return hipSuccess;
 }
 
+bool DeviceEngine::pull_first(const DeviceFst& rhs, int semantics) {
+  if (rhs.has_eps) return false;
+  if (semantics == 1) {  // run_chain's eager tier chain: use_p
+    if (rhs.nan || !rhs.nonneg || !rhs.pull_ok) return false;
+    return std::getenv("FSTAMD_EAGER_TIER1") == nullptr;
+  }
+  const char* le = std::getenv("FSTAMD_LAZY_ENGINE");  // the lazy dispatch below: use_lp
+  if (le && *le) return false;
+  return rhs.nonneg && rhs.finite && rhs.lazy_pull_ok;
+}
+
 hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                    int semantics, const BatchOutDev& out, hipStream_t stream,
                                    LaunchStats* stats) {
   HIP_TRY(hipSetDevice(dev_));
+  // streamed labels are waited for by the pull tiers only (they must come first)
+  if (in.ready && !pull_first(rhs, semantics)) return hipErrorInvalidValue;
+  auto snap_first = [&]() -> hipError_t {
+    if (!out.first_status || in.num_strings == 0) return hipSuccess;
+    return hipMemcpyAsync(out.first_status, out.status, (size_t)in.num_strings * 4,
+                          hipMemcpyDeviceToDevice, stream);
+  };
   unsigned int* counter = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!counter) return hipErrorOutOfMemory;
   HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
@@ -709,6 +727,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     if (use_p) {
       EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_p, back_cap_w, wd};
       HIP_TRY(launch_eager_pull(rhs, in, n, counter + 14, lp, out, grid_p, stream));
+      HIP_TRY(snap_first());
       // test hook: FSTAMD_EAGER_ONLY_FIRST leaves tier P's OVERFLOW / UNSUPPORTED strings
       // as they are, so a test can tell what the tier itself took
       if (std::getenv("FSTAMD_EAGER_ONLY_FIRST")) {
@@ -984,6 +1003,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     if (use_lp) {
       if (stats) stats->engine = 7;
       HIP_TRY(run_lazy_pull(rhs, in, n, out, stream, &lp_list, &lp_count));
+      HIP_TRY(snap_first());
       if (std::getenv("FSTAMD_LAZY_ONLY_FIRST")) {  // test hook: what the pull took alone
         if (stats) {
           HIP_TRY(hipEventRecord(ev1_, stream));

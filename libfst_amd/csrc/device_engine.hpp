@@ -157,6 +157,19 @@ struct BatchOutDev {
   uint64_t arc_cap;
   unsigned long long* cursor;
   uint32_t* work;
+  // The host batch's streamed mode (c_api.cpp run_streamed; rhs without input epsilons, so
+  // every path has exactly L arcs):
+  //   slots: string si's path sits at arena slot slots[si] (the batch's own label offsets:
+  //     no cursor, no compaction);
+  //   host_ol / host_w (pull tiers only): each finished path's olabels and weights are
+  //     also copied into these host-mapped result arrays (whole lines per store), and the
+  //     chase skips the ilabels (the host stages them: on an OK path il[k] = label k).
+  const uint64_t* slots = nullptr;
+  uint32_t* host_ol = nullptr;
+  double* host_w = nullptr;
+  // (host side, not read by kernels) when set, run_chain copies the statuses right after
+  // the first tier here: which strings the pull tier finished (and copied out) itself
+  int32_t* first_status = nullptr;
 };
 
 // Chain inputs (batch API) or one general lhs FST (single-call C ABI).
@@ -165,6 +178,10 @@ struct ChainInput {
   const uint64_t* offsets;
   uint32_t num_strings;
   uint32_t max_len;
+  // Streamed host batches: the labels live in host memory that host threads fill while the
+  // kernels run; *ready (host-coherent) = how many labels are in place (a prefix, always at
+  // a 128-B line boundary or the end).  A pull-tier wave waits until its string's labels are.
+  const unsigned long long* ready = nullptr;
 };
 struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
   const uint32_t* state_off;   // [ns + 1]
@@ -295,6 +312,11 @@ class DeviceEngine {
   // non-null (this synchronises on the stream's end event).
   hipError_t run_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
+  // Whether run_chain's first tier for these semantics is a pull tier (eager tier P, the
+  // lazy pull): only those wait for streamed labels (ChainInput::ready) and copy their
+  // paths out (BatchOutDev::host_ol), so the streamed host batch needs it.  run_chain
+  // refuses streamed inputs otherwise.
+  static bool pull_first(const DeviceFst& rhs, int semantics);
   hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
   // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp), on

@@ -264,7 +264,11 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       dlo = std::min(dlo, dl);
       dhi = std::max(dhi, dl);
     }
-    if ((dhi - dlo) * 8 < 0xFFF0) {
+    // Both halves of the bound: the offsets fit the high half, and the largest lane base
+    // of a window, 8 * (kPullW - 1) + rbias8, stays below a padding record's 0xFFFF, so
+    // base - 0xFFFF always wraps past slot W (a backward jump of ~7,900 states would
+    // otherwise turn padding into an in-window cell)
+    if ((dhi - dlo) * 8 < 0xFFF0 && -dlo * 8 + 8 * (int64_t)kPullW <= 0xFFFF) {
       rbias8 = (uint32_t)(-dlo * 8);
       rrec4.resize(rrec.size());
       for (size_t r = 0; r < rrec.size(); ++r) {

@@ -53,6 +53,54 @@ __device__ __forceinline__ void fst_trace(uint32_t item, uint32_t si, uint32_t k
 #define FT(item, si, k, ph) ((void)0)
 #endif
 
+// The arena slot of string si's path of P arcs: the next P slots of the batch's cursor,
+// or, in the streamed host batch (BatchOutDev::slots), the string's fixed slot.
+__device__ __forceinline__ unsigned long long reserve_path(const BatchOutDev& out, uint32_t si,
+                                                           uint32_t P) {
+  return out.slots ? out.slots[si] : atomicAdd(out.cursor, (unsigned long long)P);
+}
+
+// Streamed host batches (ChainInput::ready): a pull-tier wave waits until its string's
+// labels, [.., end), are in place.  `seen` (uniform, per wave) keeps the last count read, so
+// a wave polls only when a string ends past it; strings are claimed in increasing order.
+// False when the watchdog expires (the string then reports INTERNAL, never hangs).  The
+// labels' host lines are never read before the count covers them (the count stops at line
+// boundaries), so no cache holds a stale copy.
+__device__ __forceinline__ bool wait_labels(const ChainInput& in, uint64_t end,
+                                            unsigned long long& seen,
+                                            unsigned long long wd_ticks) {
+  if (!in.ready || end <= seen) return true;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const unsigned long long v = __hip_atomic_load(
+        const_cast<unsigned long long*>(in.ready), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    seen = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+    if (seen >= end) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > wd_ticks) return false;
+    __builtin_amdgcn_s_sleep(64);
+  }
+}
+
+// Streamed host batches (BatchOutDev::host_ol): after a batched chase, the wave copies the
+// finished paths' olabels and weights from their arena slots to the host-mapped result,
+// one string at a time so every store writes whole lines (the chase's own stores are one
+// lane per string, scattered).  The chase's stores are drained and this CU's L1 dropped
+// first (agent acquire: s_waitcnt vmcnt(0) + buffer_inv sc1), so the reads see them.
+__device__ __forceinline__ void copy_out_paths(const BatchOutDev& out, uint32_t njobs,
+                                               uint64_t my_o, uint32_t my_L, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (uint32_t j = 0; j < njobs; ++j) {  // uniform
+    const uint32_t Lj = __builtin_amdgcn_readlane(my_L, j);
+    const uint64_t oj = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_o >> 32), j) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((uint32_t)my_o, j);
+    for (uint32_t x = lane; x < Lj; x += 64) {
+      __builtin_nontemporal_store(out.out_ol[oj + x], out.host_ol + oj + x);
+      __builtin_nontemporal_store(out.out_w[oj + x], out.host_w + oj + x);
+    }
+  }
+}
+
 // Fst.arcsByIlabel (src/fst.zig:112-136): global arc range [lo, hi) of the arcs of
 // state `s` whose ilabel == label.  Spans of <= 8 arcs are counted with independent
 // loads (no dependent binary-search chain); longer spans use the two binary searches.

@@ -334,7 +334,7 @@ __device__ void bfs_shortest_path(const BfsTables& T, uint32_t n_nodes, uint32_t
       } else if (cur != start) {  // shortest-path.zig:120-122
         write_status(out, si, kPathEmpty, n_nodes, n_arcs);
       } else {
-        const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)hops);
+        const unsigned long long o = reserve_path(out, si, hops);
         if (o + hops > out.arc_cap) {
           write_status(out, si, kPathOutputFull, n_nodes, n_arcs);
         } else {
@@ -766,7 +766,7 @@ __device__ void bfs_lazy_path(const BfsTables& T, uint32_t ncap, uint32_t n_node
       write_status(out, si, st, n_nodes, n_arcs);
       return;
     }
-    const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)hops);
+    const unsigned long long o = reserve_path(out, si, hops);
     if (o + hops > out.arc_cap) {
       write_status(out, si, kPathOutputFull, n_nodes, n_arcs);
       return;
@@ -909,7 +909,7 @@ __device__ void sp_replay(const BfsTables& T, uint32_t n_nodes, uint32_t n_arcs,
     write_status(out, si, kPathEmpty, n_nodes, n_arcs);
     return;
   }
-  const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)hops);
+  const unsigned long long o = reserve_path(out, si, hops);
   if (o + hops > out.arc_cap) {
     write_status(out, si, kPathOutputFull, n_nodes, n_arcs);
     return;

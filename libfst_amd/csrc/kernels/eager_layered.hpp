@@ -413,7 +413,7 @@ eager_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* 
         write_status(out, si, kPathEmpty, tuples, relax);
       } else {
         const double fw = w_times(w_one(), rhs.final_w[T.s2p(cur)[bp]]);  // compose.zig:73
-        const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
+        const unsigned long long o = reserve_path(out, si, L);
         if (o + L > out.arc_cap) {
           write_status(out, si, kPathOutputFull, tuples, relax);
         } else {
@@ -740,7 +740,7 @@ eager_layered_lds_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned i
         write_status(out, si, kPathEmpty, tuples, relax);
       } else {
         const double fw = w_times(w_one(), rhs.final_w[T.s2p(cur)[bp]]);  // compose.zig:73
-        const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)Lk);
+        const unsigned long long o = reserve_path(out, si, Lk);
         if (o + Lk > out.arc_cap) {
           write_status(out, si, kPathOutputFull, tuples, relax);
         } else {

@@ -260,6 +260,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;  // uniform: pending backtraces (slab j belongs to job j)
+  unsigned long long ready_seen = 0;  // uniform: labels known staged (streamed batches)
 
   // lane r < njobs walks job r's path (shortest-path.zig:109-136): one 8-B back record
   // per arc, {reverse record of the arc, slab position of the source}
@@ -284,7 +285,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint32_t k = jb.L - 1 - t;
         const uint32_t b = FB(sl[FB(id, lp.back_cap, 60)], rv.nrec, 63);
         const uint2 h = hdr[k];
-        out.out_il[jb.o + k] = in.labels[jb.off + k];
+        if (!out.host_ol) out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
         if constexpr (RK == 3) {
           const uint32_t r = rv.rrec4[b];
@@ -321,6 +322,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         out.work[2 * jb.si + 1] = jb.relax;
       }
     }
+    if (out.host_ol) copy_out_paths(out, njobs, jb.o, jb.L, lane);
     njobs = 0;
     wave_lds_sync();
   };
@@ -370,6 +372,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
 
+    if (fail == kPathOk && !wait_labels(in, off + L, ready_seen, lp.wd_ticks))
+      fail = kPathInternal;  // (the watchdog: the host never staged its labels)
     uint32_t labs = 0;
     for (uint32_t k = 0; k < L && fail == kPathOk; ++k) {
       if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
@@ -596,7 +600,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       continue;
     }
     unsigned long long o = 0;
-    if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
+    if (lane == 0) o = reserve_path(out, si, L);
     o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
         __builtin_amdgcn_readfirstlane((uint32_t)o);
     if (o + L > out.arc_cap) {

@@ -186,7 +186,7 @@ __device__ __forceinline__ void wave_pick_and_backtrace(
     if (!hit) {
       write_status(out, si, kPathEmpty, tuples, relax);
     } else {
-      const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
+      const unsigned long long o = reserve_path(out, si, L);
       if (o + L > out.arc_cap) {
         write_status(out, si, kPathOutputFull, tuples, relax);
       } else {

@@ -365,7 +365,7 @@ eager_window_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
       continue;
     }
     unsigned long long o = 0;
-    if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
+    if (lane == 0) o = reserve_path(out, si, L);
     o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
         __builtin_amdgcn_readfirstlane((uint32_t)o);
     if (o + L > out.arc_cap) {

@@ -653,7 +653,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
           cur = step(cur, arc);
         }
         if (st == kPathOk) {
-          o = atomicAdd(out.cursor, (unsigned long long)P);
+          o = reserve_path(out, si, P);
           if (o + P > out.arc_cap) {
             st = kPathOutputFull;
           } else {

@@ -523,7 +523,7 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
           cur = prev;
         }
         if (st == kPathOk) {
-          o = atomicAdd(out.cursor, (unsigned long long)P);
+          o = reserve_path(out, si, P);
           if (o + P > out.arc_cap) {
             st = kPathOutputFull;
           } else {

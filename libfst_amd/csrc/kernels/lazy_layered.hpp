@@ -604,7 +604,7 @@ lazy_layered_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* n
         if (lane == 0) {
           // the path has exactly L arcs: each back-pointer steps back one layer, and
           // layer 0 holds only the start (compose-shortest-path.zig:372-380)
-          const unsigned long long o = atomicAdd(out.cursor, (unsigned long long)L);
+          const unsigned long long o = reserve_path(out, si, L);
           if (o + L > out.arc_cap) {
             write_status(out, si, kPathOutputFull, n, (uint32_t)relax);
           } else {

@@ -190,6 +190,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;
+  unsigned long long ready_seen = 0;  // uniform: labels known staged (streamed batches)
 
   // the batched backtrace of tier P (shortest-path.zig:109-136 / compose-shortest-
   // path.zig:368-380: the path has exactly L arcs, one per layer)
@@ -213,7 +214,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint32_t k = jb.L - 1 - t;
         const uint32_t b = FB(sl[FB(id, lp.back_cap, 70)], rv.nrec, 73);
         const uint2 h = hdr[k];
-        out.out_il[jb.o + k] = in.labels[jb.off + k];
+        if (!out.host_ol) out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
         if constexpr (RK == 2) {
           const uint2 r = rv.rrec8[b];
@@ -244,6 +245,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         out.work[2 * jb.si + 1] = jb.relax;
       }
     }
+    if (out.host_ol) copy_out_paths(out, njobs, jb.o, jb.L, lane);
     njobs = 0;
     wave_lds_sync();
   };
@@ -292,6 +294,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
 
+    if (fail == kPathOk && !wait_labels(in, off + L, ready_seen, lp.wd_ticks))
+      fail = kPathInternal;  // (the watchdog: the host never staged its labels)
     uint32_t labs = 0;
     // uniform: the current layer's pop ranks equal its id ranks (layer 0; every layer the
     // sort below finds already in order, or with at most one tuple): the merge's first
@@ -867,7 +871,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       continue;
     }
     unsigned long long o = 0;
-    if (lane == 0) o = atomicAdd(out.cursor, (unsigned long long)L);
+    if (lane == 0) o = reserve_path(out, si, L);
     o = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)o);
     if (o + L > out.arc_cap) {

@@ -790,7 +790,7 @@ lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_bes
             P = 0;
           }
           if (st == kPathOk) {
-            o = atomicAdd(out.cursor, (unsigned long long)P);
+            o = reserve_path(out, si, P);
             if (o + P > out.arc_cap) {
               st = kPathOutputFull;
             } else {

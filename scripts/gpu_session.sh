@@ -14,6 +14,7 @@ for spec in "$@"; do
   echo "=== [$name] rc=$rc in $(( $(date +%s) - start ))s"
   tail -n 25 "gpurun_out/$name.log"
   case $rc in
-    124|137|134|139|132|135) echo "=== stopping: $name ended with $rc"; exit $rc;;
+    0) ;;
+    *) echo "=== stopping: $name ended with $rc"; exit $rc;;
   esac
 done

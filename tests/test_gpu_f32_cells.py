@@ -136,3 +136,31 @@ def test_record_widths_at_the_rec8_bound(sem, wmax, monkeypatch):
     check(blob, *csr(seqs), sem)
     monkeypatch.setenv("FSTAMD_NO_REC8", "1")
     check(blob, *csr(seqs), sem)
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+@pytest.mark.parametrize("back", [7_800, 8_100])
+def test_long_backward_arc_and_the_rec4_bias(sem, back, monkeypatch):
+    # tier P's 4-B records hold 8 * (target - source) + bias; a padding record is 0xFFFF.
+    # One backward arc of `back` states makes the bias ~8 * back, so rows of windows near
+    # state 0 (t >= (0xFFFF - bias) / 8) would read padding as an in-window cell if the
+    # records were built: the bound must refuse them (both sizes straddle the old,
+    # bias-only bound) and the answers stay the oracle's, with and without FSTAMD_NO_REC4
+    ns = back + 200
+    f = O.Fst()
+    for i in range(ns):
+        f.add_state(float(i % 3))
+    f.start = 0
+    for s in range(ns - 1):
+        f.add_arc(s, 1, 1 + s % 5, float(s % 2), s + 1)
+        f.add_arc(s, 1, 7, 3.0, min(ns - 1, s + 2))
+        f.add_arc(s, 3, 9, 1.0, s)
+    f.add_arc(back, 2, 11, 0.0, 0)  # the only backward arc
+    blob = O.freeze(f)
+    rng = np.random.default_rng(back)
+    seqs = [[1] * L for L in (60, 100, 150, 200, 250)]
+    seqs += [[int(x) for x in rng.choice([1, 1, 1, 3], int(rng.integers(80, 250)))]
+             for _ in range(60)]
+    check(blob, *csr(seqs), sem)
+    monkeypatch.setenv("FSTAMD_NO_REC4", "1")
+    check(blob, *csr(seqs), sem)

@@ -221,14 +221,17 @@ def test_bench_two_ranks_one_gpu(mode):
     # bench.py's multi-process path in both scaling modes (the driver's 1/2/4/8-GPU runs
     # use RCCL, one GPU per rank): two ranks share cuda:0 over gloo here, each times its
     # shard and checks a sample against the oracle; rank 0 prints the one JSON line
+    # strong: under an explicit torchrun (the driver's form); weak: `bench.py --gpus 2`
+    # alone, which starts its two ranks itself (a child torchrun)
     repo = os.path.dirname(HERE)
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
+    launcher = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port", str(port)]
+    cmd = (launcher if mode == "strong" else [sys.executable]) + [
            os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
            "--backend", "gloo", "--scaling", mode, "--global-batch", "8192", "--batch", "4096",
-           "--no-cpu", "--no-e2e", "--no-varied", "--lazy-batch", "0", "--no-f64"]
-    env = dict(os.environ)
+           "--no-cpu", "--no-varied", "--lazy-batch", "0", "--no-f64"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
