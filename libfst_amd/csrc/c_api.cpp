@@ -862,29 +862,41 @@ FstError run_pipelined(int dev, FrozenFst& b, const uint32_t* labels, const uint
 // One device, an rhs without input epsilons whose first tier is a pull tier (the metric's
 // case: DeviceEngine::pull_first).  Every path then has exactly L arcs, so string i's path
 // can sit at its own label offsets (BatchOutDev::slots) and the result's CSR offsets are
-// the rebased input offsets.  The host arrays ARE the kernel's I/O:
-//  * host threads copy the caller's labels into result.ilabels (pinned, device-mapped) in
-//    chunks of whole 128-B lines and publish how many are in place (`ready`, a host-coherent
-//    word); the pull tier reads each string's labels from there once they are (on an OK
-//    path il[k] = label k: the ilabels are the answer already);
-//  * the pull tier copies each finished path's olabels and weights into the result with
-//    whole-line stores as it goes (copy_out_paths), so there is no D2H of paths at all;
-//  * statuses and final weights (12 B per string) come down once, after the last tier;
+// the rebased input offsets.  The batch runs as a few parts of growing size (labels 1/43,
+// 6/43, 36/43: each part's upload fits in the previous part's compute), alternating
+// between two engines (streams), each part's launch waiting on its labels' upload event;
+// the second engine's kernels fill the GPU while the first one's drain.  Meanwhile:
+//  * other host threads copy the labels into result.ilabels (on an OK path il[k] = label
+//    k: the result's ilabels are the input labels);
+//  * the pull tier copies each finished path's olabels and weights into the (pinned,
+//    device-mapped) result with whole-line stores as it goes (copy_out_paths): no D2H of
+//    paths, no compaction pass on the device;
+//  * statuses and final weights (12 B per string) come down per part;
 //  * strings the pull tier handed on are finished by the later tiers in the device arena
 //    (same slots) and downloaded after them; strings without a path are compacted out.
-// Returns FST_PATH_UNSUPPORTED (an int, not an FstError) when the mode does not apply; the
-// caller then takes the pipelined path.
+// No kernel ever waits on the host or another queue (only stream-ordered event waits).
+// Labels read from host memory instead (zero-copy) measured 34.5 vs 30.6 ms per 1M metric
+// strings: a PCIe read at every string's start.  Returns kStreamNotApplicable when the mode
+// does not apply; the caller then takes the pipelined path.
 constexpr int kStreamNotApplicable = -1;
-constexpr uint64_t kStreamChunk = 1ull << 18;  // labels per staging chunk (1 MB, whole lines)
 
-struct ReadyWord {  // the `ready` count: host-coherent, device-mapped, one per thread
-  unsigned long long* p = nullptr;
-  ReadyWord() {
-    void* q = nullptr;
-    if (hipHostMalloc(&q, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess)
-      p = (unsigned long long*)q;
+struct StreamKit {  // per calling thread and device: the upload stream and its events
+  hipStream_t up = nullptr;
+  std::vector<hipEvent_t> ev;
+  bool init(int dev) {
+    if (!up && hipSetDevice(dev) == hipSuccess)
+      (void)hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
+    return up != nullptr;
   }
-  // (never freed: thread exit may come after the runtime's teardown)
+  bool events(size_t n) {
+    while (ev.size() < n) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+      ev.push_back(e);
+    }
+    return true;
+  }
+  // (never destroyed: thread exit may come after the runtime's teardown)
 };
 
 int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
@@ -893,11 +905,10 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   DeviceFst* D = b.device(dev);
   if (!D) return FST_OOM;
   if (D->has_eps || !DeviceEngine::pull_first(*D, semantics)) return kStreamNotApplicable;
-  thread_local ReadyWord ready_word;
-  // (a plain pointer: the staging threads must publish to THIS thread's word, and a
-  // thread_local named inside their lambda would be their own)
-  unsigned long long* const ready = ready_word.p;
-  if (!ready) return kStreamNotApplicable;
+  thread_local std::map<int, StreamKit> kits;
+  StreamKit& K = kits[dev];
+  if (!K.init(dev) || !K.events(4)) return kStreamNotApplicable;
+  const hipStream_t up = K.up;
   const uint64_t base0 = offsets[0], total = offsets[num] - base0;
   if (!alloc_result(out, num, total)) return FST_OOM;
   if (!pin_is_pinned(out->ilabels) || !pin_is_pinned(out->olabels) ||
@@ -905,99 +916,170 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     fst_batch_result_free(out);
     return kStreamNotApplicable;
   }
-  uint64_t* const poff = out->path_offsets;
-  uint32_t max_len = 0;
-  for (uint32_t i = 0; i < num; ++i) {
-    poff[i] = offsets[i] - base0;
-    max_len = std::max<uint32_t>(max_len, (uint32_t)(offsets[i + 1] - offsets[i]));
-  }
-  poff[num] = total;
   const uint32_t* src = labels ? labels + base0 : nullptr;
-
-  // ---- label staging: chunk c = labels [c * kStreamChunk, ...), threads round robin,
-  // `ready` advanced over the finished prefix (in order) ----
-  const uint64_t nchunks = (total + kStreamChunk - 1) / kStreamChunk;
-  struct Stager {
-    std::mutex mu;
-    std::vector<uint8_t> done;
-    uint64_t next = 0;
-  } St;
-  St.done.assign(nchunks, 0);
-  auto stage = [&](uint64_t c) {
-    const uint64_t a = c * kStreamChunk, z = std::min(total, a + kStreamChunk);
-    std::memcpy(out->ilabels + a, src + a, (z - a) * 4);
-    std::lock_guard<std::mutex> g(St.mu);
-    St.done[c] = 1;
-    while (St.next < nchunks && St.done[St.next]) ++St.next;
-    __atomic_store_n(ready, std::min(total, St.next * kStreamChunk), __ATOMIC_RELEASE);
-  };
   struct Threads {  // joined on every return (declared after what they use)
     std::vector<std::thread> th;
-    ~Threads() {
+    void join() {
       for (auto& t : th) t.join();
+      th.clear();
     }
-  } Th;
-  __atomic_store_n(ready, 0ull, __ATOMIC_RELEASE);
-  if (nchunks <= 1) {
-    if (nchunks) stage(0);
-  } else {
-    stage(0);  // the first waves start at once
-    const uint64_t T = std::min<uint64_t>(4, nchunks - 1);
+    ~Threads() { join(); }
+  };
+
+  // ---- the result's CSR offsets (= the rebased input offsets) and max_len ----
+  uint64_t* const poff = out->path_offsets;
+  uint32_t max_len = 0;
+  {
+    const uint32_t nt = num >= (1u << 18) ? 4 : 1;
+    std::vector<uint32_t> mx(nt, 0);
+    auto rebase = [&](uint32_t t) {
+      uint32_t m = 0;
+      for (uint64_t i = (uint64_t)num * t / nt, e = (uint64_t)num * (t + 1) / nt; i < e; ++i) {
+        poff[i] = offsets[i] - base0;
+        m = std::max<uint32_t>(m, (uint32_t)(offsets[i + 1] - offsets[i]));
+      }
+      mx[t] = m;
+    };
+    Threads R;
+    for (uint32_t t = 1; t < nt; ++t) R.th.emplace_back(rebase, t);
+    rebase(0);
+    R.join();
+    for (uint32_t m : mx) max_len = std::max(max_len, m);
+    poff[num] = total;
+  }
+
+  // ---- parts: string ranges cut at 1/43 and 7/43 of the labels (small batches: one) ----
+  std::vector<uint32_t> cut{0};
+  if (total >= (1u << 22) && num >= (1u << 15)) {
+    for (uint64_t f : {1ull, 7ull}) {
+      const uint64_t want = total * f / 43;
+      const uint32_t i = (uint32_t)(std::upper_bound(poff, poff + num, want) - poff);
+      if (i > cut.back() && i < num) cut.push_back(i);
+    }
+  }
+  cut.push_back(num);
+  const size_t parts = cut.size() - 1;
+
+  // ---- engines and device buffers ----
+  DeviceEngine::Lease EA = DeviceEngine::acquire(dev);
+  if (!EA) return FST_INVALID_ARG;
+  DeviceEngine::Lease EB;
+  if (parts > 1) EB = DeviceEngine::try_acquire(dev);  // (none free: one engine in order)
+  const hipStream_t sA = EA.stream(), sB = EB ? EB.stream() : nullptr;
+  DevBuf d_lab(std::max<uint64_t>(total, 1) * 4), d_off((num + 1) * 8ull),
+      d_first(std::max<size_t>(num, 1) * 4ull);
+  DevOut o(num, std::max<uint64_t>(total, 1));
+  if (!d_lab.p || !d_off.p || !d_first.p || !o.ok()) return FST_OOM;
+  PinnedVec<int32_t> first(num);
+  struct SyncAll {  // every return: no kernel or copy still uses the buffers or the result
+    hipStream_t s[3];
+    ~SyncAll() {
+      for (hipStream_t x : s)
+        if (x) (void)hipStreamSynchronize(x);
+    }
+  } sync_all{{up, sA, sB}};
+
+  // ---- uploads (offsets, then each part's labels: one event per part) ----
+  struct Ready {
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t n = 0;
+    bool failed = false;
+  } R;
+  Threads Th;
+  Th.th.emplace_back([&] {
+    bool ok = hipSetDevice(dev) == hipSuccess &&
+              hipMemcpyAsync(d_off.p, poff, (num + 1) * 8ull, hipMemcpyHostToDevice, up) ==
+                  hipSuccess;
+    for (size_t p = 0; p < parts && ok; ++p) {
+      const uint64_t a = poff[cut[p]], z = poff[cut[p + 1]];
+      // (a pageable source is staged through pinned memory before this returns)
+      ok = (z == a || hipMemcpyAsync((uint32_t*)d_lab.p + a, src + a, (z - a) * 4,
+                                     hipMemcpyHostToDevice, up) == hipSuccess) &&
+           hipEventRecord(K.ev[p], up) == hipSuccess;
+      std::lock_guard<std::mutex> g(R.mu);
+      if (ok) R.n = p + 1;
+      R.cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(R.mu);
+    if (!ok) R.failed = true;
+    R.cv.notify_all();
+  });
+  {
+    const uint64_t T = total >= (1u << 20) ? 3 : 1;  // the result's ilabels
     for (uint64_t t = 0; t < T; ++t)
-      Th.th.emplace_back([&stage, t, T, nchunks] {
-        for (uint64_t c = 1 + t; c < nchunks; c += T) stage(c);
+      Th.th.emplace_back([&, t, T] {
+        const uint64_t a = total * t / T, z = total * (t + 1) / T;
+        if (z > a) std::memcpy(out->ilabels + a, src + a, (z - a) * 4);
       });
   }
 
-  // ---- the engines: device inputs, outputs at fixed slots, the pull tier's copy-out ----
-  DeviceEngine::Lease E = DeviceEngine::acquire(dev);
-  if (!E) return FST_INVALID_ARG;
-  const hipStream_t stream = E.stream();
-  DevBuf d_off((num + 1) * 8ull), d_first(std::max<size_t>(num, 1) * 4ull);
-  DevOut o(num, std::max<uint64_t>(total, 1));
-  if (!d_off.p || !d_first.p || !o.ok()) return FST_OOM;
-  struct SyncEngine {  // every return: the kernels are done with the result and the buffers
-    hipStream_t s;
-    ~SyncEngine() { (void)hipStreamSynchronize(s); }
-  } sync_engine{stream};
-  if (hipMemcpyAsync(d_off.p, poff, (num + 1) * 8ull, hipMemcpyHostToDevice, stream) !=
-      hipSuccess)
-    return FST_OOM;
-  ChainInput in{out->ilabels, (const uint64_t*)d_off.p, num, max_len, ready};
-  BatchOutDev v = o.v;
-  v.slots = (const uint64_t*)d_off.p;
-  v.host_ol = out->olabels;
-  v.host_w = out->weights;
-  // A/B knobs (timing only: FSTAMD_STREAM_AB=1 drops the copy-out -- the paths then stay on
-  // the device, results incomplete; =2 stages every label to a device buffer first)
-  const char* ab = std::getenv("FSTAMD_STREAM_AB");
-  std::unique_ptr<DevBuf> d_lab;
-  if (ab && std::atoi(ab) & 1) v.host_ol = nullptr, v.host_w = nullptr;
-  if (ab && std::atoi(ab) & 2) {
-    Th.~Threads();
-    new (&Th) Threads();
-    d_lab = std::make_unique<DevBuf>(std::max<uint64_t>(total, 1) * 4);
-    if (!d_lab->p || (total && hipMemcpyAsync(d_lab->p, out->ilabels, total * 4,
-                                              hipMemcpyHostToDevice, stream) != hipSuccess))
-      return FST_OOM;
-    in.labels = (const uint32_t*)d_lab->p;
-    in.ready = nullptr;
-  }
-  v.first_status = (int32_t*)d_first.p;
+  // ---- the parts: engine A takes parts 0, 2, .., engine B 1, 3, .. (A all without B) ----
+  struct PartRun {
+    FstError err = FST_OK;
+    LaunchStats st;
+  };
+  std::vector<PartRun> pr(parts);
+  auto drive = [&](DeviceEngine::Lease& E, hipStream_t s, size_t p0, size_t step) {
+    if (hipSetDevice(dev) != hipSuccess) {
+      pr[p0].err = FST_INVALID_ARG;
+      return;
+    }
+    for (size_t p = p0; p < parts; p += step) {
+      {
+        std::unique_lock<std::mutex> g(R.mu);
+        R.cv.wait(g, [&] { return R.failed || R.n > p; });
+        if (R.n <= p) {
+          pr[p].err = FST_OOM;
+          return;
+        }
+      }
+      const uint32_t s0 = cut[p], np = cut[p + 1] - cut[p];
+      ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p + s0, np, max_len};
+      BatchOutDev v = o.v;
+      v.status += s0;
+      v.path_len += s0;
+      v.path_off += s0;
+      v.final_w += s0;
+      v.slots = (const uint64_t*)d_off.p + s0;
+      v.host_ol = out->olabels;
+      v.host_w = out->weights;
+      v.first_status = (int32_t*)d_first.p + s0;
+      if (hipStreamWaitEvent(s, K.ev[p], 0) != hipSuccess ||
+          E->run_chain(*D, in, n, semantics, v, s, &pr[p].st) != hipSuccess ||
+          hipMemcpyAsync(out->status + s0, v.status, np * 4ull, hipMemcpyDeviceToHost, s) !=
+              hipSuccess ||
+          hipMemcpyAsync(out->final_weights + s0, v.final_w, np * 8ull, hipMemcpyDeviceToHost,
+                         s) != hipSuccess ||
+          hipMemcpyAsync(first.data() + s0, v.first_status, np * 4ull, hipMemcpyDeviceToHost,
+                         s) != hipSuccess) {
+        pr[p].err = FST_OOM;
+        return;
+      }
+    }
+  };
   if (t_prof) t_prof->lap(0);
-  LaunchStats st;
-  if (E->run_chain(*D, in, n, semantics, v, stream, &st) != hipSuccess) return FST_OOM;
-  t_last_stats = st;
-  PinnedVec<int32_t> first(num);
-  if ((num && (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost,
-                              stream) != hipSuccess ||
-               hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost,
-                              stream) != hipSuccess ||
-               hipMemcpyAsync(first.data(), d_first.p, num * 4ull, hipMemcpyDeviceToHost,
-                              stream) != hipSuccess)) ||
-      hipStreamSynchronize(stream) != hipSuccess)
-    return FST_OOM;
+  {
+    Threads P;
+    if (EB) P.th.emplace_back([&] { drive(EB, sB, 1, 2); });
+    drive(EA, sA, 0, EB ? 2 : 1);
+    P.join();
+  }
+  for (hipStream_t x : {up, sA, sB})
+    if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
+  Th.join();
+  LaunchStats agg{};
+  for (size_t p = 0; p < parts; ++p) {
+    if (pr[p].err != FST_OK) return pr[p].err;
+    if (p == 0) agg = pr[p].st;
+    else {
+      agg.kernel_ms += pr[p].st.kernel_ms;
+      agg.launches += pr[p].st.launches;
+    }
+  }
+  t_last_stats = agg;
   if (t_prof) t_prof->lap(2);
+  const hipStream_t stream = sA;
 
   // ---- fix-ups: paths the later tiers wrote (device arena, same slots), then the CSR ----
   uint64_t nfix = 0, nbad = 0;
@@ -1040,7 +1122,7 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   }
   out->total_arcs = poff[num];
   if (t_prof) {
-    t_prof->runs = (int)st.launches;
+    t_prof->runs = (int)agg.launches;
     t_prof->lap(3);
   }
   return FST_OK;

@@ -457,6 +457,22 @@ DeviceEngine::Lease DeviceEngine::acquire(int dev) {
   }
 }
 
+DeviceEngine::Lease DeviceEngine::try_acquire(int dev) {
+  if (dev < 0) return Lease();
+  EnginePool& P = engine_pool(dev);
+  std::lock_guard<std::mutex> lk(P.mu);
+  if (!P.idle.empty()) {
+    DeviceEngine* e = P.idle.back();
+    P.idle.pop_back();
+    return Lease(e);
+  }
+  if (P.all.size() < max_engines()) {
+    P.all.emplace_back(new DeviceEngine(dev));
+    return Lease(P.all.back().get());
+  }
+  return Lease();
+}
+
 hipStream_t DeviceEngine::Lease::own_stream() const { return e_ ? e_->stream_ : nullptr; }
 
 hipStream_t DeviceEngine::Lease::use(hipStream_t s) {
@@ -559,8 +575,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                                    int semantics, const BatchOutDev& out, hipStream_t stream,
                                    LaunchStats* stats) {
   HIP_TRY(hipSetDevice(dev_));
-  // streamed labels are waited for by the pull tiers only (they must come first)
-  if (in.ready && !pull_first(rhs, semantics)) return hipErrorInvalidValue;
+  // the pull tiers alone copy paths out to the host (they must come first)
+  if (out.host_ol && !pull_first(rhs, semantics)) return hipErrorInvalidValue;
   auto snap_first = [&]() -> hipError_t {
     if (!out.first_status || in.num_strings == 0) return hipSuccess;
     return hipMemcpyAsync(out.first_status, out.status, (size_t)in.num_strings * 4,

@@ -178,10 +178,6 @@ struct ChainInput {
   const uint64_t* offsets;
   uint32_t num_strings;
   uint32_t max_len;
-  // Streamed host batches: the labels live in host memory that host threads fill while the
-  // kernels run; *ready (host-coherent) = how many labels are in place (a prefix, always at
-  // a 128-B line boundary or the end).  A pull-tier wave waits until its string's labels are.
-  const unsigned long long* ready = nullptr;
 };
 struct GraphInput {       // CSR of a MutableFst lhs, arcs in insertion order
   const uint32_t* state_off;   // [ns + 1]
@@ -307,6 +303,8 @@ class DeviceEngine {
   };
   // Blocks while every engine of the device is leased.  An empty lease on failure.
   static Lease acquire(int dev);
+  // The same without blocking: an empty lease when every engine of the device is leased.
+  static Lease try_acquire(int dev);
 
   // All launches are asynchronous on `stream`; stats are filled when `stats` is
   // non-null (this synchronises on the stream's end event).

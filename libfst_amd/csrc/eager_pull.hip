@@ -268,7 +268,13 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     // of a window, 8 * (kPullW - 1) + rbias8, stays below a padding record's 0xFFFF, so
     // base - 0xFFFF always wraps past slot W (a backward jump of ~7,900 states would
     // otherwise turn padding into an in-window cell)
-    if ((dhi - dlo) * 8 < 0xFFF0 && -dlo * 8 + 8 * (int64_t)kPullW <= 0xFFFF) {
+    // Tier P then keeps 1-B back records (x * kp + m, eager_pull.hpp): the direct layout
+    // only, every in-arc group within 255 / kp blocks
+    uint64_t max_nb = 0;
+    for (const uint4& r : rspan)
+      if (r.z != kSpanMixed) max_nb = std::max<uint64_t>(max_nb, r.y);
+    if ((dhi - dlo) * 8 < 0xFFF0 && -dlo * 8 + 8 * (int64_t)kPullW <= 0xFFFF && direct &&
+        max_nb * kp <= 255) {
       rbias8 = (uint32_t)(-dlo * 8);
       rrec4.resize(rrec.size());
       for (size_t r = 0; r < rrec.size(); ++r) {

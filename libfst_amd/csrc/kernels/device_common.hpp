@@ -60,28 +60,6 @@ __device__ __forceinline__ unsigned long long reserve_path(const BatchOutDev& ou
   return out.slots ? out.slots[si] : atomicAdd(out.cursor, (unsigned long long)P);
 }
 
-// Streamed host batches (ChainInput::ready): a pull-tier wave waits until its string's
-// labels, [.., end), are in place.  `seen` (uniform, per wave) keeps the last count read, so
-// a wave polls only when a string ends past it; strings are claimed in increasing order.
-// False when the watchdog expires (the string then reports INTERNAL, never hangs).  The
-// labels' host lines are never read before the count covers them (the count stops at line
-// boundaries), so no cache holds a stale copy.
-__device__ __forceinline__ bool wait_labels(const ChainInput& in, uint64_t end,
-                                            unsigned long long& seen,
-                                            unsigned long long wd_ticks) {
-  if (!in.ready || end <= seen) return true;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    const unsigned long long v = __hip_atomic_load(
-        const_cast<unsigned long long*>(in.ready), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    seen = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)v);
-    if (seen >= end) return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > wd_ticks) return false;
-    __builtin_amdgcn_s_sleep(64);
-  }
-}
-
 // Streamed host batches (BatchOutDev::host_ol): after a batched chase, the wave copies the
 // finished paths' olabels and weights from their arena slots to the host-mapped result,
 // one string at a time so every store writes whole lines (the chase's own stores are one

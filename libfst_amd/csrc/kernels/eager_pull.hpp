@@ -124,8 +124,8 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec
                                                uint32_t& rank_word) {
   // byte offset of the source's cell; outside the window (or padding): slot W
   const uint32_t off = min(r.src - tmin8, 8u * W);
-  const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + off);
-  const uint32_t rw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S.rk) + off);
+  const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + FB(off, 8 * (W + 1), 150));
+  const uint32_t rw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S.rk) + FB(off, 8 * (W + 1), 151));
   // (folding the pad c.w into the OR makes the compiler read the cell with one
   // ds_read2_b64 instead of b64 + b32, but costs a register and spills: 19.1 vs 20.1 M
   // strings/s)
@@ -142,7 +142,7 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const 
                                                uint32_t tmin8, uint32_t& pk, uint32_t& nd,
                                                uint32_t& rank_word) {
   const uint32_t off = min(r.x - tmin8, 8u * W);
-  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
+  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + FB(off, 8 * (W + 1), 152));
   pk = c.y | r.y | off;
   rank_word = c.y;
   nd = c.x + r.z;
@@ -157,7 +157,7 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const 
                                                uint32_t tmin8, uint32_t& pk, uint32_t& nd,
                                                uint32_t& rank_word) {
   const uint32_t off = min(r.x - tmin8, 8u * W);
-  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
+  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + FB(off, 8 * (W + 1), 152));
   pk = c.y | r.y | off;
   rank_word = c.y;
   nd = c.x + rec8_weight(r.y);  // (one v_add_u32 with a byte-0 SDWA operand)
@@ -174,7 +174,7 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W, true>& S, const 
                                                uint32_t base8, uint32_t& pk, uint32_t& nd,
                                                uint32_t& rank_word) {
   const uint32_t off = min(base8 - (r >> 16), 8u * W);
-  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + off);
+  const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(S.cell) + FB(off, 8 * (W + 1), 152));
   pk = c.y | (r & 0xFFFFu);
   rank_word = c.y;
   nd = c.x + (r & 0xFFu);
@@ -246,10 +246,10 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   // a cell: {distance, rank word}
   auto set_cell = [&](uint32_t i, DT d, uint32_t rw) {
     if constexpr (F32) {
-      S.cell[i] = make_uint2(d, rw);
+      S.cell[FB(i, W + 1, 153)] = make_uint2(d, rw);
     } else {
-      S.d[i] = d;
-      S.rk[i] = rw;
+      S.d[FB(i, W + 1, 154)] = d;
+      S.rk[FB(i, W + 1, 155)] = rw;
     }
   };
   auto rec = [&](uint32_t r) -> RT {
@@ -260,7 +260,6 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;  // uniform: pending backtraces (slab j belongs to job j)
-  unsigned long long ready_seen = 0;  // uniform: labels known staged (streamed batches)
 
   // lane r < njobs walks job r's path (shortest-path.zig:109-136): one 8-B back record
   // per arc, {reverse record of the arc, slab position of the source}
@@ -269,7 +268,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t maxL = 0;
     ChaseJob jb{};
     if (lane < njobs) {
-      jb = S.job[lane];
+      jb = S.job[FB(lane, kChaseBatch, 156)];
       maxL = jb.L;
     }
     maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
@@ -283,7 +282,15 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
-        const uint32_t b = FB(sl[FB(id, lp.back_cap, 60)], rv.nrec, 63);
+        uint32_t b;
+        if constexpr (RK == 3) {  // the byte x * KP + m of the tuple at slab position id,
+                                  // whose state is tcur: block 0 at tcur * KP, blocks 1.. at
+                                  // rxrec[tcur].x (eager_pull.hip)
+          const uint32_t v = reinterpret_cast<const uint8_t*>(sl)[FB(id, lp.back_cap, 60)];
+          b = FB(v < (uint32_t)KP ? tcur * KP + v : rv.rxrec[tcur].x + v - KP, rv.nrec, 63);
+        } else {
+          b = FB(sl[FB(id, lp.back_cap, 60)], rv.nrec, 63);
+        }
         const uint2 h = hdr[k];
         if (!out.host_ol) out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
@@ -332,7 +339,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) set_cell(i, kInf, kPullAbsent);
-  if (lane < (uint32_t)kWords) S.bits[lane] = 0;
+  if (lane < (uint32_t)kWords) S.bits[FB(lane, kWords, 157)] = 0;
   wave_lds_sync();
   uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
 
@@ -372,8 +379,6 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
 
-    if (fail == kPathOk && !wait_labels(in, off + L, ready_seen, lp.wd_ticks))
-      fail = kPathInternal;  // (the watchdog: the host never staged its labels)
     uint32_t labs = 0;
     for (uint32_t k = 0; k < L && fail == kPathOk; ++k) {
       if ((k & 15u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > lp.wd_ticks) {
@@ -463,7 +468,10 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
         }
-        uint32_t ra = rec0 + ((c >> kMShift) & 15u);
+        // the back record: RK 3 (direct layout) keeps one byte, the in-arc's position
+        // x * KP + m in its target's group (block x, slot m; the chase re-derives the record
+        // from the target state); the other kinds the record index itself
+        uint32_t ra = (RK == 3 ? 0u : rec0) + ((c >> kMShift) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
           if constexpr (DIRECT) {  // block 1's record; the true count past 255 blocks
@@ -487,7 +495,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
                 c = p2;
-                ra = rx + m;
+                ra = RK == 3 ? x * KP + m : rx + m;
               }
               if (want_work) relax += (uint32_t)__popcll(__ballot(w2 < kPullAbsent));
             }
@@ -502,7 +510,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           // (a 32-bit OR into the word's half: ~4 lanes of a row share an address instead
           // of ~8, and same-address LDS atomics serialise -- they were all of the kernel's
           // LDS conflict cycles)
-          atomicOr(reinterpret_cast<uint32_t*>(S.bits) + (key >> 5), 1u << (key & 31u));
+          atomicOr(reinterpret_cast<uint32_t*>(S.bits) + FB(key >> 5, 2 * kWords, 158), 1u << (key & 31u));
         }
       }
       wave_lds_sync();
@@ -510,16 +518,16 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // ---- (P2) ranks: popcount prefix over the first-key bitmap ----
       const uint32_t nw = (n_cur * 8 + 63) / 64;  // keys < 8 * n_cur
       unsigned long long word = 0;
-      if (lane < nw) word = S.bits[lane];
+      if (lane < nw) word = S.bits[FB(lane, kWords, 159)];
       const uint32_t pc = (uint32_t)__popcll(word);
       const uint32_t inc = wave_incl_scan_dpp(pc);
       const uint32_t n_next = __builtin_amdgcn_readlane(inc, 63);
       if (lane < nw) {
         // per 32-bit half: {popcount of the keys before it, its bits}, so P3's lookup is one
         // 32-bit mask and count
-        S.pre[lane] = make_uint4(inc - pc, (uint32_t)word,
+        S.pre[FB(lane, kWords, 160)] = make_uint4(inc - pc, (uint32_t)word,
                                  inc - pc + (uint32_t)__popc((uint32_t)word), (uint32_t)(word >> 32));
-        S.bits[lane] = 0;
+        S.bits[FB(lane, kWords, 161)] = 0;
       }
       wave_lds_sync();
       if (n_next == 0) {  // no candidate: the lattice dies here, no final is reachable
@@ -541,7 +549,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rank = 0;
         if ((uint32_t)e < rows_n) {
           const uint32_t key = pres ? fst[e] >> kFirstShift : 0u;
-          const uint2 p = reinterpret_cast<const uint2*>(S.pre)[key >> 5];
+          const uint2 p = reinterpret_cast<const uint2*>(S.pre)[FB(key >> 5, 2 * kWords, 162)];
           rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
         }
         // (an absent slot keeps its merged distance, +inf or >= kDistAbsent: no select; the
@@ -553,7 +561,10 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 61) * 4u)) = bra[e];
+          if constexpr (RK == 3)
+            reinterpret_cast<uint8_t*>(back)[FB(nbase + i, lp.back_cap, 61)] = (uint8_t)bra[e];
+          else
+            *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 61) * 4u)) = bra[e];
           if (last) {  // final candidates, lexmin (total, rank) within the lane
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
@@ -608,7 +619,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       continue;
     }
     if (lane == 0) {
-      ChaseJob& j = S.job[njobs];
+      ChaseJob& j = S.job[FB(njobs, kChaseBatch, 163)];
       j.si = si;
       j.L = L;
       j.id = base + (bp & 511u);  // shortest-path.zig:109-136 starts at the best final

@@ -66,17 +66,19 @@ struct LazyPullCells {  // f64 distances: d, {idw, pw}, tb
   unsigned long long rp[W + 1];    // lo: idw; hi: pw
   double tb[W + 1];
   __device__ __forceinline__ const char* base(const void* a) const { return (const char*)a; }
-  __device__ __forceinline__ double get_d(uint32_t o) const { return *(const double*)(base(d) + o); }
-  __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return *(const uint32_t*)(base(rp) + o); }
-  __device__ __forceinline__ uint32_t get_pw(uint32_t o) const { return *(const uint32_t*)(base(rp) + o + 4); }
-  __device__ __forceinline__ double get_tb(uint32_t o) const { return *(const double*)(base(tb) + o); }
+  // (DEBUG_BOUNDS: byte offsets o < 8 (W + 1), slots i <= W, as every LDS index below)
+  __device__ __forceinline__ double get_d(uint32_t o) const { return *(const double*)(base(d) + FB(o, 8 * (W + 1), 100)); }
+  __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return *(const uint32_t*)(base(rp) + FB(o, 8 * (W + 1), 101)); }
+  __device__ __forceinline__ uint32_t get_pw(uint32_t o) const { return *(const uint32_t*)(base(rp) + FB(o, 8 * (W + 1), 102) + 4); }
+  __device__ __forceinline__ double get_tb(uint32_t o) const { return *(const double*)(base(tb) + FB(o, 8 * (W + 1), 103)); }
   __device__ __forceinline__ void set(uint32_t i, double dd, uint32_t idw, uint32_t pw, double t) {
+    i = FB(i, W + 1, 104);
     d[i] = dd;
     rp[i] = ((unsigned long long)pw << 32) | idw;
     tb[i] = t;
   }
   __device__ __forceinline__ void set_pop(uint32_t i, uint32_t q) {  // pop rank q
-    uint32_t* w = (uint32_t*)&rp[i] + 1;
+    uint32_t* w = (uint32_t*)&rp[FB(i, W + 1, 105)] + 1;
     *w = (*w & kLpRunMask) | (q << 20);
   }
 };
@@ -91,11 +93,11 @@ template <int W>
 struct LazyPullCells<W, float> {
   uint2 a[W + 1];                  // {f32 bits of d, idw}
   uint32_t b[W + 1];               // pw
-  __device__ __forceinline__ uint2 get_a(uint32_t o) const { return *(const uint2*)((const char*)a + o); }
+  __device__ __forceinline__ uint2 get_a(uint32_t o) const { return *(const uint2*)((const char*)a + FB(o, 8 * (W + 1), 106)); }
   __device__ __forceinline__ float get_d(uint32_t o) const { return __uint_as_float(get_a(o).x); }
   __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return get_a(o).y; }
   __device__ __forceinline__ uint32_t get_pw(uint32_t o) const {
-    return *(const uint32_t*)((const char*)b + (o >> 1));
+    return *(const uint32_t*)((const char*)b + (FB(o, 8 * (W + 1), 107) >> 1));
   }
   // d - tb of the cell's tuple
   __device__ __forceinline__ uint32_t get_delta(uint32_t o) const {
@@ -106,15 +108,18 @@ struct LazyPullCells<W, float> {
   }
   // pw carries the run in its low 12 bits; tb enters as d - delta
   __device__ __forceinline__ void set(uint32_t i, float dd, uint32_t idw, uint32_t pw, float t) {
+    i = FB(i, W + 1, 108);
     a[i] = make_uint2(__float_as_uint(dd), idw);
     b[i] = pw < kLpAbsent ? pw | ((kLpCfMask - (uint32_t)(dd - t)) << kLpCfShift) : pw;
   }
   // the same with delta already known (pw | delta << 12)
   __device__ __forceinline__ void set_packed(uint32_t i, float dd, uint32_t idw, uint32_t pwd) {
+    i = FB(i, W + 1, 109);
     a[i] = make_uint2(__float_as_uint(dd), idw);
     b[i] = pwd;
   }
   __device__ __forceinline__ void set_pop(uint32_t i, uint32_t q) {
+    i = FB(i, W + 1, 110);
     b[i] = (b[i] & 0xFFFFFu) | (q << 20);
   }
 };
@@ -190,7 +195,6 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;
-  unsigned long long ready_seen = 0;  // uniform: labels known staged (streamed batches)
 
   // the batched backtrace of tier P (shortest-path.zig:109-136 / compose-shortest-
   // path.zig:368-380: the path has exactly L arcs, one per layer)
@@ -199,7 +203,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t maxL = 0;
     ChaseJob jb{};
     if (lane < njobs) {
-      jb = S.job[lane];
+      jb = S.job[FB(lane, kLpChase, 111)];
       maxL = jb.L;
     }
     maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
@@ -255,7 +259,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
-  if (lane < (uint32_t)kWords) S.bits[lane] = 0;
+  if (lane < (uint32_t)kWords) S.bits[FB(lane, kWords, 112)] = 0;
   wave_lds_sync();
   uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
 
@@ -294,8 +298,6 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     uint32_t myp = kEmptyKey;
     double myfw = 0.0;
 
-    if (fail == kPathOk && !wait_labels(in, off + L, ready_seen, lp.wd_ticks))
-      fail = kPathInternal;  // (the watchdog: the host never staged its labels)
     uint32_t labs = 0;
     // uniform: the current layer's pop ranks equal its id ranks (layer 0; every layer the
     // sort below finds already in order, or with at most one tuple): the merge's first
@@ -532,7 +534,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           // (a 32-bit OR into the word's half: ~4 lanes of a row share an address instead
           // of ~8, and same-address LDS atomics serialise -- they were all of the kernel's
           // LDS conflict cycles)
-          atomicOr(reinterpret_cast<uint32_t*>(S.bits) + (key >> 5), 1u << (key & 31u));
+          atomicOr(reinterpret_cast<uint32_t*>(S.bits) + FB(key >> 5, 2 * kWords, 113), 1u << (key & 31u));
         }
       }
       wave_lds_sync();
@@ -540,16 +542,16 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       // ---- (P2) id ranks of the next layer: popcount prefix over the first keys ----
       const uint32_t nw = (n_cur * 8 + 63) / 64;
       unsigned long long word = 0;
-      if (lane < nw) word = S.bits[lane];
+      if (lane < nw) word = S.bits[FB(lane, kWords, 114)];
       const uint32_t pc = (uint32_t)__popcll(word);
       const uint32_t inc = wave_incl_scan_dpp(pc);
       const uint32_t n_next = __builtin_amdgcn_readlane(inc, 63);
       if (lane < nw) {
         // per 32-bit half: {popcount of the keys before it, its bits}, so P3's lookup is one
         // 32-bit mask and count
-        S.pre[lane] = make_uint4(inc - pc, (uint32_t)word,
+        S.pre[FB(lane, kWords, 115)] = make_uint4(inc - pc, (uint32_t)word,
                                  inc - pc + (uint32_t)__popc((uint32_t)word), (uint32_t)(word >> 32));
-        S.bits[lane] = 0;
+        S.bits[FB(lane, kWords, 116)] = 0;
       }
       wave_lds_sync();
       // an uncertified tuple: the rounds engine takes the string
@@ -577,7 +579,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         uint32_t rank = 0;
         if ((uint32_t)e < rows_n) {
           const uint32_t key = pres ? fst[e] >> 17 : 0u;
-          const uint2 p = reinterpret_cast<const uint2*>(S.pre)[key >> 5];
+          const uint2 p = reinterpret_cast<const uint2*>(S.pre)[FB(key >> 5, 2 * kWords, 117)];
           rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
         }
         // pop rank: identity until the sort below fills it in
@@ -595,7 +597,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         // (f32 cells: the distance's bits, ordered as the non-negative distances are; P4
         // rebuilds the slots from the cells' id-rank words when the layer needs its sort)
-        if (pres && sort) S.ord0[rank] = F32 ? __float_as_uint((float)dx) : i;
+        if (pres && sort) S.ord0[FB(rank, W, 118)] = F32 ? __float_as_uint((float)dx) : i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -639,8 +641,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           if ((uint32_t)e >= rows_s) continue;  // uniform
           const uint32_t q = (uint32_t)e * 64 + lane;
           if (q + 1 < n_next) {
-            if constexpr (F32) unsorted |= S.ord0[q] > S.ord0[q + 1];
-            else unsorted |= CL.get_d(8 * S.ord0[q]) > CL.get_d(8 * S.ord0[q + 1]);
+            if constexpr (F32) unsorted |= S.ord0[FB(q, W, 119)] > S.ord0[FB(q + 1, W, 120)];
+            else unsorted |= CL.get_d(8 * S.ord0[FB(q, W, 119)]) > CL.get_d(8 * S.ord0[FB(q + 1, W, 120)]);
           }
         }
         const bool in_order = !__ballot(unsorted);
@@ -652,7 +654,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             if ((uint32_t)e >= rows_n) continue;  // uniform
             const uint32_t i = (uint32_t)e * 64 + lane;
             const uint32_t iw = CL.get_idw(8 * i);
-            if (iw < kLpAbsent) S.ord0[iw >> 20] = i;
+            if (iw < kLpAbsent) S.ord0[FB(iw >> 20, W, 121)] = i;
           }
           wave_lds_sync();
         }
@@ -669,7 +671,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           if ((uint32_t)e >= rows_s) continue;  // uniform
           const uint32_t q = (uint32_t)e * 64 + lane;
           if (q < n_next) {
-            cs[e] = S.ord0[q];
+            cs[e] = S.ord0[FB(q, W, 122)];
             cd[e] = CL.get_d(8 * cs[e]);
             mn = fmin(mn, cd[e]);
             mx = fmax(mx, cd[e]);
@@ -693,7 +695,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           const uint32_t q = (uint32_t)e * 64 + lane;
           if (q < n_next) {
             const uint32_t key = ik ? (uint32_t)(cd[e] - mn) : 0u;  // exact: integers < 2^23
-            S.ord0[q] = (key << 9) | cs[e];
+            S.ord0[FB(q, W, 123)] = (key << 9) | cs[e];
             kacc |= key;
             if constexpr (!F32)  // (f32 cells: integer distances, ik)
               diff |= ik ? 0ull : (unsigned long long)__double_as_longlong((double)cd[e]) ^ mnb;
@@ -720,15 +722,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           // LDS operations complete in order, so the fences below separate the steps.
 #pragma unroll
           for (int b = 0; b < lp_bins<DT>() / 64; ++b) {
-            S.mask[b * 64 + lane] = 0;
-            S.hist[b * 64 + lane] = 0;
+            S.mask[FB(b * 64 + lane, lp_bins<DT>(), 124)] = 0;
+            S.hist[FB(b * 64 + lane, lp_bins<DT>(), 125)] = 0;
           }
           wave_lds_sync();
           uint32_t ck[EW], cw[EW];
 #pragma unroll
           for (int e = 0; e < EW; ++e) {  // every row's (key, slot) in one LDS round trip
             ck[e] = 0;
-            if ((uint32_t)e < rows_s && (uint32_t)e * 64 + lane < n_next) ck[e] = S.ord0[e * 64 + lane];
+            if ((uint32_t)e < rows_s && (uint32_t)e * 64 + lane < n_next) ck[e] = S.ord0[FB(e * 64 + lane, W, 126)];
           }
 #pragma unroll
           for (int e = 0; e < EW; ++e) {
@@ -737,16 +739,16 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t q = (uint32_t)e * 64 + lane;
             const bool valid = q < n_next;
             const uint32_t key = ck[e] >> 9;
-            if (valid) atomicOr(&S.mask[key], 1ull << lane);
+            if (valid) atomicOr(&S.mask[FB(key, lp_bins<DT>(), 127)], 1ull << lane);
             wave_lds_sync();
-            const unsigned long long peers = valid ? S.mask[key] : 0ull;
-            const uint32_t hb = valid ? S.hist[key] : 0u;
+            const unsigned long long peers = valid ? S.mask[FB(key, lp_bins<DT>(), 128)] : 0ull;
+            const uint32_t hb = valid ? S.hist[FB(key, lp_bins<DT>(), 129)] : 0u;
             wave_lds_sync();
             const unsigned long long lt = peers & ((1ull << lane) - 1ull);
             cw[e] = hb + (uint32_t)__popcll(lt);
             if (valid && lt == 0) {  // the key's first lane in this chunk
-              S.hist[key] = hb + (uint32_t)__popcll(peers);
-              S.mask[key] = 0;
+              S.hist[FB(key, lp_bins<DT>(), 130)] = hb + (uint32_t)__popcll(peers);
+              S.mask[FB(key, lp_bins<DT>(), 131)] = 0;
             }
             wave_lds_sync();
           }
@@ -755,23 +757,25 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           // pending chase jobs follow it
           static_assert(lp_bins<DT>() == 256 || lp_bins<DT>() == 128, "bins per lane");
           if constexpr (lp_bins<DT>() == 256) {
-            const uint4 h = reinterpret_cast<const uint4*>(S.hist)[lane];
+            static_assert(4 * 64 == lp_bins<DT>(), "4 bins per lane cover hist exactly");
+            const uint4 h = reinterpret_cast<const uint4*>(S.hist)[FB(lane, lp_bins<DT>() / 4, 132)];
             const uint32_t s4 = h.x + h.y + h.z + h.w;
             const uint32_t ex = wave_incl_scan_dpp(s4) - s4;
-            reinterpret_cast<uint4*>(S.hist)[lane] =
+            reinterpret_cast<uint4*>(S.hist)[FB(lane, lp_bins<DT>() / 4, 133)] =
                 make_uint4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
           } else {
-            const uint2 h = reinterpret_cast<const uint2*>(S.hist)[lane];
+            static_assert(2 * 64 == lp_bins<DT>(), "2 bins per lane cover hist exactly");
+            const uint2 h = reinterpret_cast<const uint2*>(S.hist)[FB(lane, lp_bins<DT>() / 2, 134)];
             const uint32_t s2 = h.x + h.y;
             const uint32_t ex = wave_incl_scan_dpp(s2) - s2;
-            reinterpret_cast<uint2*>(S.hist)[lane] = make_uint2(ex, ex + h.x);
+            reinterpret_cast<uint2*>(S.hist)[FB(lane, lp_bins<DT>() / 2, 135)] = make_uint2(ex, ex + h.x);
           }
           wave_lds_sync();
 #pragma unroll
           for (int e = 0; e < EW; ++e) {  // pop rank -> the cell's high word
             if ((uint32_t)e >= rows_s) continue;
             if ((uint32_t)e * 64 + lane < n_next) {
-              const uint32_t q = S.hist[ck[e] >> 9] + cw[e];
+              const uint32_t q = S.hist[FB(ck[e] >> 9, lp_bins<DT>(), 136)] + cw[e];
               CL.set_pop(ck[e] & 511u, q);
             }
           }
@@ -794,7 +798,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             if ((uint32_t)e >= rows_s) continue;
             const uint32_t q = (uint32_t)e * 64 + lane;
             const bool valid = q < n_next;
-            el[e] = valid ? (cur ? S.ord1 : S.ord0)[q] : 0u;
+            el[e] = valid ? (cur ? S.ord1 : S.ord0)[FB(q, W, 138)] : 0u;
             if (ik) {
               v[e] = (el[e] >> bit) & 1u;
             } else {
@@ -817,7 +821,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t below1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(o >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)o, 0u));
             const uint32_t dst = v[e] ? Z + ob + below1 : zb + below0;
-            if (valid) (cur ? S.ord0 : S.ord1)[dst] = el[e];
+            if (valid) (cur ? S.ord0 : S.ord1)[FB(dst, W, 139)] = el[e];
             zb += (uint32_t)__popcll(z[e]);
             ob += (uint32_t)__popcll(o);
           }
@@ -825,10 +829,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           wave_lds_sync();
         }
         for (uint32_t q = lane; q < n_next && !counting; q += 64) {  // pop rank q -> cell
-          CL.set_pop((cur ? S.ord1 : S.ord0)[q] & 511u, q);
+          CL.set_pop((cur ? S.ord1 : S.ord0)[FB(q, W, 140)] & 511u, q);
         }
         wave_lds_sync();
-        if (!counting && lane < (uint32_t)kWords) S.bits[lane] = 0;  // (ord1 overlays bits)
+        if (!counting && lane < (uint32_t)kWords) S.bits[FB(lane, kWords, 137)] = 0;  // (ord1 overlays bits)
         wave_lds_sync();
         }  // !in_order
         io = in_order;
@@ -850,7 +854,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       wave_lds_sync();
 #pragma unroll 1
       for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
-      if (lane < (uint32_t)kWords) S.bits[lane] = 0;
+      if (lane < (uint32_t)kWords) S.bits[FB(lane, kWords, 112)] = 0;
       wave_lds_sync();
       wlast = 0;
       if (lane == 0) write_status(out, si, fail, tuples, relax);
@@ -879,7 +883,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       continue;
     }
     if (lane == 0) {
-      ChaseJob& j = S.job[njobs];
+      ChaseJob& j = S.job[FB(njobs, kLpChase, 141)];
       j.si = si;
       j.L = L;
       j.id = base + (bp & 511u);
