@@ -1006,9 +1006,15 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     R.cv.notify_all();
   });
   {
-    const uint64_t T = total >= (1u << 20) ? 3 : 1;  // the result's ilabels
+    // the result's ilabels, once the uploads are staged: the runtime's staging copies of
+    // a pageable source read the same pages, and the kernels wait for them, not for these
+    const uint64_t T = total >= (1u << 20) ? 3 : 1;
     for (uint64_t t = 0; t < T; ++t)
       Th.th.emplace_back([&, t, T] {
+        {
+          std::unique_lock<std::mutex> g(R.mu);
+          R.cv.wait(g, [&] { return R.failed || R.n == parts; });
+        }
         const uint64_t a = total * t / T, z = total * (t + 1) / T;
         if (z > a) std::memcpy(out->ilabels + a, src + a, (z - a) * 4);
       });
@@ -1020,6 +1026,9 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     LaunchStats st;
   };
   std::vector<PartRun> pr(parts);
+  // (A/B timing only: FSTAMD_STREAM_AB=1 drops the copy-out; the result then lacks paths)
+  const char* abe = std::getenv("FSTAMD_STREAM_AB");
+  const bool ab_nocopy = abe && std::atoi(abe) == 1;
   auto drive = [&](DeviceEngine::Lease& E, hipStream_t s, size_t p0, size_t step) {
     if (hipSetDevice(dev) != hipSuccess) {
       pr[p0].err = FST_INVALID_ARG;
@@ -1044,6 +1053,7 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
       v.slots = (const uint64_t*)d_off.p + s0;
       v.host_ol = out->olabels;
       v.host_w = out->weights;
+      if (ab_nocopy) v.host_ol = nullptr, v.host_w = nullptr;
       v.first_status = (int32_t*)d_first.p + s0;
       if (hipStreamWaitEvent(s, K.ev[p], 0) != hipSuccess ||
           E->run_chain(*D, in, n, semantics, v, s, &pr[p].st) != hipSuccess ||
