@@ -948,11 +948,25 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     poff[num] = total;
   }
 
-  // ---- parts: string ranges cut at 1/43 and 7/43 of the labels (small batches: one) ----
+  // ---- parts: string ranges cut at these fractions of the labels (per mille; small
+  // batches: one part): 1/43 and 7/43, so each part's upload fits in the previous part's
+  // compute.  FSTAMD_STREAM_CUTS overrides (A/B, one box: "23,163" 30.9 ms per 1M metric
+  // strings, "167" 31.2, "100,400" 31.0, "125" 31.5) ----
   std::vector<uint32_t> cut{0};
   if (total >= (1u << 22) && num >= (1u << 15)) {
-    for (uint64_t f : {1ull, 7ull}) {
-      const uint64_t want = total * f / 43;
+    std::vector<uint64_t> pm{23, 163};
+    if (const char* ce = std::getenv("FSTAMD_STREAM_CUTS")) {
+      pm.clear();
+      for (const char* q = ce; *q;) {
+        char* e = nullptr;
+        const unsigned long v = std::strtoul(q, &e, 10);
+        if (e == q) break;
+        if (v > 0 && v < 1000) pm.push_back(v);
+        q = *e ? e + 1 : e;
+      }
+    }
+    for (uint64_t f : pm) {
+      const uint64_t want = total * f / 1000;
       const uint32_t i = (uint32_t)(std::upper_bound(poff, poff + num, want) - poff);
       if (i > cut.back() && i < num) cut.push_back(i);
     }
@@ -1055,14 +1069,11 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
       v.host_w = out->weights;
       if (ab_nocopy) v.host_ol = nullptr, v.host_w = nullptr;
       v.first_status = (int32_t*)d_first.p + s0;
+      // (no download here: a copy is a blit kernel, and one queued on this stream before
+      // the next part's launch would wait for CU slots the other engine's persistent kernel
+      // holds -- the downloads come after the last part)
       if (hipStreamWaitEvent(s, K.ev[p], 0) != hipSuccess ||
-          E->run_chain(*D, in, n, semantics, v, s, &pr[p].st) != hipSuccess ||
-          hipMemcpyAsync(out->status + s0, v.status, np * 4ull, hipMemcpyDeviceToHost, s) !=
-              hipSuccess ||
-          hipMemcpyAsync(out->final_weights + s0, v.final_w, np * 8ull, hipMemcpyDeviceToHost,
-                         s) != hipSuccess ||
-          hipMemcpyAsync(first.data() + s0, v.first_status, np * 4ull, hipMemcpyDeviceToHost,
-                         s) != hipSuccess) {
+          E->run_chain(*D, in, n, semantics, v, s, &pr[p].st) != hipSuccess) {
         pr[p].err = FST_OOM;
         return;
       }
@@ -1075,6 +1086,15 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     drive(EA, sA, 0, EB ? 2 : 1);
     P.join();
   }
+  // every part's kernels are done (run_chain synchronises): statuses, final weights and
+  // the pull tier's statuses in one download each
+  if (num && (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost, sA) !=
+                  hipSuccess ||
+              hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost,
+                             sA) != hipSuccess ||
+              hipMemcpyAsync(first.data(), d_first.p, num * 4ull, hipMemcpyDeviceToHost, sA) !=
+                  hipSuccess))
+    return FST_OOM;
   for (hipStream_t x : {up, sA, sB})
     if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
   Th.join();

@@ -76,6 +76,18 @@ def main():
             print(json.dumps({"ab": ab, "ms": float(np.median(ts[1:]) * 1e3),
                               "kernel_ms": float(np.median(ks[1:]))}), flush=True)
         os.environ.pop("FSTAMD_STREAM_AB")
+    if "--cuts" in sys.argv:  # streamed-batch part cuts (FSTAMD_STREAM_CUTS), timing only
+        for cuts in ("167", "23,163", "125", "200", "167", "100,400"):
+            os.environ["FSTAMD_STREAM_CUTS"] = cuts
+            ts = []
+            for i in range(6):
+                t0 = time.perf_counter()
+                r = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, 0)
+                ts.append(time.perf_counter() - t0)
+                assert r.status[0] == F.FST_PATH_OK
+                del r
+            print(json.dumps({"cuts": cuts, "ms": float(np.median(ts[1:]) * 1e3)}), flush=True)
+        os.environ.pop("FSTAMD_STREAM_CUTS")
     for i in range(6):
         t0 = time.perf_counter()
         r = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, 0)
