@@ -578,6 +578,82 @@ struct HostProf {
 };
 thread_local HostProf* t_prof = nullptr;
 
+// ---- Small batches: the coalesced single calls (one utterance each) and small host
+// batches.  Per call the regular path costs ~10 uploads / downloads / synchronisations of
+// ~10-25 us each beside a ~160 us kernel (WeText-scale tagger, profiles/r05/s2): here the
+// inputs go up in one copy from one pinned block, the outputs live in one device block
+// that comes down in one copy (the whole arena: it is small), and the only host waits are
+// the engines' own routing reads and that final download.  A result the arena could not
+// hold (OUTPUT_FULL) reruns on the regular path.
+constexpr uint64_t kSmallLabels = 1u << 16;
+constexpr uint32_t kSmallStrings = 1u << 12;
+constexpr int kSmallRetry = -2;
+
+int run_small_batch(DeviceEngine::Lease& E, DeviceFst& D, const uint32_t* labels,
+                    const uint64_t* offsets, uint32_t num, uint64_t total, uint32_t max_len,
+                    uint32_t n, int semantics, HostPaths* h) {
+  const hipStream_t stream = E.stream();
+  const uint64_t cap = std::max<uint64_t>((D.has_eps ? 4 : 1) * total + 16, 1024);
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  // device block: inputs [offsets | labels], then outputs [status | len | off | fin |
+  // cursor | il | ol | w], each region 256-B aligned
+  const uint64_t o_off = 0, o_lab = al((num + 1) * 8ull), in_bytes = o_lab + total * 4;
+  const uint64_t o_st = al(in_bytes), o_len = o_st + al(num * 4ull), o_po = o_len + al(num * 4ull),
+                 o_fin = o_po + al(num * 8ull), o_cur = o_fin + al(num * 8ull),
+                 o_il = o_cur + 256, o_ol = o_il + al(cap * 4), o_w = o_ol + al(cap * 4),
+                 end = o_w + cap * 8;
+  DevBuf blk(end);
+  PinnedVec<uint8_t> hin(in_bytes), hout(end - o_st);
+  if (!blk.p) return FST_OOM;
+  uint64_t* ho = (uint64_t*)(hin.data() + o_off);
+  for (uint32_t i = 0; i <= num; ++i) ho[i] = offsets[i] - offsets[0];
+  if (total) std::memcpy(hin.data() + o_lab, labels + offsets[0], total * 4);
+  uint8_t* p = (uint8_t*)blk.p;
+  if (hipMemcpyAsync(p, hin.data(), in_bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
+    return FST_OOM;
+  ChainInput in{(const uint32_t*)(p + o_lab), (const uint64_t*)(p + o_off), num, max_len};
+  BatchOutDev v{(int32_t*)(p + o_st), (uint32_t*)(p + o_len), (uint64_t*)(p + o_po),
+                (double*)(p + o_fin), (uint32_t*)(p + o_il), (uint32_t*)(p + o_ol),
+                (double*)(p + o_w), cap, (unsigned long long*)(p + o_cur), nullptr};
+  if (t_prof) t_prof->lap(0);
+  LaunchStats st;
+  st.defer = true;  // (kernel time read after the download's synchronisation)
+  if (E->run_chain(D, in, n, semantics, v, stream, &st) != hipSuccess ||
+      hipMemcpyAsync(hout.data(), p + o_st, end - o_st, hipMemcpyDeviceToHost, stream) !=
+          hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return FST_OOM;
+  (void)E->finish_deferred(&st);
+  t_last_stats = st;
+  if (t_prof) {
+    t_prof->lap(2);
+    ++t_prof->runs;
+  }
+  const uint8_t* q = hout.data() - o_st;  // (offsets below are block offsets)
+  const int32_t* status = (const int32_t*)(q + o_st);
+  for (uint32_t i = 0; i < num; ++i)
+    if (status[i] == kPathOutputFull) return kSmallRetry;
+  const uint64_t used = std::min<uint64_t>(*(const uint64_t*)(q + o_cur), cap);
+  h->status.resize(num);
+  h->len.resize(num);
+  h->off.resize(num);
+  h->fin.resize(num);
+  h->il.resize(used);
+  h->ol.resize(used);
+  h->w.resize(used);
+  std::memcpy(h->status.data(), status, num * 4ull);
+  std::memcpy(h->len.data(), q + o_len, num * 4ull);
+  std::memcpy(h->off.data(), q + o_po, num * 8ull);
+  std::memcpy(h->fin.data(), q + o_fin, num * 8ull);
+  if (used) {
+    std::memcpy(h->il.data(), q + o_il, used * 4);
+    std::memcpy(h->ol.data(), q + o_ol, used * 4);
+    std::memcpy(h->w.data(), q + o_w, used * 8);
+  }
+  if (t_prof) t_prof->lap(3);
+  return FST_OK;
+}
+
 // The call runs on the engine `E` leases (its stream; E->dev() is the device).
 FstError run_chain_batch_host(DeviceEngine::Lease& E, FrozenFst& b, const uint32_t* labels,
                               const uint64_t* offsets, uint32_t num, uint32_t n, int semantics,
@@ -591,6 +667,10 @@ FstError run_chain_batch_host(DeviceEngine::Lease& E, FrozenFst& b, const uint32
   uint32_t max_len = 0;
   for (uint32_t i = 0; i < num; ++i)
     max_len = std::max<uint32_t>(max_len, (uint32_t)(offsets[i + 1] - offsets[i]));
+  if (!keep && num && total <= kSmallLabels && num <= kSmallStrings) {
+    const int r = run_small_batch(E, *D, labels, offsets, num, total, max_len, n, semantics, h);
+    if (r != kSmallRetry) return (FstError)r;
+  }
   std::vector<uint64_t> rebased(num + 1);
   for (uint32_t i = 0; i <= num; ++i) rebased[i] = offsets[i] - offsets[0];
   DevBuf d_lab(total * 4), d_off((num + 1) * 8ull);
@@ -1414,11 +1494,20 @@ void run_chain_calls(int dev, std::vector<ChainCall*>& calls) {
                 labels.begin() + offs[i]);
     HostPaths h;
     FstError e = FST_INVALID_ARG;
+    HostProf prof;  // FSTAMD_HOST_PROF=1: the phases of this coalesced batch
+    t_prof = prof.on ? &prof : nullptr;
     {
       DeviceEngine::Lease E = DeviceEngine::acquire(dev);
       if (E)
         e = run_chain_batch_host(E, *calls[g0]->rhs, labels.data(), offs.data(), num,
                                  calls[g0]->n, FST_SEM_LAZY, &h);
+    }
+    if (t_prof) {
+      prof.lap(5);
+      char what[96];
+      std::snprintf(what, sizeof(what), "chain call batch (%u string(s))", num);
+      prof.print(what);
+      t_prof = nullptr;
     }
     for (uint32_t i = 0; i < num; ++i) {
       ChainCall* c = calls[g0 + i];

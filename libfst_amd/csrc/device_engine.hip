@@ -552,7 +552,7 @@ __global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_
                                     uint32_t* count);
 
 static hipError_t finish_stats(hipEvent_t e0, hipEvent_t e1, LaunchStats* stats) {
-  if (!stats) return hipSuccess;
+  if (!stats || stats->defer) return hipSuccess;  // (defer: DeviceEngine::finish_deferred)
   HIP_TRY(hipEventSynchronize(e1));
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
@@ -569,6 +569,15 @@ bool DeviceEngine::pull_first(const DeviceFst& rhs, int semantics) {
   const char* le = std::getenv("FSTAMD_LAZY_ENGINE");  // the lazy dispatch below: use_lp
   if (le && *le) return false;
   return rhs.nonneg && rhs.finite && rhs.lazy_pull_ok;
+}
+
+hipError_t DeviceEngine::finish_deferred(LaunchStats* stats) {
+  if (!stats || !stats->defer) return hipSuccess;
+  float ms = 0.f;
+  const hipError_t e = hipEventElapsedTime(&ms, ev0_, ev1_);
+  stats->kernel_ms = e == hipSuccess ? ms : 0.0;
+  stats->defer = false;
+  return e;
 }
 
 hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
@@ -955,6 +964,11 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
                      "to the dense replay %u\n",
                      num, cnt[0], cnt[1], todo_n);
     }
+    // the LDS (and hashed) replays took every string: they leave none UNSUPPORTED, so there
+    // is nothing for the band, dense or general engines -- and the general engine's count
+    // readback would cost the call a synchronisation (the band and dense replays do mark
+    // strings UNSUPPORTED, so this holds only when neither runs)
+    const bool all_done = small && todo_n == 0;
     bool ran = true;
     if (todo_n > 0) {
       // the band replay first (rhs whose arcs all go forward: config 3), the dense replay
@@ -991,7 +1005,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       if (stats) stats->launches += 1;
     }
     if (stats && !ran) stats->engine = 3;  // too large for the dense engine: rounds only
-    if (!std::getenv("FSTAMD_DENSE_NOFALLBACK"))  // debug: leave UNSUPPORTED strings
+    if (!std::getenv("FSTAMD_DENSE_NOFALLBACK") && !all_done)  // debug: leave UNSUPPORTED
       HIP_TRY(run_bfs_chain(rhs, in, n, out, stream, !ran && !small, true));
     if (stats) {
       HIP_TRY(hipEventRecord(ev1_, stream));
@@ -1935,9 +1949,13 @@ hipError_t DeviceEngine::compose_lattice(const DeviceFst& rhs, const GraphInput&
   // until it overflows a small tier (config 1: 781K tuples, 78 ms lost in tier 1).
   const uint64_t bound = (uint64_t)lhs.num_states * rhs.view.num_states *
                          (1u + (rhs.has_eps ? 1u : 0u) + (lhs.eps_out ? 1u : 0u));
+  // The bound is trusted only up to 1M tuples: a large sparse rhs (a WeText-scale tagger,
+  // 0.43 M states) makes it ~14 M for a 15-label utterance whose lattice has ~140 tuples,
+  // and clearing that tier's tables cost 17.7 ms per fst_compose_frozen call; such lattices
+  // start at the first tier and grow on overflow.
   int tier0 = 1;
-  while (bfs_caps(tier0).ncap < bound && bfs_caps(tier0 + 1).stride <= kBfsBudget &&
-         bfs_caps(tier0).ncap < (1u << 30))
+  while (bound <= (1u << 20) && bfs_caps(tier0).ncap < bound &&
+         bfs_caps(tier0 + 1).stride <= kBfsBudget && bfs_caps(tier0).ncap < (1u << 30))
     ++tier0;
   // One 1024-thread workgroup: the ~4,200 BFS levels of config 1 are ~190 tuples wide
   // (kernel 182 vs 214 ms with 256 threads).  FSTAMD_LATTICE_WG=256 for A/B runs.

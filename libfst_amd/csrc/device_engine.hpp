@@ -233,6 +233,9 @@ struct LaunchStats {
   uint32_t launches = 0;
   uint32_t engine = 0;
   uint32_t grid = 0;
+  // set by the caller: run_chain records its events but does not wait for them; the caller
+  // synchronises the stream itself and then calls DeviceEngine::finish_deferred
+  bool defer = false;
 };
 
 // ---- pull tier (eager_pull.hip, kernels/eager_pull.hpp) ----
@@ -315,6 +318,8 @@ class DeviceEngine {
   // paths out (BatchOutDev::host_ol), so the streamed host batch needs it.  run_chain
   // refuses streamed inputs otherwise.
   static bool pull_first(const DeviceFst& rhs, int semantics);
+  // kernel_ms of a deferred LaunchStats, once the caller has synchronised the stream
+  hipError_t finish_deferred(LaunchStats* stats);
   hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
   // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp), on
