@@ -927,19 +927,49 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       }
       if (first128 && num >= 1024 && (uint64_t)cnt[0] * 3 > (uint64_t)num)
         rhs.tiny_lazy_256.store(1, std::memory_order_relaxed);
+      if (first128 && num < 1024) {  // small batches: the same rule over their sum
+        const uint64_t seen = rhs.tiny_lazy_seen.fetch_add(num) + num;
+        const uint64_t over = rhs.tiny_lazy_over.fetch_add(cnt[0]) + cnt[0];
+        if (seen >= 1024 && over * 3 > seen) rhs.tiny_lazy_256.store(1, std::memory_order_relaxed);
+      }
       if (first128 && num >= 64 && (uint64_t)cnt[0] * 10 > (uint64_t)num * 9)
         rhs.skip_tiny_lazy.store(1, std::memory_order_relaxed);
       todo = lb;
       todo_n = cnt[1];
+      uint32_t* rest = lb;             // the strings still OVERFLOW, and their count (device)
+      unsigned int* rest_cnt = c + 3;
+      uint32_t* spare = la;
+      unsigned int* spare_cnt = c + 1;
+      // Larger LDS sizes for the outliers of the LDS replays, or for every string of a small
+      // batch (a coalesced single call: a long utterance, ~400-900 tuples, went to the dense
+      // replay's HBM index -- 2.7 ms for 63 labels of the WeText-scale tagger): 512 tuples
+      // (~55 KB, 2 waves per CU), then 1024 (~110 KB, 1 per CU), one string per wave.
+      uint32_t cnt_big[2] = {0, 0};
+      for (int t = 3; t <= 4 && todo_n > 0 && ((uint64_t)todo_n * 4 <= num || num <= 64); ++t) {
+        unsigned int* ci = counter + 48 + 2 * (t - 3);  // [48|50] items, [49|51] |next list|
+        HIP_TRY(hipMemsetAsync(ci, 0, 8, stream));
+        HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, t, rest, todo_n, ci, &g));
+        collect_list_kernel<<<(todo_n + 255) / 256, 256, 0, stream>>>(rest, rest_cnt, out.status,
+                                                                      kPathOverflow, spare, ci + 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&todo_n, ci + 1, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        cnt_big[t - 3] = todo_n;
+        std::swap(rest, spare);
+        spare_cnt = rest_cnt;
+        rest_cnt = ci + 1;
+        todo = rest;
+        if (stats) stats->launches += 1;
+      }
       // The LDS replays took most strings (>= 3/4): the rest are small-lattice outliers,
       // served by the hashed replay (HBM tables sized by the lattice, x8 per retry) rather
       // than by the dense index sized by (L + 1) * NS (a WeText-scale tagger: 1.6 GB per
       // wave).  When they took few (large lattices), the dense replay takes the rest.
       if (todo_n > 0 && (uint64_t)todo_n * 4 <= num) {
-        uint32_t* cur = lb;
-        unsigned int* cur_cnt = c + 3;
-        uint32_t* nxt = la;
-        unsigned int* nxt_cnt = c + 1;
+        uint32_t* cur = rest;
+        unsigned int* cur_cnt = rest_cnt;
+        uint32_t* nxt = spare;
+        unsigned int* nxt_cnt = spare_cnt;
         uint64_t want = 4096;
         for (int t = 0; t < 4 && todo_n > 0; ++t, want *= 8) {
           HIP_TRY(hipMemsetAsync(c + 4, 0, 4, stream));  // [44] item counter
@@ -961,8 +991,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       if (std::getenv("FSTAMD_ROUTE_LOG"))
         std::fprintf(stderr,
                      "[libfst_amd route] lazy: %u strings, LDS-128 handed on %u, LDS-256 %u, "
-                     "to the dense replay %u\n",
-                     num, cnt[0], cnt[1], todo_n);
+                     "LDS-512 %u, LDS-1024 %u, to the dense replay %u\n",
+                     num, cnt[0], cnt[1], cnt_big[0], cnt_big[1], todo_n);
     }
     // the LDS (and hashed) replays took every string: they leave none UNSUPPORTED, so there
     // is nothing for the band, dense or general engines -- and the general engine's count
@@ -1320,15 +1350,22 @@ hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& i
   ws.stamp_base = 0;  // stamps from 1 per launch: the LDS table starts zeroed
   ws.max_pops = ws.qcap + 1;
   ws.wd_ticks = watchdog_ticks();
-  const int occ = tier == 1 ? lazy_tiny_per_cu<1>() : lazy_tiny_per_cu<2>();
+  const int occ = tier == 1 ? lazy_tiny_per_cu<1>() : tier == 2 ? lazy_tiny_per_cu<2>()
+                 : tier == 3 ? lazy_tiny_per_cu<3>() : lazy_tiny_per_cu<4>();
   const uint32_t grid =
       (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(num_items, 1u));
   GraphInput none{};
   if (tier == 1)
     lazy_wave_kernel<false, 1><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
                                                          num_items, ws, out);
-  else
+  else if (tier == 2)
     lazy_wave_kernel<false, 2><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
+                                                         num_items, ws, out);
+  else if (tier == 3)
+    lazy_wave_kernel<false, 3><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
+                                                         num_items, ws, out);
+  else
+    lazy_wave_kernel<false, 4><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
                                                          num_items, ws, out);
   HIP_TRY(hipGetLastError());
   if (grid_out) *grid_out = grid;

@@ -132,6 +132,9 @@ struct DeviceFst {
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};
   // ... and one whose 128-tuple LDS size handed on over a third of a batch starts at 256
   mutable std::atomic<int> tiny_lazy_256{0}, tiny_eager_256{0};
+  // ... counted over small batches too (coalesced single calls: batches of a few strings
+  // never reach the per-batch thresholds): strings the 128-tuple LDS replay saw / handed on
+  mutable std::atomic<uint64_t> tiny_lazy_seen{0}, tiny_lazy_over{0};
   RevView rev{};
   void* rev_bufs[9] = {};
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a

@@ -304,13 +304,15 @@ struct LazyLds {
 // Two LDS sizes: kTiny 1 = 128 tuples (~15 KB, 10 waves per CU), 2 = 256 tuples (~29 KB,
 // 5 per CU) for what outgrows the first (a WeText-scale tagger's utterances: ~140 tuples on
 // average, ~300 at most, libfst_amd/wetext_standin.py).
-constexpr uint32_t lz_tiny_n(int t) { return t == 1 ? 128u : 256u; }
+// Round 5: 3 = 512 tuples (~55 KB, 2 waves per CU) and 4 = 1024 (~110 KB, 1 per CU) for the
+// long utterances of small batches (coalesced single calls), DeviceEngine::run_chain.
+constexpr uint32_t lz_tiny_n(int t) { return 64u << t; }
 constexpr uint32_t lz_tiny_h(int t) { return 2 * lz_tiny_n(t); }
 constexpr uint32_t lz_tiny_q(int t) { return 3 * lz_tiny_n(t); }
 constexpr uint32_t kLzTinyN = lz_tiny_n(1), kLzTinyH = lz_tiny_h(1), kLzTinyQ = lz_tiny_q(1);
 
 template <bool kGraph, int kTiny = 0>
-__global__ void __launch_bounds__(64, kTiny == 1 ? 3 : kTiny == 2 ? 1 : FSTAMD_REPLAY_WAVES)
+__global__ void __launch_bounds__(64, kTiny == 1 ? 3 : kTiny >= 2 ? 1 : FSTAMD_REPLAY_WAVES)
 lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, uint32_t num_items, LazyWs ws,
                  BatchOutDev out) {

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--utt", type=int, default=0)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--sweep", type=int, default=0,
+                    help="also time the first N utterances (20 calls each): length vs latency")
     a = ap.parse_args()
     tag = W.tagger()
     rhs = F.Fst.from_bytes(W.freeze_blob(tag))
@@ -49,6 +51,25 @@ def main():
                       "median_us": float(np.median(ts)) * 1e6,
                       "p10_us": float(np.percentile(ts, 10)) * 1e6,
                       "p90_us": float(np.percentile(ts, 90)) * 1e6}), flush=True)
+    if a.sweep:
+        rows = []
+        for u in range(a.sweep):
+            lb = labels[int(offsets[u]):int(offsets[u + 1])]
+            x = F.MutableFst.compile_string(bytes((lb - 1).astype(np.uint8).tolist()))
+            F.compose_frozen_shortest_path(x, rhs, 1)
+            tt = []
+            for _ in range(20):
+                t0 = time.perf_counter()
+                F.compose_frozen_shortest_path(x, rhs, 1)
+                tt.append(time.perf_counter() - t0)
+            rows.append((int(len(lb)), float(np.median(tt)) * 1e6, F.last_launch_stats().kernel_ms))
+        rows.sort()
+        lens = np.array([r[0] for r in rows])
+        us = np.array([r[1] for r in rows])
+        print(json.dumps({"sweep": a.sweep, "mean_len": float(lens.mean()),
+                          "mean_us": float(us.mean()), "median_us": float(np.median(us)),
+                          "by_len": [[r[0], round(r[1], 1), round(r[2] * 1e3, 1)] for r in rows]}),
+              flush=True)
     os.environ["FSTAMD_HOST_PROF"] = "1"
     call()
 
