@@ -22,6 +22,7 @@
 #include "kernels/eager_wave.hpp"
 #include "kernels/eager_window.hpp"
 #include "kernels/lazy_wave.hpp"
+#include "kernels/lazy_tiny.hpp"
 
 #define HIP_TRY(x)                              \
   do {                                          \
@@ -1325,12 +1326,22 @@ hipError_t DeviceEngine::launch_lazy_hashed(const DeviceFst& rhs, const ChainInp
 }
 
 namespace {
+// FSTAMD_TINY_OLD=1: the LDS replays of round 5 (lazy_wave_kernel's tiny tiers, 108 B per
+// tuple) instead of lazy_tiny_kernel (36 B), for A/B runs
+bool tiny_old() {
+  static const bool v = [] {
+    const char* e = std::getenv("FSTAMD_TINY_OLD");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  return v;
+}
 template <int T>
 int lazy_tiny_per_cu() {  // resident LDS-replay waves per CU, asked of the runtime once
   static const int occ = [] {
     int o = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &o, (const void*)lazy_wave_kernel<false, T>, 64, 0) != hipSuccess)
+            &o, tiny_old() ? (const void*)lazy_wave_kernel<false, T>
+                           : (const void*)lazy_tiny_kernel<T>, 64, 0) != hipSuccess)
       o = 1;
     return std::max(o, 1);
   }();
@@ -1355,7 +1366,16 @@ hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& i
   const uint32_t grid =
       (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(num_items, 1u));
   GraphInput none{};
-  if (tier == 1)
+  if (!tiny_old()) {
+    if (tier == 1)
+      lazy_tiny_kernel<1><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
+    else if (tier == 2)
+      lazy_tiny_kernel<2><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
+    else if (tier == 3)
+      lazy_tiny_kernel<3><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
+    else
+      lazy_tiny_kernel<4><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
+  } else if (tier == 1)
     lazy_wave_kernel<false, 1><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
                                                          num_items, ws, out);
   else if (tier == 2)

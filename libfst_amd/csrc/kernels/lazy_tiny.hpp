@@ -1,0 +1,568 @@
+// lazy_tiny.hpp -- composeShortestPath (FST_SEM_LAZY) for small lattices with every table of
+// the string in LDS: the first engine of the lazy chain batch (config 4's tagger and
+// verbalizer, coalesced single calls).
+//
+// Replaces src/ops/compose-shortest-path.zig:26-401 for one linear-chain lhs per wavefront,
+// like lazy_wave.hpp (its candidate enumeration, first-touch id assignment and lane-order
+// folding are shared and documented there), but laid out for occupancy: the replay waits
+// on two dependent rhs reads per pop, so the rate is resident strings per CU, and that is
+// LDS per string.  36 B per tuple instead of lazy_wave's 108 B:
+//  * hash slots are one word, (generation << 16) | id; the key is checked in nkey[id].  The
+//    generation advances per string (the table is cleared when it wraps), so nothing is
+//    cleared between strings;
+//  * the back pointer is 8 B: {prev id | flags, rhs arc index}.  The ilabel is the popped
+//    tuple's lhs label when the move consumed it (phases 1, 2, 4) and epsilon otherwise;
+//    the olabel and the weight are the rhs arc's (phase 2 has none: epsilon, One), read
+//    back from the frozen rhs when the path is written -- the tie-break of :110-128 needs
+//    the olabel only on an exact tie from the same pop and then reads it;
+//  * the queue is an indexed 64-ary heap of ids (2 B) with positions (2 B) and
+//    decrease-key, keyed by (dist[id], id).  Its pop order is the reference's lazy-deletion
+//    binary heap's: both pop the minimum (dist, id) over the ids pushed and not yet
+//    settled -- a stale entry of the lazy heap has a dist above dist[id], a settled id
+//    is skipped there and absent here -- so the ids, the paths and the weights are the
+//    same bits.  Heap size <= tuples: no queue overflow.
+// Sizes: tier t holds 64 << t tuples; 1 (128) = 6.1 KB, 2 (256) = 10.7 KB, 3 (512) = 19.9
+// KB, 4 (1024) = 38.4 KB.  A string that outgrows its tier ends OVERFLOW and the host reruns
+// it in the next (DeviceEngine::run_chain).
+#pragma once
+
+#include "lazy_wave.hpp"
+
+namespace fstamd {
+
+constexpr uint32_t kTyNone = 0xFFFFu;       // pos[] of an id not in the heap
+constexpr uint32_t kTyPrev = 0xFFFFu;       // nback.x bits 0..15: the previous tuple's id
+constexpr uint32_t kTySettled = 1u << 16;
+constexpr uint32_t kTyHasBack = 1u << 17;
+constexpr uint32_t kTyConsumed = 1u << 18;  // the move read the lhs label (phases 1, 2, 4)
+constexpr uint32_t kTyArc = 1u << 19;       // nback.y is an rhs arc index (not phase 2)
+
+template <int kTier>
+struct TinyLds {
+  static constexpr uint32_t N = lz_tiny_n(kTier), H = 2 * N;
+  unsigned long long nkey[N];  // (s2 << 32) | (s1 << 2) | filter
+  double ndist[N];
+  double cnd[64];              // one chunk's candidates, read by the group leaders
+  double cw[64];
+  uint2 nback[N];
+  uint32_t hs[H];
+  uint32_t carc[64];
+  uint32_t col[64];
+  uint32_t ccode[64];
+  uint32_t cid[64];
+  uint16_t qid[N];
+  uint16_t pos[N];
+};
+
+struct TyCand {
+  unsigned long long key;
+  uint32_t arc, ol, code;
+  double w;
+};
+
+// chain_cand (lazy_wave.hpp) with the arc index and the phase kept instead of the labels.
+__device__ __forceinline__ TyCand tiny_cand(const RhsView& rhs, const PopCands& P, uint32_t c) {
+  TyCand x;
+  if (c < P.n1) {  // :182-224
+    x.arc = P.lo1 + c;
+    const ArcRec r = rhs.rec[x.arc];
+    x.key = tuple_key(P.s1 + 1, r.next, 0);
+    x.ol = r.olabel;
+    x.w = w_times(w_one(), r.weight);
+    x.code = kTyConsumed | kTyArc;
+    return x;
+  }
+  c -= P.n1;
+  if (c < P.n2) {  // :227-252
+    x.arc = 0;
+    x.key = tuple_key(P.s1 + 1, P.s2, P.f == 0 ? 2u : P.f);
+    x.ol = kEpsilon;
+    x.w = w_one();
+    x.code = kTyConsumed;
+    return x;
+  }
+  c -= P.n2;
+  if (c < P.n3) {  // :254-305
+    x.arc = P.lo3 + c;
+    const ArcRec r = rhs.rec[x.arc];
+    x.key = tuple_key(P.s1, r.next, P.f == 0 ? 1u : P.f);
+    x.ol = r.olabel;
+    x.w = r.weight;
+    x.code = kTyArc;
+    return x;
+  }
+  c -= P.n3;  // :307-365
+  x.arc = P.lo3 + c;
+  const ArcRec r = rhs.rec[x.arc];
+  x.key = tuple_key(P.s1 + 1, r.next, 0);
+  x.ol = r.olabel;
+  x.w = w_times(w_one(), r.weight);
+  x.code = kTyConsumed | kTyArc;
+  return x;
+}
+
+// the olabel of a stored back pointer (phase 2: epsilon)
+__device__ __forceinline__ uint32_t tiny_back_ol(const RhsView& rhs, uint2 b) {
+  return (b.x & kTyArc) ? rhs.rec[b.y].olabel : kEpsilon;
+}
+
+// The relax rule of :110-128 for a candidate (nd, il, ol) from pop `pid` against the
+// target's (od, b): the sequential reference's decision.  bol / bol_known cache b's olabel.
+__device__ __forceinline__ bool tiny_take(const RhsView& rhs, double nd, uint32_t il, uint32_t ol,
+                                          double od, uint2 b, uint32_t pid, uint32_t label,
+                                          uint32_t& bol, bool& bol_known) {
+  if (w_is_zero(od) || nd < od) return true;
+  if (!(nd == od)) return false;
+  if (!(b.x & kTyHasBack)) return true;
+  const uint32_t bp = b.x & kTyPrev;
+  if (pid != bp) return pid < bp;
+  const uint32_t bil = (b.x & kTyConsumed) ? label : kEpsilon;
+  if (il != bil) return il < bil;
+  if (!bol_known) {
+    bol = tiny_back_ol(rhs, b);
+    bol_known = true;
+  }
+  return ol < bol;
+}
+
+// Insert id t with dist d, or move it up after its dist decreased (one lane).
+template <int kTier>
+__device__ __forceinline__ void tiny_heap_update(TinyLds<kTier>& S, uint32_t& qn, uint32_t t,
+                                                 double d) {
+  uint32_t q = S.pos[t];
+  if (q == kTyNone) q = qn++;
+  while (q > 0) {
+    const uint32_t pq = (q - 1) >> 6;
+    const uint32_t pi = S.qid[pq];
+    if (!qless(d, t, S.ndist[pi], pi)) break;
+    S.qid[q] = (uint16_t)pi;
+    S.pos[pi] = (uint16_t)q;
+    q = pq;
+  }
+  S.qid[q] = (uint16_t)t;
+  S.pos[t] = (uint16_t)q;
+}
+
+template <int kTier>
+__global__ void __launch_bounds__(64, kTier == 1 ? 5 : kTier == 2 ? 4 : kTier == 3 ? 2 : 1)
+lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* next_item,
+                 const uint32_t* items, uint32_t num_items, LazyWs ws, BatchOutDev out) {
+  constexpr uint32_t N = TinyLds<kTier>::N, H = TinyLds<kTier>::H, hmask = H - 1;
+  static_assert(N <= 1024 && (H & (H - 1)) == 0, "ids are 16-bit, the table a power of two");
+  __shared__ TinyLds<kTier> S;
+  const uint32_t lane = lane_id();
+  const size_t w = blockIdx.x;
+  for (uint32_t i = lane; i < H; i += 64) S.hs[i] = 0u;
+  uint32_t gen = 0;  // generation 0 = the cleared table
+  wave_fence();
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool dead = false;
+  uint32_t dbg_pops = 0, dbg_cb = 0, dbg_C = 0, dbg_qn = 0, dbg_nn = 0;
+#define TY_WD(code)                                                                  \
+  if (!dead && wd_expired(t0, ws.wd_ticks)) {                                        \
+    dead = true;                                                                     \
+    if (ws.dbg && lane == 0) {                                                       \
+      uint32_t* d_ = ws.dbg + w * 8;                                                 \
+      d_[0] = (code);                                                                \
+      d_[1] = dbg_pops;                                                              \
+      d_[2] = dbg_cb;                                                                \
+      d_[3] = dbg_C;                                                                 \
+      d_[4] = dbg_qn;                                                                \
+      d_[5] = dbg_nn;                                                                \
+    }                                                                                \
+  }
+
+  for (;;) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(next_item, 1u);
+    item = __shfl(item, 0, 64);
+    if (item >= num_items) break;
+    const uint32_t si = items ? items[item] : item;
+    t0 = __builtin_amdgcn_s_memrealtime();
+    dead = false;
+    if (++gen == 0x10000u) {
+      for (uint32_t i = lane; i < H; i += 64) S.hs[i] = 0u;
+      gen = 1;
+      wave_fence();
+    }
+    const uint64_t off = chain.offsets[si];
+    const ChainLhs cl{chain.labels + off, (uint32_t)(chain.offsets[si + 1] - off)};
+
+    // compose-shortest-path.zig:30-33 (a chain always has a start)
+    if (rhs.start == kNoState || n_best != 1) {
+      if (lane == 0) {
+        out.status[si] = (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN;
+        out.path_len[si] = 0;
+        out.path_off[si] = 0;
+        out.final_w[si] = w_zero();
+        if (out.work) {
+          out.work[2 * si] = 0;
+          out.work[2 * si + 1] = 0;
+        }
+      }
+      continue;
+    }
+
+    // init tuple, id 0 (:146-153)
+    uint32_t nn = 1, qn = 1;
+    if (lane == 0) {
+      const unsigned long long k0 = tuple_key(0, rhs.start, 0);
+      S.nkey[0] = k0;
+      S.ndist[0] = w_one();
+      S.nback[0] = make_uint2(0u, 0u);
+      S.hs[hmix(k0) & hmask] = gen << 16;
+      S.qid[0] = 0;
+      S.pos[0] = 0;
+    }
+    wave_fence();
+
+    uint32_t best_id = kNoState;
+    double best_fw = w_zero(), best_total = w_zero();
+    uint32_t relax_count = 0;
+    int32_t fail = kPathOk;
+    uint32_t pops = 0, pushes = 1;
+    uint32_t wd_work = 256;
+    while (qn > 0) {
+      dbg_pops = pops;
+      dbg_qn = qn;
+      dbg_nn = nn;
+      if (wd_work >= 256u) {
+        wd_work = 0;
+        TY_WD(1);
+      }
+      if (dead || ++pops > N) {  // every id is popped at most once
+        fail = kPathInternal;
+        break;
+      }
+      // ---- pop the minimum (dist, id); the last entry sifts down from the root ----
+      const uint32_t pid = S.qid[0];
+      const double pdist = S.ndist[pid];
+      --qn;
+      if (qn > 0) {
+        const uint32_t xi = S.qid[qn];
+        const double xd = S.ndist[xi];
+        uint32_t i = 0;
+        for (;;) {
+          const uint32_t c0 = i * 64 + 1;
+          if (c0 >= qn) break;
+          const uint32_t cc = c0 + lane;
+          const bool v = cc < qn;
+          const uint32_t ci = v ? (uint32_t)S.qid[cc] : 0u;
+          const double cd = v ? S.ndist[ci] : 0.0;
+          // the minimum child: min dist, then min id (heap ids are distinct); -0.0 == +0.0
+          // as in qless, and only qless sees the value
+          const double dmn = __ockl_wfred_min_f64(v ? cd : __builtin_huge_val());
+          const bool c1 = v && cd == dmn;
+          const uint32_t mi = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(c1 ? ci : ~0u));
+          const uint32_t mp = c0 + (uint32_t)__ffsll((long long)__ballot(c1 && ci == mi)) - 1;
+          if (qless(dmn, mi, xd, xi)) {
+            if (lane == 0) {
+              S.qid[i] = (uint16_t)mi;
+              S.pos[mi] = (uint16_t)i;
+            }
+            i = mp;
+          } else {
+            break;
+          }
+        }
+        if (lane == 0) {
+          S.qid[i] = (uint16_t)xi;
+          S.pos[xi] = (uint16_t)i;
+        }
+      }
+      wave_fence();
+      if (pid >= nn) {  // cannot happen on a consistent heap; never read past the tables
+        fail = kPathInternal;
+        break;
+      }
+      const uint2 pb = S.nback[pid];
+      if (pb.x & kTySettled) {
+        fail = kPathInternal;
+        break;
+      }
+      if (lane == 0) {
+        S.nback[pid].x = pb.x | kTySettled;
+        S.pos[pid] = (uint16_t)kTyNone;
+      }
+      const unsigned long long pk = S.nkey[pid];
+      PopCands P;
+      P.s1 = (uint32_t)(pk & 0xFFFFFFFFull) >> 2;
+      P.f = (uint32_t)pk & 3u;
+      P.s2 = (uint32_t)(pk >> 32);
+      if (P.s2 >= rhs.num_states) {
+        fail = kPathInternal;
+        break;
+      }
+
+      // ---- best final (:165-179) ----
+      const double fw1 = cl.final_w(P.s1);
+      const double fw2 = rhs.final_w[P.s2];
+      if (!w_is_zero(fw1) && !w_is_zero(fw2)) {
+        const double fw = w_times(fw1, fw2);
+        const double total = w_times(pdist, fw);
+        if (best_id == kNoState || total < best_total || (total == best_total && pid < best_id)) {
+          best_id = pid;
+          best_fw = fw;
+          best_total = total;
+        }
+      }
+
+      // ---- candidates of the 4 phases in reference order ----
+      prepare_chain(rhs, cl, P);
+      const uint32_t C = P.n1 + P.n2 + P.n3 + P.n4;
+      relax_count += C;
+      wd_work += C + 16u;
+      double cur_dist = pdist;  // dist[curr_id]; changes only through a self-loop
+      dbg_C = C;
+      for (uint32_t cb = 0; cb < C; cb += 64) {
+        dbg_cb = cb;
+        if (cb != 0 && (cb & 4095u) == 0) {
+          TY_WD(2);
+        }
+        if (dead) {
+          fail = kPathInternal;
+          break;
+        }
+        const uint32_t c = cb + lane;
+        const bool act = c < C;
+        TyCand x{0, 0, 0, 0, 0.0};
+        if (act) x = tiny_cand(rhs, P, c);
+        // lookup (getOrCreate's get): the slot names an id, the id's key decides
+        uint32_t tid = kNoState;
+        uint32_t slot = hmix(x.key) & hmask;
+        if (act) {
+          for (uint32_t probe = 0; probe <= hmask; ++probe) {
+            const uint32_t v = S.hs[slot];
+            if ((v >> 16) != gen) break;
+            const uint32_t id = v & 0xFFFFu;
+            if (S.nkey[id] == x.key) {
+              tid = id;
+              break;
+            }
+            slot = (slot + 1) & hmask;
+          }
+        }
+        // first-occurrence dedup of new tuples in lane order
+        const bool need = act && tid == kNoState;
+        uint32_t leader = lane;
+        unsigned long long pending = __ballot(need);
+        while (pending) {
+          const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
+          const unsigned long long lk =
+              ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(x.key >> 32), l) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((uint32_t)x.key, l);
+          const bool same = need && x.key == lk;
+          const unsigned long long m = __ballot(same);
+          if (same) leader = l;
+          pending &= ~m;
+        }
+        const bool is_new_leader = need && leader == lane;
+        const unsigned long long nlm = __ballot(is_new_leader);
+        const uint32_t n_new = (uint32_t)__popcll(nlm);
+        if (nn + n_new > N) {
+          fail = kPathOverflow;
+          break;
+        }
+        if (is_new_leader) {
+          tid = nn + (uint32_t)__popcll(nlm & lanemask_lt());
+          // claim the first free slot from where the lookup ended (load <= 1/2)
+          const uint32_t mine = (gen << 16) | tid;
+          uint32_t s = slot;
+          for (uint32_t probe = 0; probe <= hmask; ++probe) {
+            const uint32_t old = S.hs[s];
+            if ((old >> 16) != gen && atomicCAS(&S.hs[s], old, mine) == old) break;
+            s = (s + 1) & hmask;
+          }
+          S.nkey[tid] = x.key;
+          S.ndist[tid] = w_zero();
+          S.nback[tid] = make_uint2(0u, 0u);
+          S.pos[tid] = (uint16_t)kTyNone;
+        }
+        const uint32_t lt = __shfl(tid, (int)leader, 64);
+        if (need) tid = lt;
+        nn += n_new;
+        wave_fence();
+
+        // self-loop onto the popped tuple: rare, exact one-lane path
+        const unsigned long long selfm = __ballot(act && tid == pid);
+        if (selfm) {
+          S.cid[lane] = tid;
+          S.cw[lane] = x.w;
+          S.col[lane] = x.ol;
+          S.ccode[lane] = x.code;
+          S.carc[lane] = x.arc;
+          wave_fence();
+          const uint32_t cnt = C - cb < 64 ? C - cb : 64;
+          if (lane == 0) {
+            for (uint32_t i = 0; i < cnt; ++i) {
+              const uint32_t t = S.cid[i];
+              const double nd = w_times(cur_dist, S.cw[i]);
+              const double od = S.ndist[t];
+              const uint2 b = S.nback[t];
+              const uint32_t code = S.ccode[i];
+              uint32_t bol = 0;
+              bool bol_known = false;
+              if (tiny_take(rhs, nd, (code & kTyConsumed) ? P.label : kEpsilon, S.col[i], od, b,
+                            pid, P.label, bol, bol_known)) {
+                S.ndist[t] = nd;
+                S.nback[t] = make_uint2(pid | (b.x & kTySettled) | kTyHasBack | code, S.carc[i]);
+                if (t == pid) cur_dist = nd;
+                if (!(b.x & kTySettled)) {
+                  tiny_heap_update(S, qn, t, nd);
+                  ++pushes;
+                }
+              }
+            }
+          }
+          cur_dist = __shfl(cur_dist, 0, 64);
+          qn = __shfl(qn, 0, 64);
+          pushes = __shfl(pushes, 0, 64);
+          wave_fence();
+          continue;
+        }
+
+        // group by target: the first lane of each group folds its members in lane order
+        const double nd = w_times(cur_dist, x.w);
+        S.cnd[lane] = nd;
+        S.col[lane] = x.ol;
+        S.ccode[lane] = x.code;
+        S.carc[lane] = x.arc;
+        wave_fence();
+        unsigned long long gmask = 0;
+        {
+          unsigned long long pend = __ballot(act);
+          while (pend) {
+            const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
+            const uint32_t lt2 = __builtin_amdgcn_readlane(tid, l);
+            const bool same = act && tid == lt2;
+            const unsigned long long m = __ballot(same);
+            if (lane == l) gmask = m;
+            pend &= ~m;
+          }
+        }
+        bool push = false;
+        double push_d = 0.0;
+        if (gmask) {  // group leader
+          const uint32_t t = tid;
+          double od = S.ndist[t];
+          uint2 b = S.nback[t];
+          uint32_t bol = 0;
+          bool bol_known = false;
+          bool took = false;
+          unsigned long long m = gmask;
+          while (m) {
+            const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
+            m &= m - 1;
+            const double cnd = S.cnd[i];
+            const uint32_t code = S.ccode[i], col = S.col[i];
+            if (tiny_take(rhs, cnd, (code & kTyConsumed) ? P.label : kEpsilon, col, od, b, pid,
+                          P.label, bol, bol_known)) {
+              od = cnd;
+              b = make_uint2(pid | (b.x & kTySettled) | kTyHasBack | code, S.carc[i]);
+              bol = col;
+              bol_known = true;
+              took = true;
+            }
+          }
+          if (took) {
+            S.ndist[t] = od;
+            S.nback[t] = b;
+            if (!(b.x & kTySettled)) {
+              push = true;
+              push_d = od;
+            }
+          }
+        }
+        wave_fence();
+        // heap updates (insert or decrease-key), one lane; the order does not matter
+        unsigned long long pm = __ballot(push);
+        pushes += (uint32_t)__popcll(pm);
+        if (pm) {
+          uint32_t q = qn;
+          while (pm) {
+            const uint32_t l = (uint32_t)__ffsll((long long)pm) - 1;
+            pm &= pm - 1;
+            const unsigned long long pb2 = (unsigned long long)__double_as_longlong(push_d);
+            const double xd = __longlong_as_double(
+                (long long)(((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pb2 >> 32), l) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)pb2, l)));
+            const uint32_t xi = __builtin_amdgcn_readlane(tid, l);
+            if (lane == 0) tiny_heap_update(S, q, xi, xd);
+          }
+          qn = __shfl(q, 0, 64);
+        }
+        wave_fence();
+      }
+      if (fail != kPathOk) break;
+    }
+
+    // ---- result (:368-400): the path's ids in LDS, then written by all lanes ----
+    int32_t st = fail;
+    uint32_t P = 0;
+    unsigned long long o = 0;
+    if (lane == 0 && st == kPathOk) {
+      if (best_id == kNoState) {
+        st = kPathEmpty;
+      } else {
+        uint32_t cur = best_id;
+        while (cur != 0) {  // init_id == 0
+          const uint2 b = S.nback[cur];
+          if (!(b.x & kTyHasBack)) {
+            st = kPathEmpty;
+            break;
+          }
+          if (++P > nn) {
+            st = kPathCycle;
+            break;
+          }
+          S.qid[P - 1] = (uint16_t)cur;  // the heap is empty: its ids hold the path
+          cur = b.x & kTyPrev;
+        }
+        if (st == kPathOk) {
+          o = reserve_path(out, si, P);
+          if (o + P > out.arc_cap) st = kPathOutputFull;
+        }
+      }
+    }
+    st = __shfl(st, 0, 64);
+    wave_fence();
+    if (st == kPathOk) {
+      P = __shfl(P, 0, 64);
+      o = __shfl(o, 0, 64);
+      for (uint32_t k = lane; k < P; k += 64) {
+        const uint32_t id = S.qid[k];
+        const uint2 b = S.nback[id];
+        const uint32_t prev = b.x & kTyPrev;
+        uint32_t il = kEpsilon, ol = kEpsilon;
+        double aw = w_one();
+        if (b.x & kTyConsumed) il = cl.labels[(uint32_t)(S.nkey[prev] & 0xFFFFFFFFull) >> 2];
+        if (b.x & kTyArc) {
+          const ArcRec r = rhs.rec[b.y];
+          ol = r.olabel;
+          aw = (b.x & kTyConsumed) ? w_times(w_one(), r.weight) : r.weight;
+        }
+        const unsigned long long at = o + (P - 1 - k);
+        out.out_il[at] = il;
+        out.out_ol[at] = ol;
+        out.out_w[at] = aw;
+      }
+    } else {
+      P = 0;
+      o = 0;
+    }
+    if (lane == 0) {
+      out.status[si] = st;
+      out.path_len[si] = st == kPathInternal ? pops : P;  // diagnostics on a bug path
+      out.path_off[si] = st == kPathInternal ? pushes : o;
+      out.final_w[si] = st == kPathOk ? best_fw : w_zero();
+      if (out.work) {
+        out.work[2 * si] = nn;
+        out.work[2 * si + 1] = relax_count;
+      }
+    }
+    wave_fence();
+  }
+}
+#undef TY_WD
+
+}  // namespace fstamd
