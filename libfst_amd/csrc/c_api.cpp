@@ -37,55 +37,88 @@ namespace {
 
 constexpr uint64_t kInvalid = UINT64_MAX;
 
+// Handle tables (src/c-api.zig:132-271), sharded: a handle's low bits name one of kShards
+// shards, each with its own reader-writer lock over its slots AND the contents of the
+// objects they hold.  Queries take their shard shared, edits exclusive; threads working on
+// their own handles (concurrent compose calls reading their results arc by arc) do not meet
+// on one lock -- one table-wide lock cost a third of the calls/s at 256 threads.
 template <class T>
-class HandleTable {  // src/c-api.zig:132-271
+class HandleTable {
  public:
+  static constexpr uint32_t kShards = 64;
+  using SharedLock = std::shared_lock<std::shared_mutex>;
+  using ExclusiveLock = std::unique_lock<std::shared_mutex>;
+
   uint64_t insert(std::shared_ptr<T> p) {
-    uint32_t idx;
-    if (!free_.empty()) {
-      idx = free_.back();
-      free_.pop_back();
-      if (++gen_[idx] == 0) gen_[idx] = 1;
-      slots_[idx] = std::move(p);
+    // a thread fills one shard (its own, by arrival order): inserts from many threads spread
+    static std::atomic<uint32_t> next{0};
+    thread_local uint32_t mine = next.fetch_add(1, std::memory_order_relaxed) % kShards;
+    Shard& sh = shards_[mine];
+    ExclusiveLock g(sh.mu);
+    uint32_t local;
+    if (!sh.free.empty()) {
+      local = sh.free.back();
+      sh.free.pop_back();
+      if (++sh.gen[local] == 0) sh.gen[local] = 1;
+      sh.slots[local] = std::move(p);
     } else {
-      idx = (uint32_t)slots_.size();
-      if (idx == 0xFFFFFFFFu) return kInvalid;
-      slots_.push_back(std::move(p));
-      gen_.push_back(1);
+      local = (uint32_t)sh.slots.size();
+      if ((uint64_t)local * kShards + mine >= 0xFFFFFFFFull) return kInvalid;
+      sh.slots.push_back(std::move(p));
+      sh.gen.push_back(1);
     }
-    return ((uint64_t)gen_[idx] << 32) | idx;
+    return ((uint64_t)sh.gen[local] << 32) | (local * kShards + mine);
   }
-  // get/pin: a shared_ptr copy keeps the object alive outside the lock.
-  std::shared_ptr<T> get(uint64_t h) const {
+  // the lock a query (shared) or an edit (exclusive) of handle h holds around get_locked
+  SharedLock lock_shared(uint64_t h) const { return SharedLock(shard(h).mu); }
+  ExclusiveLock lock(uint64_t h) const { return ExclusiveLock(shard(h).mu); }
+  // the object of h, or null; the caller holds lock_shared(h) or lock(h)
+  T* get_locked(uint64_t h) const {
     if (h == kInvalid) return nullptr;
     const uint32_t g = (uint32_t)(h >> 32), idx = (uint32_t)h;
-    if (g == 0 || idx == 0xFFFFFFFFu || idx >= slots_.size()) return nullptr;
-    if (gen_[idx] != g) return nullptr;
-    return slots_[idx];
+    if (g == 0 || idx == 0xFFFFFFFFu) return nullptr;
+    const Shard& sh = shard(h);
+    const uint32_t local = idx / kShards;
+    if (local >= sh.slots.size() || sh.gen[local] != g) return nullptr;
+    return sh.slots[local].get();
+  }
+  // get/pin: a shared_ptr copy keeps the object alive outside the lock
+  std::shared_ptr<T> get(uint64_t h) const {
+    SharedLock g = lock_shared(h);
+    if (!get_locked(h)) return nullptr;
+    return shard(h).slots[(uint32_t)h / kShards];
   }
   bool remove(uint64_t h) {
-    if (!get(h)) return false;
-    const uint32_t idx = (uint32_t)h;
-    slots_[idx].reset();
-    if (++gen_[idx] == 0) gen_[idx] = 1;  // invalidateSlot
-    free_.push_back(idx);
+    ExclusiveLock g = lock(h);
+    if (!get_locked(h)) return false;
+    Shard& sh = shard(h);
+    const uint32_t local = (uint32_t)h / kShards;
+    sh.slots[local].reset();
+    if (++sh.gen[local] == 0) sh.gen[local] = 1;  // invalidateSlot
+    sh.free.push_back(local);
     return true;
   }
   void clear() {
-    slots_.clear();
-    gen_.clear();
-    free_.clear();
+    for (Shard& sh : shards_) {
+      ExclusiveLock g(sh.mu);
+      sh.slots.clear();
+      sh.gen.clear();
+      sh.free.clear();
+    }
   }
 
  private:
-  std::vector<std::shared_ptr<T>> slots_;
-  std::vector<uint32_t> gen_;
-  std::vector<uint32_t> free_;
+  struct alignas(64) Shard {
+    mutable std::shared_mutex mu;
+    std::vector<std::shared_ptr<T>> slots;
+    std::vector<uint32_t> gen;
+    std::vector<uint32_t> free;
+  };
+  Shard& shard(uint64_t h) { return shards_[(uint32_t)h % kShards]; }
+  const Shard& shard(uint64_t h) const { return shards_[(uint32_t)h % kShards]; }
+  Shard shards_[kShards];
 };
 
-// Handle tables (src/c-api.zig:132-271): one lock, shared by read-only queries (the
-// result readback of many concurrent calls), exclusive for inserts, removes and edits.
-std::shared_mutex g_api_mu;
 HandleTable<MutableFst> g_mut;
 HandleTable<FrozenFst> g_fst;
 
@@ -1582,32 +1615,32 @@ extern "C" {
 // ---- MutableFst lifecycle -----------------------------------------------------------
 
 FstMutableHandle fst_mutable_new(void) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>());
 }
 
 FstMutableHandle fst_mutable_clone(FstMutableHandle handle) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
-  if (!m) return kInvalid;
-  return g_mut.insert(std::make_shared<MutableFst>(*m));
+  std::shared_ptr<MutableFst> copy;
+  {
+    auto g = g_mut.lock_shared(handle);
+    const MutableFst* m = g_mut.get_locked(handle);
+    if (!m) return kInvalid;
+    copy = std::make_shared<MutableFst>(*m);
+  }
+  return g_mut.insert(std::move(copy));
 }
 
-void fst_mutable_free(FstMutableHandle handle) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  g_mut.remove(handle);
-}
+void fst_mutable_free(FstMutableHandle handle) { g_mut.remove(handle); }
 
 uint32_t fst_mutable_add_state(FstMutableHandle handle) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock(handle);
+  MutableFst* m = g_mut.get_locked(handle);
   if (!m) return FST_NO_STATE;
   return m->add_state();
 }
 
 FstError fst_mutable_set_start(FstMutableHandle handle, uint32_t state) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock(handle);
+  MutableFst* m = g_mut.get_locked(handle);
   if (!m) return FST_INVALID_ARG;
   if (state >= m->num_states()) return FST_INVALID_STATE;
   m->set_start(state);
@@ -1615,8 +1648,8 @@ FstError fst_mutable_set_start(FstMutableHandle handle, uint32_t state) {
 }
 
 FstError fst_mutable_set_final(FstMutableHandle handle, uint32_t state, double weight) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock(handle);
+  MutableFst* m = g_mut.get_locked(handle);
   if (!m) return FST_INVALID_ARG;
   if (state >= m->num_states()) return FST_INVALID_STATE;
   m->set_final(state, weight);
@@ -1625,8 +1658,8 @@ FstError fst_mutable_set_final(FstMutableHandle handle, uint32_t state, double w
 
 FstError fst_mutable_add_arc(FstMutableHandle handle, uint32_t src, uint32_t ilabel,
                              uint32_t olabel, double weight, uint32_t nextstate) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock(handle);
+  MutableFst* m = g_mut.get_locked(handle);
   if (!m) return FST_INVALID_ARG;
   if (src >= m->num_states()) return FST_INVALID_STATE;
   if (nextstate >= m->num_states()) return FST_INVALID_STATE;
@@ -1635,35 +1668,35 @@ FstError fst_mutable_add_arc(FstMutableHandle handle, uint32_t src, uint32_t ila
 }
 
 uint32_t fst_mutable_start(FstMutableHandle handle) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock_shared(handle);
+  const MutableFst* m = g_mut.get_locked(handle);
   return m ? m->start() : FST_NO_STATE;
 }
 
 uint32_t fst_mutable_num_states(FstMutableHandle handle) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock_shared(handle);
+  const MutableFst* m = g_mut.get_locked(handle);
   return m ? (uint32_t)m->num_states() : 0;
 }
 
 uint32_t fst_mutable_num_arcs(FstMutableHandle handle, uint32_t state) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock_shared(handle);
+  const MutableFst* m = g_mut.get_locked(handle);
   if (!m || state >= m->num_states()) return 0;
   return (uint32_t)m->num_arcs(state);
 }
 
 double fst_mutable_final_weight(FstMutableHandle handle, uint32_t state) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock_shared(handle);
+  const MutableFst* m = g_mut.get_locked(handle);
   if (!m || state >= m->num_states()) return w_zero();
   return m->final_weight(state);
 }
 
 uint32_t fst_mutable_get_arcs(FstMutableHandle handle, uint32_t state, FstArc* buf,
                               uint32_t buf_len) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock_shared(handle);
+  const MutableFst* m = g_mut.get_locked(handle);
   if (!m || state >= m->num_states()) return 0;
   const auto& arcs = m->arcs(state);
   const uint32_t count = std::min<uint32_t>((uint32_t)arcs.size(), buf_len);
@@ -1678,49 +1711,40 @@ uint32_t fst_mutable_get_arcs(FstMutableHandle handle, uint32_t state, FstArc* b
 FstHandle fst_freeze(FstMutableHandle mutable_handle) {
   std::shared_ptr<MutableFst> snap;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
-    auto m = g_mut.get(mutable_handle);
+    auto g = g_mut.lock_shared(mutable_handle);
+    const MutableFst* m = g_mut.get_locked(mutable_handle);
     if (!m) return kInvalid;
     snap = std::make_shared<MutableFst>(*m);  // clone under the lock (c-api.zig:507-517)
   }
   auto f = FrozenFst::from_mutable(*snap, kWeightTropical);
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
-void fst_free(FstHandle handle) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
-  g_fst.remove(handle);
-}
+void fst_free(FstHandle handle) { g_fst.remove(handle); }
 
 uint32_t fst_start(FstHandle handle) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   return f ? f->start() : FST_NO_STATE;
 }
 
 uint32_t fst_num_states(FstHandle handle) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   return f ? f->num_states() : 0;
 }
 
 uint32_t fst_num_arcs(FstHandle handle, uint32_t state) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   if (!f || state >= f->num_states()) return 0;
   return f->num_arcs(state);
 }
 
 double fst_final_weight(FstHandle handle, uint32_t state) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   if (!f || state >= f->num_states()) return w_zero();
   return f->final_weight(state);
 }
 
 uint32_t fst_get_arcs(FstHandle handle, uint32_t state, FstArc* buf, uint32_t buf_len) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(handle);
   if (!f || state >= f->num_states()) return 0;
   const StateEntry& e = f->states()[state];
@@ -1739,7 +1763,6 @@ FstHandle fst_load(const char* path) {
   if (!path) return kInvalid;
   auto f = FrozenFst::load_file(path, kWeightTropical, nullptr);  // binary.zig:16-36
   if (!f) return kInvalid;
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -1762,7 +1785,6 @@ FstMutableHandle fst_read_text(const char* path) {
   if (!ok) return kInvalid;
   auto m = std::make_shared<MutableFst>();
   if (!MutableFst::read_text(data.data(), data.size(), m.get())) return kInvalid;
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::move(m));
 }
 
@@ -1770,7 +1792,6 @@ FstError fst_save(FstHandle handle, const char* path) {
   if (!path) return FST_INVALID_ARG;
   std::shared_ptr<FrozenFst> f;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
     f = g_fst.get(handle);
     if (!f) return FST_INVALID_ARG;
   }
@@ -1798,8 +1819,8 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
   size_t a_states = 0, a_arcs = 0;
   bool a_start = false;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
-    auto ha = g_mut.get(a_handle);
+    auto g = g_mut.lock_shared(a_handle);
+    const MutableFst* ha = g_mut.get_locked(a_handle);
     if (!ha) {
       trace("sp_invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
       return kInvalid;
@@ -1862,7 +1883,6 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
   }
   trace("sp_ok", a_handle, b_handle, a_states, a_arcs, result.num_states(),
         result.total_arcs(), us(), t_last_stats.kernel_ms);
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
@@ -1876,8 +1896,8 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
   std::shared_ptr<MutableFst> a;
   std::shared_ptr<FrozenFst> b;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
-    auto ha = g_mut.get(a_handle);
+    auto g = g_mut.lock_shared(a_handle);
+    const MutableFst* ha = g_mut.get_locked(a_handle);
     if (!ha) {
       trace("invalid_a", a_handle, b_handle, 0, 0, 0, 0, us(), 0);
       return kInvalid;
@@ -1945,7 +1965,6 @@ FstMutableHandle fst_compose_frozen(FstMutableHandle a_handle, FstHandle b_handl
                  (us() - t_gpu) / 1e3);
   trace("ok", a_handle, b_handle, a->num_states(), a->total_arcs(), result.num_states(),
         result.total_arcs(), us(), st.kernel_ms);
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
@@ -1958,8 +1977,8 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
   };
   std::unique_ptr<HostGraph> m;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
-    auto h = g_mut.get(handle);
+    auto g = g_mut.lock_shared(handle);
+    const MutableFst* h = g_mut.get_locked(handle);
     if (!h) return kInvalid;
     m = std::make_unique<HostGraph>(*h);  // snapshot, flattened to CSR under the lock
   }
@@ -2001,22 +2020,20 @@ FstMutableHandle fst_shortest_path(FstMutableHandle handle, uint32_t n) {
                    "[libfst_amd host] fst_shortest_path call: snapshot %.2f upload %.2f engine + "
                    "result %.2f ms\n", t_snap, t_up - t_snap, ms() - t_up);
   }
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_mut.insert(std::make_shared<MutableFst>(std::move(result)));
 }
 
 // ---- Strings ------------------------------------------------------------------------
 
 FstMutableHandle fst_compile_string(const uint8_t* input, uint32_t len) {
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   if (!input) return kInvalid;
   return g_mut.insert(
       std::make_shared<MutableFst>(MutableFst::compile_string(input, len, input, len)));
 }
 
 static int32_t print_impl(FstMutableHandle handle, uint8_t* buf, uint32_t buf_len, bool out_tape) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
-  auto m = g_mut.get(handle);
+  auto g = g_mut.lock_shared(handle);
+  const MutableFst* m = g_mut.get_locked(handle);
   if (!m) return -1;
   std::vector<uint8_t> s;
   if (!m->print_string(out_tape, &s)) return -1;
@@ -2034,11 +2051,8 @@ int32_t fst_print_output_string(FstMutableHandle handle, uint8_t* buf, uint32_t 
 }
 
 void fst_teardown(void) {
-  {
-    std::unique_lock<std::shared_mutex> g(g_api_mu);
-    g_mut.clear();
-    g_fst.clear();
-  }
+  g_mut.clear();
+  g_fst.clear();
   pool_clear();
   pin_pool_clear();
 }
@@ -2057,7 +2071,6 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   if (opts && (opts->flags & ~FST_BATCH_DEVICES)) return FST_INVALID_ARG;
   std::shared_ptr<FrozenFst> b;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
     b = g_fst.get(b_handle);
   }
   if (!b) return FST_INVALID_ARG;
@@ -2249,7 +2262,6 @@ FstError fst_pipeline_batch(const FstHandle* stages, uint32_t num_stages, const 
   if (opts && (opts->flags & ~FST_BATCH_DEVICES)) return FST_INVALID_ARG;
   std::vector<std::shared_ptr<FrozenFst>> fs(num_stages);
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
     for (uint32_t k = 0; k < num_stages; ++k)
       if (!(fs[k] = g_fst.get(stages[k]))) return FST_INVALID_ARG;
   }
@@ -2289,7 +2301,6 @@ FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_
   if (!o || !d_offsets) return FST_INVALID_ARG;
   std::shared_ptr<FrozenFst> b;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
     b = g_fst.get(b_handle);
   }
   if (!b) return FST_INVALID_ARG;
@@ -2315,7 +2326,6 @@ FstError fst_device_compose_shortest_path(FstHandle b_handle, const uint32_t* d_
 FstError fst_device_prepare(FstHandle b_handle, int32_t device) {
   std::shared_ptr<FrozenFst> b;
   {
-    std::shared_lock<std::shared_mutex> g(g_api_mu);
     b = g_fst.get(b_handle);
   }
   if (!b) return FST_INVALID_ARG;
@@ -2343,7 +2353,6 @@ FstHandle fst_device_adopt_blob(const void* d_blob, uint64_t len, int32_t device
   DeviceFst* D = DeviceFst::adopt(d_blob, *f, dev);
   if (!D) return kInvalid;
   f->adopt_device(dev, D);
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -2363,7 +2372,6 @@ FstHandle fst_batch_load_bytes(const void* bytes, uint64_t len) {
   if (h.weight_type != kWeightTropical && h.weight_type != kWeightLog) return kInvalid;
   auto f = FrozenFst::from_bytes((const uint8_t*)bytes, len, h.weight_type, nullptr);
   if (!f) return kInvalid;
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -2371,7 +2379,6 @@ FstHandle fst_batch_load(const char* path) {
   if (!path) return kInvalid;
   auto f = FrozenFst::load_file(path, FrozenFst::kAnyWeightType, nullptr);
   if (!f) return kInvalid;
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
@@ -2394,12 +2401,10 @@ FstHandle fst_load_att(const char* path, uint32_t flags) {
   if (!MutableFst::read_text(data.data(), data.size(), &m)) return kInvalid;
   if (flags & FST_ATT_SHIFT_BYTE_LABELS) m.shift_labels();
   auto f = FrozenFst::from_mutable(m, kWeightTropical);
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 
 double fst_chain_cost(FstHandle b, uint64_t len) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(b);
   return f ? f->chain_cost(len) : -1.0;
 }
@@ -2413,7 +2418,6 @@ int32_t fst_debug_coalescer_state(int32_t device, uint32_t* queued) {
 }
 
 int32_t fst_weight_type(FstHandle b) {
-  std::shared_lock<std::shared_mutex> g(g_api_mu);
   auto f = g_fst.get(b);
   return f ? (int32_t)f->weight_type() : -1;
 }
@@ -2459,7 +2463,6 @@ FstHandle fst_bench_transducer_wt(uint32_t kind, uint32_t T, uint32_t B, uint32_
     return kInvalid;
   }
   auto f = FrozenFst::from_mutable(m, (uint8_t)weight_type);
-  std::unique_lock<std::shared_mutex> g(g_api_mu);
   return g_fst.insert(std::move(f));
 }
 

@@ -581,6 +581,12 @@ hipError_t DeviceEngine::finish_deferred(LaunchStats* stats) {
   return e;
 }
 
+namespace {
+bool tiny_old();
+template <int T>
+int lazy_tiny_per_cu();
+}  // namespace
+
 hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                    int semantics, const BatchOutDev& out, hipStream_t stream,
                                    LaunchStats* stats) {
@@ -901,7 +907,23 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       const bool first128 = ts && *ts ? std::strcmp(ts, "2") != 0
                                       : rhs.tiny_lazy_256.load(std::memory_order_relaxed) == 0;
       uint32_t cnt[2] = {0, 0};
-      if (first128) {
+      // A batch that the largest LDS size holds at once (coalesced single calls, small host
+      // batches) starts every string there: one wave per string whichever the size, so a
+      // long utterance no longer pays a replay at 256 tuples before its rerun at 512 or 1024
+      // (36 B per tuple: 1024 tuples are 38 KB, 4 waves per CU)
+      const bool direct = !(ts && *ts) && !tiny_old() &&
+                          (uint64_t)num <= (uint64_t)num_cus_ * lazy_tiny_per_cu<4>();
+      if (direct) {
+        HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 4, nullptr, num, c + 2, &g));
+        if (stats) stats->grid = g;
+        collect_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(out.status, num,
+                                                                    kPathOverflow, lb, c + 3);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(&cnt[1], c + 3, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (num >= 64 && (uint64_t)cnt[1] * 10 > (uint64_t)num * 9)
+          rhs.skip_tiny_lazy.store(1, std::memory_order_relaxed);
+      } else if (first128) {
         HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 1, nullptr, num, c, &g));
         if (stats) stats->grid = g;
         collect_status_kernel<<<(num + 255) / 256, 256, 0, stream>>>(out.status, num,
@@ -912,7 +934,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       } else {
         cnt[0] = num;
       }
-      if (cnt[0] > 0) {
+      if (!direct && cnt[0] > 0) {
         HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 2, first128 ? la : nullptr, cnt[0], c + 2, &g));
         if (first128) {
           collect_list_kernel<<<(cnt[0] + 255) / 256, 256, 0, stream>>>(la, c + 1, out.status,
@@ -926,14 +948,14 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
         HIP_TRY(hipStreamSynchronize(stream));
         if (stats) stats->launches += 1;
       }
-      if (first128 && num >= 1024 && (uint64_t)cnt[0] * 3 > (uint64_t)num)
+      if (!direct && first128 && num >= 1024 && (uint64_t)cnt[0] * 3 > (uint64_t)num)
         rhs.tiny_lazy_256.store(1, std::memory_order_relaxed);
-      if (first128 && num < 1024) {  // small batches: the same rule over their sum
+      if (!direct && first128 && num < 1024) {  // small batches: the same rule over their sum
         const uint64_t seen = rhs.tiny_lazy_seen.fetch_add(num) + num;
         const uint64_t over = rhs.tiny_lazy_over.fetch_add(cnt[0]) + cnt[0];
         if (seen >= 1024 && over * 3 > seen) rhs.tiny_lazy_256.store(1, std::memory_order_relaxed);
       }
-      if (first128 && num >= 64 && (uint64_t)cnt[0] * 10 > (uint64_t)num * 9)
+      if (!direct && first128 && num >= 64 && (uint64_t)cnt[0] * 10 > (uint64_t)num * 9)
         rhs.skip_tiny_lazy.store(1, std::memory_order_relaxed);
       todo = lb;
       todo_n = cnt[1];
@@ -946,7 +968,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       // replay's HBM index -- 2.7 ms for 63 labels of the WeText-scale tagger): 512 tuples
       // (~55 KB, 2 waves per CU), then 1024 (~110 KB, 1 per CU), one string per wave.
       uint32_t cnt_big[2] = {0, 0};
-      for (int t = 3; t <= 4 && todo_n > 0 && ((uint64_t)todo_n * 4 <= num || num <= 64); ++t) {
+      for (int t = 3; !direct && t <= 4 && todo_n > 0 && ((uint64_t)todo_n * 4 <= num || num <= 64);
+           ++t) {
         unsigned int* ci = counter + 48 + 2 * (t - 3);  // [48|50] items, [49|51] |next list|
         HIP_TRY(hipMemsetAsync(ci, 0, 8, stream));
         HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, t, rest, todo_n, ci, &g));
@@ -1359,12 +1382,20 @@ hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& i
   ws.qcap = lz_tiny_q(tier);
   ws.gcap = 0;
   ws.stamp_base = 0;  // stamps from 1 per launch: the LDS table starts zeroed
+  // test knobs: FSTAMD_TINY_GEN0 = the hash generation lazy_tiny_kernel starts from (its wrap
+  // at 65536 strings per wave, within reach); FSTAMD_TINY_WAVES caps the grid
+  const char* eg = std::getenv("FSTAMD_TINY_GEN0");
+  const char* ew = std::getenv("FSTAMD_TINY_WAVES");
+  const uint32_t gen0 = eg ? (uint32_t)std::strtoul(eg, nullptr, 10) & 0xFFFFu : 0u;
+  const uint32_t cap_waves = ew ? (uint32_t)std::strtoul(ew, nullptr, 10) : 0u;
+  if (!tiny_old()) ws.stamp_base = gen0;
   ws.max_pops = ws.qcap + 1;
   ws.wd_ticks = watchdog_ticks();
   const int occ = tier == 1 ? lazy_tiny_per_cu<1>() : tier == 2 ? lazy_tiny_per_cu<2>()
                  : tier == 3 ? lazy_tiny_per_cu<3>() : lazy_tiny_per_cu<4>();
-  const uint32_t grid =
+  uint32_t grid =
       (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(num_items, 1u));
+  if (cap_waves) grid = std::min(grid, cap_waves);
   GraphInput none{};
   if (!tiny_old()) {
     if (tier == 1)
@@ -1388,6 +1419,21 @@ hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& i
     lazy_wave_kernel<false, 4><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
                                                          num_items, ws, out);
   HIP_TRY(hipGetLastError());
+#ifdef FSTAMD_TINY_PROF
+  {
+    unsigned long long p[8];
+    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpyFromSymbol(p, HIP_SYMBOL(g_tiny_prof), sizeof(p)));
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_tiny_prof), z, sizeof(z)));
+    const double pops = p[7] ? (double)p[7] : 1.0;
+    std::fprintf(stderr,
+                 "[tiny prof] tier %d: %u strings, %llu pops; cycles per pop: pop %.0f, tuple+spans "
+                 "%.0f, records+lookup %.0f, dedup %.0f, group+fold %.0f, heap %.0f, result %.0f\n",
+                 tier, num_items, p[7], p[0] / pops, p[1] / pops, p[2] / pops, p[3] / pops,
+                 p[4] / pops, p[5] / pops, p[6] / pops);
+  }
+#endif
   if (grid_out) *grid_out = grid;
   return hipSuccess;
 }

@@ -37,6 +37,24 @@ constexpr uint32_t kTyHasBack = 1u << 17;
 constexpr uint32_t kTyConsumed = 1u << 18;  // the move read the lhs label (phases 1, 2, 4)
 constexpr uint32_t kTyArc = 1u << 19;       // nback.y is an rhs arc index (not phase 2)
 
+// FSTAMD_TINY_PROF (a debug build): cycles per phase summed over every wave, printed by
+// DeviceEngine::run_lazy_tiny -- [0] pop, [1] popped tuple + final + arc spans, [2] candidate
+// records + lookups, [3] dedup + new tuples, [4] grouping + fold, [5] heap updates, [6]
+// result, [7] pops
+#ifdef FSTAMD_TINY_PROF
+__device__ unsigned long long g_tiny_prof[8];
+#define TY_T(k)                                                  \
+  do {                                                           \
+    const unsigned long long t_ = __builtin_readcyclecounter();  \
+    prof[k] += t_ - tl;                                          \
+    tl = t_;                                                     \
+  } while (0)
+#else
+#define TY_T(k) \
+  do {          \
+  } while (0)
+#endif
+
 template <int kTier>
 struct TinyLds {
   static constexpr uint32_t N = lz_tiny_n(kTier), H = 2 * N;
@@ -153,11 +171,16 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
   const uint32_t lane = lane_id();
   const size_t w = blockIdx.x;
   for (uint32_t i = lane; i < H; i += 64) S.hs[i] = 0u;
-  uint32_t gen = 0;  // generation 0 = the cleared table
+  uint32_t gen = ws.stamp_base & 0xFFFFu;  // the cleared table is generation 0 (< any
+                                           // generation a string uses)
   wave_fence();
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   bool dead = false;
   uint32_t dbg_pops = 0, dbg_cb = 0, dbg_C = 0, dbg_qn = 0, dbg_nn = 0;
+#ifdef FSTAMD_TINY_PROF
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tl = __builtin_readcyclecounter();
+#endif
 #define TY_WD(code)                                                                  \
   if (!dead && wd_expired(t0, ws.wd_ticks)) {                                        \
     dead = true;                                                                     \
@@ -271,6 +294,10 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         }
       }
       wave_fence();
+      TY_T(0);
+#ifdef FSTAMD_TINY_PROF
+      prof[7] += 1;
+#endif
       if (pid >= nn) {  // cannot happen on a consistent heap; never read past the tables
         fail = kPathInternal;
         break;
@@ -310,6 +337,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       // ---- candidates of the 4 phases in reference order ----
       prepare_chain(rhs, cl, P);
       const uint32_t C = P.n1 + P.n2 + P.n3 + P.n4;
+      TY_T(1);
       relax_count += C;
       wd_work += C + 16u;
       double cur_dist = pdist;  // dist[curr_id]; changes only through a self-loop
@@ -342,6 +370,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
             slot = (slot + 1) & hmask;
           }
         }
+        TY_T(2);
         // first-occurrence dedup of new tuples in lane order
         const bool need = act && tid == kNoState;
         uint32_t leader = lane;
@@ -382,6 +411,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         if (need) tid = lt;
         nn += n_new;
         wave_fence();
+        TY_T(3);
 
         // self-loop onto the popped tuple: rare, exact one-lane path
         const unsigned long long selfm = __ballot(act && tid == pid);
@@ -474,6 +504,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           }
         }
         wave_fence();
+        TY_T(4);
         // heap updates (insert or decrease-key), one lane; the order does not matter
         unsigned long long pm = __ballot(push);
         pushes += (uint32_t)__popcll(pm);
@@ -492,6 +523,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           qn = __shfl(q, 0, 64);
         }
         wave_fence();
+        TY_T(5);
       }
       if (fail != kPathOk) break;
     }
@@ -561,8 +593,17 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       }
     }
     wave_fence();
+    TY_T(6);
   }
+#ifdef FSTAMD_TINY_PROF
+  if (lane < 8) {
+    unsigned long long v = 0;
+    for (int k = 0; k < 8; ++k) v = lane == (uint32_t)k ? prof[k] : v;
+    atomicAdd(&g_tiny_prof[lane], v);
+  }
+#endif
 }
 #undef TY_WD
+#undef TY_T
 
 }  // namespace fstamd

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <sys/resource.h>
 #include <vector>
 
 #include "../../include/fst_batch.h"
@@ -41,7 +42,7 @@ bool same(double a, double b) { return std::memcmp(&a, &b, 8) == 0; }
 
 int main(int argc, char** argv) {
   int threads = 32, calls = 1000, len = 64, T = 4096;
-  bool varied = false, free_midway = false;
+  bool varied = false, free_midway = false, light = false;
   std::string kind = "ambiguous", rhs_file, strings_file;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -53,6 +54,7 @@ int main(int argc, char** argv) {
     else if (a == "--rhs") kind = next();
     else if (a == "--varied") varied = true;
     else if (a == "--free-midway") free_midway = true;
+    else if (a == "--light-check") light = true;  // state count only (no per-arc reads)
     else if (a == "--rhs-file") rhs_file = next();
     else if (a == "--strings-file") strings_file = next();
     else {
@@ -140,7 +142,7 @@ int main(int argc, char** argv) {
         const uint32_t P = (uint32_t)e.arcs.size();
         ok = fst_mutable_num_states(r) == P + 1 && fst_mutable_start(r) == 0 &&
              same(fst_mutable_final_weight(r, P), e.fin);
-        for (uint32_t k = 0; ok && k < P; ++k) {
+        for (uint32_t k = 0; ok && !light && k < P; ++k) {
           ok = fst_mutable_get_arcs(r, k, buf.data(), 2) == 1 && buf[0].ilabel == e.arcs[k].ilabel &&
                buf[0].olabel == e.arcs[k].olabel && same(buf[0].weight, e.arcs[k].weight) &&
                buf[0].nextstate == k + 1;
@@ -150,6 +152,12 @@ int main(int argc, char** argv) {
       fst_mutable_free(r);
     }
   };
+  auto cpu_now = [] {  // process CPU seconds (user + system), all threads
+    rusage u{};
+    getrusage(RUSAGE_SELF, &u);
+    return u.ru_utime.tv_sec + u.ru_stime.tv_sec + 1e-6 * (u.ru_utime.tv_usec + u.ru_stime.tv_usec);
+  };
+  const double cpu0 = cpu_now();
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (int t = 0; t < threads; ++t) th.emplace_back(worker, t);
@@ -161,13 +169,15 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   const double secs =
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const double cpu_s = cpu_now() - cpu0;
   if (!free_midway) fst_free(rhs);
   std::printf(
       "{\"threads\": %d, \"calls_per_thread\": %d, \"len\": %d, \"rhs\": \"%s\", "
       "\"transducer_len\": %d, \"varied\": %s, \"free_midway\": %s, \"seconds\": %.4f, "
-      "\"calls_per_s\": %.1f, \"mismatches\": %ld, \"invalid_after_free\": %ld}\n",
+      "\"calls_per_s\": %.1f, \"cpu_seconds\": %.3f, \"mismatches\": %ld, "
+      "\"invalid_after_free\": %ld}\n",
       threads, calls, len, kind.c_str(), T, varied ? "true" : "false",
-      free_midway ? "true" : "false", secs, threads * (double)calls / secs, mismatches.load(),
-      invalid.load());
+      free_midway ? "true" : "false", secs, threads * (double)calls / secs, cpu_s,
+      mismatches.load(), invalid.load());
   return mismatches.load() == 0 ? 0 : 1;
 }

@@ -36,6 +36,10 @@ def main():
     ap.add_argument("--transducer-len", type=int, default=4096)
     ap.add_argument("--rhs", default="ambiguous")
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--light-check", action="store_true",
+                    help="--wetext: check the state count only (no per-arc API reads)")
+    ap.add_argument("--stderr-to", default="",
+                    help="--wetext: keep the tool's stderr (FSTAMD_HOST_PROF / ROUTE_LOG lines)")
     ap.add_argument("--wetext", action="store_true",
                     help="the WeText-scale tagger stand-in and 4,096 of its utterances "
                          "(libfst_amd/wetext_standin.py) instead of a bench rhs")
@@ -86,7 +90,11 @@ def wetext(a):
         f.write(labels.astype(np.uint32).tobytes())
     for t in [int(x) for x in a.threads.split(",")]:
         r = subprocess.run([TOOL, "--threads", str(t), "--calls", str(a.calls), "--rhs-file", bpath,
-                            "--strings-file", spath], capture_output=True, text=True, timeout=600)
+                            "--strings-file", spath] + (["--light-check"] if a.light_check else []),
+                           capture_output=True, text=True, timeout=600)
+        if a.stderr_to:
+            with open(f"{a.stderr_to}.{t}", "w") as f:
+                f.write(r.stderr)
         line = json.loads(r.stdout.strip().splitlines()[-1])
         line["rc"] = r.returncode
         line["rhs"] = "WeText-scale tagger stand-in (0.43 M states), 4,096 utterances"

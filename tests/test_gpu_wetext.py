@@ -96,3 +96,18 @@ def test_two_stage_pipeline(standin, sem, shards):
     out = bytes(int(x) - 1 for x in got.olabels[int(got.offsets[i]):int(got.offsets[i + 1])] if x)
     out.decode("utf-8")
     assert b"w{" not in out and b"n{" not in out
+
+
+@pytest.mark.parametrize("start", ["", "1", "2"])
+def test_lds_replay_generation_wrap(standin, start, monkeypatch):
+    # lazy_tiny_kernel's hash generation starts near its wrap (65536) and 8 waves take the
+    # batch, so every wave clears its table mid-launch and reuses it; the direct 1024-tuple
+    # size (no start forced) and the 128 / 256 sizes each
+    monkeypatch.setenv("FSTAMD_TINY_GEN0", "65500")
+    monkeypatch.setenv("FSTAMD_TINY_WAVES", "8")
+    if start:
+        monkeypatch.setenv("FSTAMD_LAZY_TINY_START", start)
+    tb, _, tag, _ = standin
+    labels, offsets = W.utterances(np.random.default_rng(77), 700)
+    got, ref = check(tb, labels, offsets, LAZY, rhs=tag)
+    assert (got.status == F.FST_PATH_OK).all()
