@@ -24,6 +24,10 @@
 #include <mutex>
 #include <new>
 #include <shared_mutex>
+
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <thread>
 #include <vector>
 
@@ -1475,15 +1479,38 @@ struct ChainCall {
   // result
   FstError err = FST_OOM;
   int32_t status = kPathInternal;
-  std::vector<Arc> arcs;
+  // the batch's host result, shared by its callers: each copies its own path out (the
+  // leader allocating and the callers freeing one arc vector per call had the callers
+  // queue on the leader's malloc arena)
+  std::shared_ptr<const HostPaths> paths;
+  uint32_t index = 0;
   double fin = 0;
   LaunchStats stats;
-  // combiner hand-off (under ChainCombiner::mu): each waiter sleeps on its own condition,
-  // so a finished batch wakes exactly its callers and one queued caller to lead next
-  std::condition_variable cv;
-  bool done = false;
-  bool taken = false;  // in a leader's batch
+  // combiner hand-off: each caller sleeps on its own word (a futex), so a finished batch
+  // wakes exactly its callers, which return without touching the combiner's lock, and one
+  // queued caller to lead next.  The queue and the leader count stay under
+  // ChainCombiner::mu; the lock-free word took the wake-ups of 256 waiting threads off it
+  // (each had re-taken the lock on waking: half the process's CPU time at 256 threads).
+  std::atomic<uint32_t> word{0};  // kCallWaiting / kCallLead / kCallDone
+  bool taken = false;             // in a leader's batch (under ChainCombiner::mu)
 };
+constexpr uint32_t kCallWaiting = 0, kCallLead = 1, kCallDone = 2;
+
+void call_wake(std::atomic<uint32_t>& w) {
+  // after a post the caller may already have returned and its frame be reused: a wake on
+  // that address is at most a spurious one, and every waiter re-checks its word
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+void call_wait(std::atomic<uint32_t>& w) {  // until the word leaves kCallWaiting
+  while (w.load(std::memory_order_acquire) == kCallWaiting)
+    syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAIT_PRIVATE, kCallWaiting, nullptr,
+            nullptr, 0);
+}
+// a queued caller (under ChainCombiner::mu): a leader slot is free
+void call_hint_lead(ChainCall* c) {
+  uint32_t z = kCallWaiting;
+  if (c->word.compare_exchange_strong(z, kCallLead, std::memory_order_acq_rel)) call_wake(c->word);
+}
 
 struct ChainCombiner {
   std::mutex mu;
@@ -1525,7 +1552,8 @@ void run_chain_calls(int dev, std::vector<ChainCall*>& calls) {
     for (uint32_t i = 0; i < num; ++i)
       std::copy(calls[g0 + i]->labels->begin(), calls[g0 + i]->labels->end(),
                 labels.begin() + offs[i]);
-    HostPaths h;
+    auto hp = std::make_shared<HostPaths>();
+    HostPaths& h = *hp;
     FstError e = FST_INVALID_ARG;
     HostProf prof;  // FSTAMD_HOST_PROF=1: the phases of this coalesced batch
     t_prof = prof.on ? &prof : nullptr;
@@ -1550,11 +1578,8 @@ void run_chain_calls(int dev, std::vector<ChainCall*>& calls) {
       c->status = h.status[i];
       if (c->status != kPathOk) continue;
       c->fin = h.fin[i];
-      c->arcs.resize(h.len[i]);
-      for (uint32_t k = 0; k < h.len[i]; ++k) {
-        const uint64_t o = h.off[i] + k;
-        c->arcs[k] = Arc{h.il[o], h.ol[o], h.w[o], k + 1};
-      }
+      c->paths = hp;
+      c->index = i;
     }
     g0 = g1;
   }
@@ -1577,8 +1602,14 @@ FstError coalesced_chain_call(int dev, ChainCall* c) {
   // a call leads when a leader slot is free and no leader has taken it yet; a slot is only
   // ever taken here, by the thread itself under the lock, and given back by the same thread
   // after its batch, so slots can be neither lost nor duplicated (round-3 ADVICE)
-  c->cv.wait(lk, [&] { return c->done || (!c->taken && C.leaders < chain_leaders()); });
-  if (c->done) return c->err;
+  while (c->taken || C.leaders >= chain_leaders()) {
+    lk.unlock();
+    call_wait(c->word);
+    lk.lock();
+    if (c->word.load(std::memory_order_acquire) == kCallDone) return c->err;
+    uint32_t h = kCallLead;  // hinted: look again (a done word is never rewritten)
+    c->word.compare_exchange_strong(h, kCallWaiting, std::memory_order_acq_rel);
+  }
   ++C.leaders;
   // this call first, then the oldest queued ones
   auto it = std::find(C.q.begin(), C.q.end(), c);
@@ -1589,16 +1620,17 @@ FstError coalesced_chain_call(int dev, ChainCall* c) {
   C.q.erase(C.q.begin(), C.q.begin() + take);
   for (ChainCall* x : batch) x->taken = true;
   // a second free slot: let the oldest remaining caller lead a batch beside this one
-  if (!C.q.empty() && C.leaders < chain_leaders()) C.q.front()->cv.notify_one();
+  if (!C.q.empty() && C.leaders < chain_leaders()) call_hint_lead(C.q.front());
   lk.unlock();
   run_chain_calls(dev, batch);
-  lk.lock();
   for (ChainCall* x : batch) {
-    x->done = true;
-    if (x != c) x->cv.notify_one();
+    if (x == c) continue;
+    x->word.store(kCallDone, std::memory_order_release);
+    call_wake(x->word);
   }
+  lk.lock();
   --C.leaders;
-  if (!C.q.empty()) C.q.front()->cv.notify_one();
+  if (!C.q.empty()) call_hint_lead(C.q.front());
   return c->err;
 }
 
@@ -1856,11 +1888,14 @@ FstMutableHandle fst_compose_frozen_shortest_path(FstMutableHandle a_handle, Fst
       const FstError e = coalesced_chain_call(current_device(), &c);
       if (e == FST_OK) {
         if (c.status == kPathOk) {
-          const uint32_t P = (uint32_t)c.arcs.size();
+          const HostPaths& h = *c.paths;
+          const uint32_t P = h.len[c.index];
+          const uint64_t o = h.off[c.index];
           result.add_states(P + 1);
           result.set_start(0);
           result.set_final(P, c.fin);
-          for (uint32_t k = 0; k < P; ++k) result.add_arc(k, c.arcs[k]);
+          for (uint32_t k = 0; k < P; ++k)
+            result.add_arc(k, Arc{h.il[o + k], h.ol[o + k], h.w[o + k], k + 1});
           rc = 0;
         } else if (c.status == kPathEmpty) {
           rc = 0;  // the empty FST

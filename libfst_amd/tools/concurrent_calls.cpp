@@ -16,6 +16,7 @@
 // (u32 count, u64 offsets[count + 1], u32 labels = byte + 1), e.g. the WeText-scale tagger
 // stand-in and its utterances (scripts/concurrent_calls_bench.py --wetext).
 // prints one JSON line: calls/s, mismatches, invalid results.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -25,6 +26,12 @@
 #include <thread>
 #include <sys/resource.h>
 #include <vector>
+
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
 
 #include "../../include/fst_batch.h"
 
@@ -37,6 +44,51 @@ struct Expect {
 };
 
 bool same(double a, double b) { return std::memcmp(&a, &b, 8) == 0; }
+
+// CC_PROF=<file>: a CPU sampling profile of the timed region (SIGPROF every 200 us of process
+// CPU time; the interrupted thread's program counter), written as "<object> <offset>" lines
+// for addr2line.
+constexpr int kMaxSamples = 1 << 16, kDepth = 12;
+void* g_samples[kMaxSamples][kDepth];
+std::atomic<int> g_nsamples{0};
+void on_prof(int, siginfo_t*, void* ctx) {
+  const int i = g_nsamples.fetch_add(1, std::memory_order_relaxed);
+  if (i >= kMaxSamples) return;
+  g_samples[i][0] = (void*)((ucontext_t*)ctx)->uc_mcontext.gregs[REG_RIP];
+  void* fr[kDepth + 2] = {};
+  const int n = backtrace(fr, kDepth + 2);  // [0] this handler, [1] the signal trampoline
+  for (int k = 1; k < kDepth; ++k) g_samples[i][k] = k + 1 < n ? fr[k + 1] : nullptr;
+}
+void prof_start() {
+  void* warm[4];
+  backtrace(warm, 4);  // loads the unwinder outside the handler
+  struct sigaction sa {};
+  sa.sa_sigaction = on_prof;
+  sa.sa_flags = SA_SIGINFO | SA_RESTART;
+  sigaction(SIGPROF, &sa, nullptr);
+  itimerval it{{0, 200}, {0, 200}};
+  setitimer(ITIMER_PROF, &it, nullptr);
+}
+void prof_stop(const char* path) {
+  itimerval it{};
+  setitimer(ITIMER_PROF, &it, nullptr);
+  FILE* f = std::fopen(path, "w");
+  if (!f) return;
+  const int n = std::min(g_nsamples.load(), kMaxSamples);
+  for (int i = 0; i < n; ++i) {  // one line per sample: "<object>:<offset>" frames, pc first
+    for (int k = 0; k < kDepth && g_samples[i][k]; ++k) {
+      Dl_info d{};
+      void* pc = g_samples[i][k];
+      if (dladdr(pc, &d) && d.dli_fname)
+        std::fprintf(f, "%s%s:%#lx", k ? " " : "", d.dli_fname,
+                     (unsigned long)((char*)pc - (char*)d.dli_fbase));
+      else
+        std::fprintf(f, "%s?:%p", k ? " " : "", pc);
+    }
+    std::fprintf(f, "\n");
+  }
+  std::fclose(f);
+}
 
 }  // namespace
 
@@ -157,6 +209,8 @@ int main(int argc, char** argv) {
     getrusage(RUSAGE_SELF, &u);
     return u.ru_utime.tv_sec + u.ru_stime.tv_sec + 1e-6 * (u.ru_utime.tv_usec + u.ru_stime.tv_usec);
   };
+  const char* prof_path = std::getenv("CC_PROF");
+  if (prof_path) prof_start();
   const double cpu0 = cpu_now();
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
@@ -170,6 +224,7 @@ int main(int argc, char** argv) {
   const double secs =
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   const double cpu_s = cpu_now() - cpu0;
+  if (prof_path) prof_stop(prof_path);
   if (!free_midway) fst_free(rhs);
   std::printf(
       "{\"threads\": %d, \"calls_per_thread\": %d, \"len\": %d, \"rhs\": \"%s\", "
