@@ -119,6 +119,57 @@ __device__ __forceinline__ void span_by_ilabel(const RhsView& r, uint32_t s, uin
   hi = off + a;
 }
 
+// arcsByIlabel for a wave-uniform state with many arcs (the wave-per-string replays: a
+// tagger's root and boundary states carry ~100-300 arcs, one per UTF-8 lead byte).  The
+// two binary searches above are chains of ~2 log2(n) dependent loads (the root of the
+// WeText-scale stand-in: ~18 round trips per pop); here the whole wave counts the arcs
+// below / up to `label`, 8 chunks of 64 ilabels per round trip, and past 512 arcs a first
+// round samples 64 evenly spaced ilabels to narrow each bound to one window of n / 64.
+// Every lane must be active (uniform control flow); lo, hi come out wave-uniform.
+__device__ __forceinline__ void wave_count_ilabels(const RhsView& r, uint32_t base, uint32_t n,
+                                                   uint32_t label, uint32_t& lt, uint32_t& le) {
+  const uint32_t lane = threadIdx.x & 63;
+  lt = 0;
+  le = 0;
+  for (uint32_t b0 = 0; b0 < n; b0 += 512) {
+    uint32_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t i = b0 + k * 64 + lane;
+      x[k] = i < n ? r.il[FB(base + i, r.num_arcs, 5)] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool v = b0 + k * 64 + lane < n;
+      lt += (uint32_t)__popcll(__ballot(v && x[k] < label));
+      le += (uint32_t)__popcll(__ballot(v && x[k] <= label));
+    }
+  }
+}
+__device__ __forceinline__ void wave_span_by_ilabel(const RhsView& r, uint32_t off, uint32_t n,
+                                                    uint32_t label, uint32_t& lo, uint32_t& hi) {
+  if (n <= 512) {
+    uint32_t lt, le;
+    wave_count_ilabels(r, off, n, label, lt, le);
+    lo = off + lt;
+    hi = off + le;
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  auto q = [n](uint32_t k) { return (uint32_t)(((uint64_t)k * n) >> 6); };
+  const uint32_t smp = r.il[FB(off + q(lane), r.num_arcs, 6)];
+  const uint32_t klt = (uint32_t)__popcll(__ballot(smp < label));
+  const uint32_t kle = (uint32_t)__popcll(__ballot(smp <= label));
+  // the first arc with ilabel >= label lies in [q(k - 1) + 1, q(k)] for k = klt (q(64) = n)
+  const uint32_t a0 = klt ? q(klt - 1) + 1 : 0, a1 = klt < 64 ? q(klt) : n;
+  const uint32_t b0 = kle ? q(kle - 1) + 1 : 0, b1 = kle < 64 ? q(kle) : n;
+  uint32_t lt, le, dummy;
+  wave_count_ilabels(r, off + a0, a1 - a0, label, lt, dummy);
+  wave_count_ilabels(r, off + b0, b1 - b0, label, dummy, le);
+  lo = off + a0 + lt;
+  hi = off + b0 + le;
+}
+
 // arcsByIlabel (src/fst.zig:112-136) with the per-state summary: one 16-B load when all
 // arcs of the state share an ilabel (or it has none), binary search otherwise.
 // kTwo: answer a two-label state (RhsView::sspan2) without the search.  Only the general

@@ -408,12 +408,12 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       }
       wave_lds_sync();
     } else {
-      uint32_t hi;
+      uint32_t hi;  // many arcs: counted by the whole wave (no dependent search chain)
       if (has1) {
-        span_by_ilabel(rhs, s, label, lo1, hi);
+        wave_span_by_ilabel(rhs, aoff, na, label, lo1, hi);
         n1 = hi - lo1;
       }
-      span_by_ilabel(rhs, s, kEpsilon, lo3, hi);
+      wave_span_by_ilabel(rhs, aoff, na, kEpsilon, lo3, hi);
       C = n1 + (hi - lo3);
       if (near_end) {
         for (uint32_t c = lane; c < C; c += 64) {

@@ -369,12 +369,12 @@ __device__ __forceinline__ void lazy_dense_string(const RhsView& rhs, const Chai
       }
       wave_lds_sync();
     } else {
-      uint32_t hi;
+      uint32_t hi;  // many arcs: counted by the whole wave (no dependent search chain)
       if (has1) {
-        span_by_ilabel(rhs, s, label, lo1, hi);
+        wave_span_by_ilabel(rhs, aoff, na, label, lo1, hi);
         n1 = hi - lo1;
       }
-      span_by_ilabel(rhs, s, kEpsilon, lo3, hi);
+      wave_span_by_ilabel(rhs, aoff, na, kEpsilon, lo3, hi);
       C = n1 + (hi - lo3);
     }
     relax += C;

@@ -139,9 +139,10 @@ __device__ __forceinline__ void prepare_chain(const RhsView& rhs, const ChainLhs
     hi3 = off + (uint32_t)__popcll(__ballot(v && x == kEpsilon));
     lo1 = off + (uint32_t)__popcll(__ballot(v && x < P.label));
     hi1 = off + (uint32_t)__popcll(__ballot(v && x <= P.label));
-  } else {
-    span_by_ilabel(rhs, P.s2, kEpsilon, lo3, hi3);
-    if (has_arc && P.label != kEpsilon) span_by_ilabel(rhs, P.s2, P.label, lo1, hi1);
+  } else {  // many arcs: the leading epsilon run from the summary, the label's run counted
+    lo3 = off;
+    hi3 = off + ss.w;
+    if (has_arc && P.label != kEpsilon) wave_span_by_ilabel(rhs, off, n, P.label, lo1, hi1);
   }
   P.lo3 = lo3;
   const uint32_t ne = hi3 - lo3;
