@@ -6,7 +6,7 @@
 // like lazy_wave.hpp (its candidate enumeration, first-touch id assignment and lane-order
 // folding are shared and documented there), but laid out for occupancy: the replay waits
 // on two dependent rhs reads per pop, so the rate is resident strings per CU, and that is
-// LDS per string.  36 B per tuple instead of lazy_wave's 108 B:
+// LDS per string.  34 B per tuple instead of lazy_wave's 108 B:
 //  * hash slots are one word, (generation << 16) | id; the key is checked in nkey[id].  The
 //    generation advances per string (the table is cleared when it wraps), so nothing is
 //    cleared between strings;
@@ -15,14 +15,18 @@
 //    the olabel and the weight are the rhs arc's (phase 2 has none: epsilon, One), read
 //    back from the frozen rhs when the path is written -- the tie-break of :110-128 needs
 //    the olabel only on an exact tie from the same pop and then reads it;
-//  * the queue is an indexed 64-ary heap of ids (2 B) with positions (2 B) and
-//    decrease-key, keyed by (dist[id], id).  Its pop order is the reference's lazy-deletion
-//    binary heap's: both pop the minimum (dist, id) over the ids pushed and not yet
-//    settled -- a stale entry of the lazy heap has a dist above dist[id], a settled id
-//    is skipped there and absent here -- so the ids, the paths and the weights are the
-//    same bits.  Heap size <= tuples: no queue overflow.
-// Sizes: tier t holds 64 << t tuples; 1 (128) = 6.1 KB, 2 (256) = 10.7 KB, 3 (512) = 19.9
-// KB, 4 (1024) = 38.4 KB.  A string that outgrows its tier ends OVERFLOW and the host reruns
+//  * the queue is the frontier itself: an unordered array of the ids pushed and not yet
+//    settled (2 B each, an in-frontier flag in the back pointer), popped by one wave
+//    argmin of (dist[id], id) and appended to in parallel (no sift, no per-push lane-0
+//    loop; a better dist needs no queue update at all).  Its pop order is the reference's
+//    lazy-deletion binary heap's: both pop the minimum (dist, id) over the ids pushed and
+//    not yet settled -- a stale entry of the lazy heap has a dist above dist[id], a
+//    settled id is skipped there and absent here -- so the ids, the paths and the weights
+//    are the same bits.  Frontier size <= tuples: no queue overflow.
+//  * one loop groups a chunk's candidates by tuple key: its leaders are the first-touch
+//    owners of new tuples (getOrCreate in lane order) and the folding lanes alike.
+// Sizes: tier t holds 64 << t tuples at 34 B; 1 (128) = 5.9 KB, 2 (256) = 10.2 KB, 3 (512)
+// = 18.9 KB, 4 (1024) = 36.4 KB.  A string that outgrows its tier ends OVERFLOW and the host reruns
 // it in the next (DeviceEngine::run_chain).
 #pragma once
 
@@ -30,12 +34,13 @@
 
 namespace fstamd {
 
-constexpr uint32_t kTyNone = 0xFFFFu;       // pos[] of an id not in the heap
 constexpr uint32_t kTyPrev = 0xFFFFu;       // nback.x bits 0..15: the previous tuple's id
 constexpr uint32_t kTySettled = 1u << 16;
 constexpr uint32_t kTyHasBack = 1u << 17;
 constexpr uint32_t kTyConsumed = 1u << 18;  // the move read the lhs label (phases 1, 2, 4)
 constexpr uint32_t kTyArc = 1u << 19;       // nback.y is an rhs arc index (not phase 2)
+constexpr uint32_t kTyInQ = 1u << 20;       // in the frontier
+constexpr uint32_t kTyKeep = kTySettled | kTyInQ;  // kept when the back pointer changes
 
 // FSTAMD_TINY_PROF (a debug build): cycles per phase summed over every wave, printed by
 // DeviceEngine::run_lazy_tiny -- [0] pop, [1] popped tuple + final + arc spans, [2] candidate
@@ -68,8 +73,7 @@ struct TinyLds {
   uint32_t col[64];
   uint32_t ccode[64];
   uint32_t cid[64];
-  uint16_t qid[N];
-  uint16_t pos[N];
+  uint16_t qid[N];             // the frontier (unordered), then the path's ids
 };
 
 struct TyCand {
@@ -143,24 +147,6 @@ __device__ __forceinline__ bool tiny_take(const RhsView& rhs, double nd, uint32_
   return ol < bol;
 }
 
-// Insert id t with dist d, or move it up after its dist decreased (one lane).
-template <int kTier>
-__device__ __forceinline__ void tiny_heap_update(TinyLds<kTier>& S, uint32_t& qn, uint32_t t,
-                                                 double d) {
-  uint32_t q = S.pos[t];
-  if (q == kTyNone) q = qn++;
-  while (q > 0) {
-    const uint32_t pq = (q - 1) >> 6;
-    const uint32_t pi = S.qid[pq];
-    if (!qless(d, t, S.ndist[pi], pi)) break;
-    S.qid[q] = (uint16_t)pi;
-    S.pos[pi] = (uint16_t)q;
-    q = pq;
-  }
-  S.qid[q] = (uint16_t)t;
-  S.pos[t] = (uint16_t)q;
-}
-
 template <int kTier>
 __global__ void __launch_bounds__(64, kTier == 1 ? 5 : kTier == 2 ? 4 : kTier == 3 ? 2 : 1)
 lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* next_item,
@@ -232,10 +218,9 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       const unsigned long long k0 = tuple_key(0, rhs.start, 0);
       S.nkey[0] = k0;
       S.ndist[0] = w_one();
-      S.nback[0] = make_uint2(0u, 0u);
+      S.nback[0] = make_uint2(kTyInQ, 0u);
       S.hs[hmix(k0) & hmask] = gen << 16;
       S.qid[0] = 0;
-      S.pos[0] = 0;
     }
     wave_fence();
 
@@ -257,42 +242,31 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         fail = kPathInternal;
         break;
       }
-      // ---- pop the minimum (dist, id); the last entry sifts down from the root ----
-      const uint32_t pid = S.qid[0];
-      const double pdist = S.ndist[pid];
-      --qn;
-      if (qn > 0) {
-        const uint32_t xi = S.qid[qn];
-        const double xd = S.ndist[xi];
-        uint32_t i = 0;
-        for (;;) {
-          const uint32_t c0 = i * 64 + 1;
-          if (c0 >= qn) break;
-          const uint32_t cc = c0 + lane;
-          const bool v = cc < qn;
-          const uint32_t ci = v ? (uint32_t)S.qid[cc] : 0u;
-          const double cd = v ? S.ndist[ci] : 0.0;
-          // the minimum child: min dist, then min id (heap ids are distinct); -0.0 == +0.0
-          // as in qless, and only qless sees the value
-          const double dmn = __ockl_wfred_min_f64(v ? cd : __builtin_huge_val());
-          const bool c1 = v && cd == dmn;
-          const uint32_t mi = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(c1 ? ci : ~0u));
-          const uint32_t mp = c0 + (uint32_t)__ffsll((long long)__ballot(c1 && ci == mi)) - 1;
-          if (qless(dmn, mi, xd, xi)) {
-            if (lane == 0) {
-              S.qid[i] = (uint16_t)mi;
-              S.pos[mi] = (uint16_t)i;
-            }
-            i = mp;
-          } else {
-            break;
+      // ---- pop: the frontier's minimum (dist, id) (ids distinct), the last entry moves
+      // into its place ----
+      double bd = __builtin_huge_val();
+      uint32_t bi = kNoState, bp = 0;
+      for (uint32_t c0 = 0; c0 < qn; c0 += 64) {
+        const uint32_t cc = c0 + lane;
+        if (cc < qn) {
+          const uint32_t id = S.qid[cc];
+          const double d = S.ndist[id];
+          if (bi == kNoState || qless(d, id, bd, bi)) {
+            bd = d;
+            bi = id;
+            bp = cc;
           }
         }
-        if (lane == 0) {
-          S.qid[i] = (uint16_t)xi;
-          S.pos[xi] = (uint16_t)i;
-        }
       }
+      // min dist, then min id among those; -0.0 == +0.0 as in qless (the exact dist is
+      // read back from ndist below)
+      const double dmn = __ockl_wfred_min_f64(bi != kNoState ? bd : __builtin_huge_val());
+      const bool c1 = bi != kNoState && bd == dmn;
+      const uint32_t pid = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_u32(c1 ? bi : ~0u));
+      const uint32_t wl = (uint32_t)__ffsll((long long)__ballot(c1 && bi == pid)) - 1;
+      const uint32_t ppos = __builtin_amdgcn_readlane(bp, wl);
+      --qn;
+      if (lane == 0) S.qid[ppos] = S.qid[qn];
       wave_fence();
       TY_T(0);
 #ifdef FSTAMD_TINY_PROF
@@ -303,14 +277,12 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         break;
       }
       const uint2 pb = S.nback[pid];
-      if (pb.x & kTySettled) {
+      const double pdist = S.ndist[pid];
+      if ((pb.x & kTySettled) || !(pb.x & kTyInQ)) {
         fail = kPathInternal;
         break;
       }
-      if (lane == 0) {
-        S.nback[pid].x = pb.x | kTySettled;
-        S.pos[pid] = (uint16_t)kTyNone;
-      }
+      if (lane == 0) S.nback[pid].x = (pb.x & ~kTyInQ) | kTySettled;
       const unsigned long long pk = S.nkey[pid];
       PopCands P;
       P.s1 = (uint32_t)(pk & 0xFFFFFFFFull) >> 2;
@@ -371,21 +343,26 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           }
         }
         TY_T(2);
-        // first-occurrence dedup of new tuples in lane order
-        const bool need = act && tid == kNoState;
+        // group the chunk by tuple key in lane order: a group's first lane leads it --
+        // the first touch of a new tuple (getOrCreate: ids by first occurrence in lane
+        // order) and the lane that folds the group's relaxations
+        unsigned long long gmask = 0;
         uint32_t leader = lane;
-        unsigned long long pending = __ballot(need);
-        while (pending) {
-          const uint32_t l = (uint32_t)__ffsll((long long)pending) - 1;
-          const unsigned long long lk =
-              ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(x.key >> 32), l) << 32) |
-              (uint32_t)__builtin_amdgcn_readlane((uint32_t)x.key, l);
-          const bool same = need && x.key == lk;
-          const unsigned long long m = __ballot(same);
-          if (same) leader = l;
-          pending &= ~m;
+        {
+          unsigned long long pend = __ballot(act);
+          while (pend) {
+            const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
+            const unsigned long long lk =
+                ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(x.key >> 32), l) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((uint32_t)x.key, l);
+            const bool same = act && x.key == lk;
+            const unsigned long long m = __ballot(same);
+            if (lane == l) gmask = m;
+            if (same) leader = l;
+            pend &= ~m;
+          }
         }
-        const bool is_new_leader = need && leader == lane;
+        const bool is_new_leader = gmask && tid == kNoState;
         const unsigned long long nlm = __ballot(is_new_leader);
         const uint32_t n_new = (uint32_t)__popcll(nlm);
         if (nn + n_new > N) {
@@ -405,10 +382,11 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           S.nkey[tid] = x.key;
           S.ndist[tid] = w_zero();
           S.nback[tid] = make_uint2(0u, 0u);
-          S.pos[tid] = (uint16_t)kTyNone;
         }
-        const uint32_t lt = __shfl(tid, (int)leader, 64);
-        if (need) tid = lt;
+        if (n_new) {
+          const uint32_t lt = __shfl(tid, (int)leader, 64);
+          if (act) tid = lt;
+        }
         nn += n_new;
         wave_fence();
         TY_T(3);
@@ -434,13 +412,13 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
               bool bol_known = false;
               if (tiny_take(rhs, nd, (code & kTyConsumed) ? P.label : kEpsilon, S.col[i], od, b,
                             pid, P.label, bol, bol_known)) {
+                const bool add = !(b.x & kTyKeep);  // neither settled nor in the frontier
                 S.ndist[t] = nd;
-                S.nback[t] = make_uint2(pid | (b.x & kTySettled) | kTyHasBack | code, S.carc[i]);
+                S.nback[t] = make_uint2(pid | (b.x & kTyKeep) | (add ? kTyInQ : 0u) | kTyHasBack |
+                                            code, S.carc[i]);
                 if (t == pid) cur_dist = nd;
-                if (!(b.x & kTySettled)) {
-                  tiny_heap_update(S, qn, t, nd);
-                  ++pushes;
-                }
+                if (add) S.qid[qn++] = (uint16_t)t;
+                if (!(b.x & kTySettled)) ++pushes;
               }
             }
           }
@@ -458,20 +436,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         S.ccode[lane] = x.code;
         S.carc[lane] = x.arc;
         wave_fence();
-        unsigned long long gmask = 0;
-        {
-          unsigned long long pend = __ballot(act);
-          while (pend) {
-            const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
-            const uint32_t lt2 = __builtin_amdgcn_readlane(tid, l);
-            const bool same = act && tid == lt2;
-            const unsigned long long m = __ballot(same);
-            if (lane == l) gmask = m;
-            pend &= ~m;
-          }
-        }
-        bool push = false;
-        double push_d = 0.0;
+        bool push = false, app = false;
         if (gmask) {  // group leader
           const uint32_t t = tid;
           double od = S.ndist[t];
@@ -488,40 +453,27 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
             if (tiny_take(rhs, cnd, (code & kTyConsumed) ? P.label : kEpsilon, col, od, b, pid,
                           P.label, bol, bol_known)) {
               od = cnd;
-              b = make_uint2(pid | (b.x & kTySettled) | kTyHasBack | code, S.carc[i]);
+              b = make_uint2(pid | (b.x & kTyKeep) | kTyHasBack | code, S.carc[i]);
               bol = col;
               bol_known = true;
               took = true;
             }
           }
           if (took) {
+            push = !(b.x & kTySettled);
+            app = !(b.x & kTyKeep);  // pushed, and not yet in the frontier
+            if (app) b.x |= kTyInQ;
             S.ndist[t] = od;
             S.nback[t] = b;
-            if (!(b.x & kTySettled)) {
-              push = true;
-              push_d = od;
-            }
           }
         }
-        wave_fence();
         TY_T(4);
-        // heap updates (insert or decrease-key), one lane; the order does not matter
-        unsigned long long pm = __ballot(push);
-        pushes += (uint32_t)__popcll(pm);
-        if (pm) {
-          uint32_t q = qn;
-          while (pm) {
-            const uint32_t l = (uint32_t)__ffsll((long long)pm) - 1;
-            pm &= pm - 1;
-            const unsigned long long pb2 = (unsigned long long)__double_as_longlong(push_d);
-            const double xd = __longlong_as_double(
-                (long long)(((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pb2 >> 32), l) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)pb2, l)));
-            const uint32_t xi = __builtin_amdgcn_readlane(tid, l);
-            if (lane == 0) tiny_heap_update(S, q, xi, xd);
-          }
-          qn = __shfl(q, 0, 64);
-        }
+        // pushes: new frontier entries appended in lane order (a better dist of an id in
+        // the frontier needs nothing: the pop reads dist[id])
+        pushes += (uint32_t)__popcll(__ballot(push));
+        const unsigned long long am = __ballot(app);
+        if (app) S.qid[qn + (uint32_t)__popcll(am & lanemask_lt())] = (uint16_t)tid;
+        qn += (uint32_t)__popcll(am);
         wave_fence();
         TY_T(5);
       }
