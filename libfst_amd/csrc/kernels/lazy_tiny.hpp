@@ -63,6 +63,15 @@ __device__ unsigned long long g_tiny_prof[8];
 template <int kTier>
 struct TinyLds {
   static constexpr uint32_t N = lz_tiny_n(kTier), H = 2 * N;
+  // the rhs state summary (RhsView::sspan) of each tuple's s2, loaded when the tuple is
+  // created (its latency hidden behind the rest of that chunk) so that a pop starts with
+  // no global round trip: the latency-bound sizes only (3, 4: small batches, single calls)
+#ifdef FSTAMD_TY_NOCACHE  // A/B builds
+  static constexpr bool kCache = false;
+#else
+  static constexpr bool kCache = kTier >= 3;
+#endif
+  uint4 span[kCache ? N : 1];
   unsigned long long nkey[N];  // (s2 << 32) | (s1 << 2) | filter
   double ndist[N];
   double cnd[64];              // one chunk's candidates, read by the group leaders
@@ -82,45 +91,38 @@ struct TyCand {
   double w;
 };
 
-// chain_cand (lazy_wave.hpp) with the arc index and the phase kept instead of the labels.
-__device__ __forceinline__ TyCand tiny_cand(const RhsView& rhs, const PopCands& P, uint32_t c) {
-  TyCand x;
+// Candidate c of a pop in reference order (chain_cand, lazy_wave.hpp): its rhs arc (phases
+// 1, 3, 4; none in phase 2), its code and the s1 / filter of its target key.
+__device__ __forceinline__ void tiny_cand_arc(const PopCands& P, uint32_t c, uint32_t& arc,
+                                              uint32_t& code, uint32_t& ks1, uint32_t& kf) {
   if (c < P.n1) {  // :182-224
-    x.arc = P.lo1 + c;
-    const ArcRec r = rhs.rec[x.arc];
-    x.key = tuple_key(P.s1 + 1, r.next, 0);
-    x.ol = r.olabel;
-    x.w = w_times(w_one(), r.weight);
-    x.code = kTyConsumed | kTyArc;
-    return x;
+    arc = P.lo1 + c;
+    code = kTyConsumed | kTyArc;
+    ks1 = P.s1 + 1;
+    kf = 0;
+    return;
   }
   c -= P.n1;
   if (c < P.n2) {  // :227-252
-    x.arc = 0;
-    x.key = tuple_key(P.s1 + 1, P.s2, P.f == 0 ? 2u : P.f);
-    x.ol = kEpsilon;
-    x.w = w_one();
-    x.code = kTyConsumed;
-    return x;
+    arc = 0;
+    code = kTyConsumed;
+    ks1 = P.s1 + 1;
+    kf = P.f == 0 ? 2u : P.f;
+    return;
   }
   c -= P.n2;
   if (c < P.n3) {  // :254-305
-    x.arc = P.lo3 + c;
-    const ArcRec r = rhs.rec[x.arc];
-    x.key = tuple_key(P.s1, r.next, P.f == 0 ? 1u : P.f);
-    x.ol = r.olabel;
-    x.w = r.weight;
-    x.code = kTyArc;
-    return x;
+    arc = P.lo3 + c;
+    code = kTyArc;
+    ks1 = P.s1;
+    kf = P.f == 0 ? 1u : P.f;
+    return;
   }
   c -= P.n3;  // :307-365
-  x.arc = P.lo3 + c;
-  const ArcRec r = rhs.rec[x.arc];
-  x.key = tuple_key(P.s1 + 1, r.next, 0);
-  x.ol = r.olabel;
-  x.w = w_times(w_one(), r.weight);
-  x.code = kTyConsumed | kTyArc;
-  return x;
+  arc = P.lo3 + c;
+  code = kTyConsumed | kTyArc;
+  ks1 = P.s1 + 1;
+  kf = 0;
 }
 
 // the olabel of a stored back pointer (phase 2: epsilon)
@@ -221,6 +223,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       S.nback[0] = make_uint2(kTyInQ, 0u);
       S.hs[hmix(k0) & hmask] = gen << 16;
       S.qid[0] = 0;
+      if constexpr (TinyLds<kTier>::kCache) S.span[0] = rhs.sspan[rhs.start];
     }
     wave_fence();
 
@@ -293,21 +296,69 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         break;
       }
 
-      // ---- best final (:165-179) ----
-      const double fw1 = cl.final_w(P.s1);
-      const double fw2 = rhs.final_w[P.s2];
-      if (!w_is_zero(fw1) && !w_is_zero(fw2)) {
-        const double fw = w_times(fw1, fw2);
-        const double total = w_times(pdist, fw);
-        if (best_id == kNoState || total < best_total || (total == best_total && pid < best_id)) {
-          best_id = pid;
-          best_fw = fw;
-          best_total = total;
+      // ---- best final (:165-179): a chain's only final state is s1 == L ----
+      if (P.s1 == cl.L) {
+        const double fw2 = rhs.final_w[P.s2];
+        if (!w_is_zero(fw2)) {
+          const double fw = w_times(w_one(), fw2);
+          const double total = w_times(pdist, fw);
+          if (best_id == kNoState || total < best_total ||
+              (total == best_total && pid < best_id)) {
+            best_id = pid;
+            best_fw = fw;
+            best_total = total;
+          }
         }
       }
 
-      // ---- candidates of the 4 phases in reference order ----
-      prepare_chain(rhs, cl, P);
+      // ---- arcsByIlabel for the lhs label and epsilon (prepare_chain, lazy_wave.hpp): a
+      // state of <= 64 arcs has its records and ilabels loaded together, arc j in lane j ----
+      uint4 ss;
+      if constexpr (TinyLds<kTier>::kCache) ss = S.span[pid];
+      else ss = rhs.sspan[P.s2];
+      const uint32_t off = ss.x, na = ss.y;
+      // (the batch sizes 1, 2 load each candidate's record itself: the shuffles measured
+      // 3 % slower there, where other waves hide the second round trip)
+      const bool inl = TinyLds<kTier>::kCache && na <= 64;
+      const bool has_arc = P.s1 < cl.L;
+      P.label = has_arc ? cl.labels[P.s1] : 0u;
+      ArcRec lr{0u, 0u, 0.0};
+      uint32_t lil = 0;
+      if (na <= 64 && lane < na) {
+        if (inl) lr = rhs.rec[off + lane];
+        if (ss.z == kSpanMixed) lil = rhs.il[off + lane];
+      }
+      {
+        uint32_t lo3, hi3, lo1 = 0, hi1 = 0;
+        if (ss.z != kSpanMixed) {  // one ilabel (or no arc)
+          const bool eps = ss.z == kEpsilon;
+          lo3 = off;
+          hi3 = eps ? off + na : off;
+          lo1 = off;
+          hi1 = !eps && ss.z == P.label ? off + na : off;
+        } else if (na <= 64) {
+          const bool v = lane < na;
+          lo3 = off;
+          hi3 = off + (uint32_t)__popcll(__ballot(v && lil == kEpsilon));
+          lo1 = off + (uint32_t)__popcll(__ballot(v && lil < P.label));
+          hi1 = off + (uint32_t)__popcll(__ballot(v && lil <= P.label));
+        } else {  // many arcs: the leading epsilon run from the summary, the label counted
+          lo3 = off;
+          hi3 = off + ss.w;
+          if (has_arc && P.label != kEpsilon) wave_span_by_ilabel(rhs, off, na, P.label, lo1, hi1);
+        }
+        const uint32_t ne = hi3 - lo3;
+        P.lo3 = lo3;
+        P.n1 = 0;
+        P.lo1 = 0;
+        if (has_arc && P.label != kEpsilon) {  // :182-224
+          P.lo1 = lo1;
+          P.n1 = hi1 - lo1;
+        }
+        P.n2 = (has_arc && P.label == kEpsilon && P.f != 1) ? 1u : 0u;  // :227-252
+        P.n3 = (P.f != 2) ? ne : 0u;                                     // :254-305
+        P.n4 = (has_arc && P.label == kEpsilon && P.f == 0) ? ne : 0u;  // :307-365
+      }
       const uint32_t C = P.n1 + P.n2 + P.n3 + P.n4;
       TY_T(1);
       relax_count += C;
@@ -326,7 +377,29 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         const uint32_t c = cb + lane;
         const bool act = c < C;
         TyCand x{0, 0, 0, 0, 0.0};
-        if (act) x = tiny_cand(rhs, P, c);
+        {
+          uint32_t ks1, kf;
+          tiny_cand_arc(P, c, x.arc, x.code, ks1, kf);
+          ArcRec r{0u, 0u, 0.0};
+          if (inl) {  // from the lane holding the arc (every lane takes part in the shuffles)
+            const int j = (int)((x.arc - off) & 63u);
+            r.next = __shfl(lr.next, j, 64);
+            r.olabel = __shfl(lr.olabel, j, 64);
+            r.weight = __shfl(lr.weight, j, 64);
+          } else if (act && (x.code & kTyArc)) {
+            r = rhs.rec[x.arc];
+          }
+          if (x.code & kTyArc) {
+            x.key = tuple_key(ks1, r.next, kf);
+            x.ol = r.olabel;
+            x.w = (x.code & kTyConsumed) ? w_times(w_one(), r.weight) : r.weight;
+          } else {
+            x.key = tuple_key(ks1, P.s2, kf);
+            x.ol = kEpsilon;
+            x.w = w_one();
+          }
+          if (!act) x = TyCand{0, 0, 0, 0, 0.0};
+        }
         // lookup (getOrCreate's get): the slot names an id, the id's key decides
         uint32_t tid = kNoState;
         uint32_t slot = hmix(x.key) & hmask;
@@ -383,6 +456,10 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           S.ndist[tid] = w_zero();
           S.nback[tid] = make_uint2(0u, 0u);
         }
+        uint4 new_span = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (TinyLds<kTier>::kCache) {
+          if (is_new_leader) new_span = rhs.sspan[(uint32_t)(x.key >> 32)];
+        }
         if (n_new) {
           const uint32_t lt = __shfl(tid, (int)leader, 64);
           if (act) tid = lt;
@@ -425,6 +502,9 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           cur_dist = __shfl(cur_dist, 0, 64);
           qn = __shfl(qn, 0, 64);
           pushes = __shfl(pushes, 0, 64);
+          if constexpr (TinyLds<kTier>::kCache) {
+            if (is_new_leader) S.span[tid] = new_span;
+          }
           wave_fence();
           continue;
         }
@@ -474,6 +554,9 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         const unsigned long long am = __ballot(app);
         if (app) S.qid[qn + (uint32_t)__popcll(am & lanemask_lt())] = (uint16_t)tid;
         qn += (uint32_t)__popcll(am);
+        if constexpr (TinyLds<kTier>::kCache) {
+          if (is_new_leader) S.span[tid] = new_span;
+        }
         wave_fence();
         TY_T(5);
       }
