@@ -228,7 +228,12 @@ struct DevBuf {
     }
     if (hipMalloc(&p, cls) == hipSuccess) return;
     p = nullptr;
+    (void)hipGetLastError();
     pool_release(dev);  // cached blocks of other classes back to the device, then retry
+    if (hipMalloc(&p, cls) == hipSuccess) return;
+    (void)hipGetLastError();
+    DeviceEngine::trim_idle(dev);  // and the idle engines' workspaces
+    (void)hipSetDevice(dev);
     if (hipMalloc(&p, cls) != hipSuccess) p = nullptr;
   }
   ~DevBuf() {
@@ -1024,7 +1029,7 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   if (D->has_eps || !DeviceEngine::pull_first(*D, semantics)) return kStreamNotApplicable;
   thread_local std::map<int, StreamKit> kits;
   StreamKit& K = kits[dev];
-  if (!K.init(dev) || !K.events(4)) return kStreamNotApplicable;
+  if (!K.init(dev)) return kStreamNotApplicable;
   const hipStream_t up = K.up;
   const uint64_t base0 = offsets[0], total = offsets[num] - base0;
   if (!alloc_result(out, num, total)) return FST_OOM;
@@ -1090,6 +1095,10 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   }
   cut.push_back(num);
   const size_t parts = cut.size() - 1;
+  if (parts > 64 || !K.events(parts)) {  // one upload event a part
+    fst_batch_result_free(out);
+    return kStreamNotApplicable;
+  }
 
   // ---- engines and device buffers ----
   DeviceEngine::Lease EA = DeviceEngine::acquire(dev);
@@ -1098,9 +1107,9 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   if (parts > 1) EB = DeviceEngine::try_acquire(dev);  // (none free: one engine in order)
   const hipStream_t sA = EA.stream(), sB = EB ? EB.stream() : nullptr;
   DevBuf d_lab(std::max<uint64_t>(total, 1) * 4), d_off((num + 1) * 8ull),
-      d_first(std::max<size_t>(num, 1) * 4ull);
+      d_first(std::max<size_t>(num, 1) * 4ull), d_ctr(64 * 4);  // item counter per part
   DevOut o(num, std::max<uint64_t>(total, 1));
-  if (!d_lab.p || !d_off.p || !d_first.p || !o.ok()) return FST_OOM;
+  if (!d_lab.p || !d_off.p || !d_first.p || !d_ctr.p || !o.ok()) return FST_OOM;
   PinnedVec<int32_t> first(num);
   struct SyncAll {  // every return: no kernel or copy still uses the buffers or the result
     hipStream_t s[3];
@@ -1119,7 +1128,12 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   } R;
   Threads Th;
   Th.th.emplace_back([&] {
+    // (the fills first, on the idle GPU: every string INTERNAL until a tier finishes it,
+    // the parts' item counters zero; the parts wait on events recorded after them)
     bool ok = hipSetDevice(dev) == hipSuccess &&
+              hipMemsetD32Async((hipDeviceptr_t)o.status.p, kPathInternal, num, up) == hipSuccess &&
+              hipMemsetD32Async((hipDeviceptr_t)d_first.p, kPathInternal, num, up) == hipSuccess &&
+              hipMemsetAsync(d_ctr.p, 0, 64 * 4, up) == hipSuccess &&
               hipMemcpyAsync(d_off.p, poff, (num + 1) * 8ull, hipMemcpyHostToDevice, up) ==
                   hipSuccess;
     for (size_t p = 0; p < parts && ok; ++p) {
@@ -1154,7 +1168,6 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   // ---- the parts: engine A takes parts 0, 2, .., engine B 1, 3, .. (A all without B) ----
   struct PartRun {
     FstError err = FST_OK;
-    LaunchStats st;
   };
   std::vector<PartRun> pr(parts);
   // (A/B timing only: FSTAMD_STREAM_AB=1 drops the copy-out; the result then lacks paths)
@@ -1186,25 +1199,42 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
       v.host_w = out->weights;
       if (ab_nocopy) v.host_ol = nullptr, v.host_w = nullptr;
       v.first_status = (int32_t*)d_first.p + s0;
-      // (no download here: a copy is a blit kernel, and one queued on this stream before
-      // the next part's launch would wait for CU slots the other engine's persistent kernel
-      // holds -- the downloads come after the last part)
+      // the pull tier alone: no fill, copy or host synchronisation between parts (a fill
+      // or copy is a blit kernel that waits for CU slots behind the other engine's
+      // persistent kernel, and had held this engine's next part back); the later tiers
+      // and the downloads come after the last part
       if (hipStreamWaitEvent(s, K.ev[p], 0) != hipSuccess ||
-          E->run_chain(*D, in, n, semantics, v, s, &pr[p].st) != hipSuccess) {
+          E->launch_pull_part(*D, in, n, semantics, v, s, (unsigned int*)d_ctr.p + p) !=
+              hipSuccess) {
         pr[p].err = FST_OOM;
         return;
       }
     }
   };
   if (t_prof) t_prof->lap(0);
+  const auto tk0 = std::chrono::steady_clock::now();
   {
     Threads P;
     if (EB) P.th.emplace_back([&] { drive(EB, sB, 1, 2); });
     drive(EA, sA, 0, EB ? 2 : 1);
     P.join();
   }
-  // every part's kernels are done (run_chain synchronises): statuses, final weights and
-  // the pull tier's statuses in one download each
+  for (hipStream_t x : {up, sA, sB})
+    if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
+  for (size_t p = 0; p < parts; ++p)
+    if (pr[p].err != FST_OK) return pr[p].err;
+  // the later tiers, once, over the strings the pull tier handed on (in the device arena,
+  // the same slots)
+  {
+    ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
+    BatchOutDev v = o.v;
+    v.slots = (const uint64_t*)d_off.p;
+    EA->set_after_pull(true);
+    const hipError_t e = EA->run_chain(*D, in, n, semantics, v, sA, nullptr);
+    EA->set_after_pull(false);
+    if (e != hipSuccess) return FST_OOM;
+  }
+  // statuses, final weights and the pull tier's statuses in one download each
   if (num && (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost, sA) !=
                   hipSuccess ||
               hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost,
@@ -1215,15 +1245,11 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   for (hipStream_t x : {up, sA, sB})
     if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
   Th.join();
-  LaunchStats agg{};
-  for (size_t p = 0; p < parts; ++p) {
-    if (pr[p].err != FST_OK) return pr[p].err;
-    if (p == 0) agg = pr[p].st;
-    else {
-      agg.kernel_ms += pr[p].st.kernel_ms;
-      agg.launches += pr[p].st.launches;
-    }
-  }
+  LaunchStats agg{};  // (the parts overlap on two streams: their wall time, not a sum)
+  agg.engine = semantics == 1 ? 0 : 7;
+  agg.launches = (uint32_t)parts + 1;
+  agg.kernel_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tk0).count();
   t_last_stats = agg;
   if (t_prof) t_prof->lap(2);
   const hipStream_t stream = sA;

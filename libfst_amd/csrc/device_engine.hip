@@ -518,6 +518,22 @@ DeviceEngine::DeviceEngine(int dev) : dev_(dev) {
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) stream_ = nullptr;
 }
 
+void DeviceEngine::trim_idle(int dev) {
+  if (dev < 0) return;
+  EnginePool& P = engine_pool(dev);
+  std::lock_guard<std::mutex> g(P.mu);
+  for (DeviceEngine* e : P.idle) e->free_scratch();
+}
+
+void DeviceEngine::free_scratch() {
+  (void)hipSetDevice(dev_);
+  for (size_t i = 0; i < bufs_.size(); ++i) {
+    if (bufs_[i]) (void)hipFree(bufs_[i]);  // (hipFree waits for the device's work)
+    bufs_[i] = nullptr;
+    sizes_[i] = 0;
+  }
+}
+
 void* DeviceEngine::scratch(size_t idx, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (sizes_[idx] >= bytes) return bufs_[idx];
@@ -525,8 +541,23 @@ void* DeviceEngine::scratch(size_t idx, size_t bytes) {
   bufs_[idx] = nullptr;
   sizes_[idx] = 0;
   if (hipMalloc(&bufs_[idx], bytes) != hipSuccess) {
-    bufs_[idx] = nullptr;
-    return nullptr;
+    // out of HBM: the scratch of the device's idle engines (workspaces grow and are kept
+    // per engine, so up to max_engines() sets of them) and the cached pool blocks go back,
+    // then once more (this engine's own buffers may be in use by this call's launches)
+    (void)hipGetLastError();
+    {
+      EnginePool& P = engine_pool(dev_);
+      std::lock_guard<std::mutex> g(P.mu);
+      for (DeviceEngine* e : P.idle)
+        if (e != this) e->free_scratch();
+    }
+    device_pool_release(dev_);
+    (void)hipSetDevice(dev_);
+    if (hipMalloc(&bufs_[idx], bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      bufs_[idx] = nullptr;
+      return nullptr;
+    }
   }
   sizes_[idx] = bytes;
   return bufs_[idx];
@@ -593,18 +624,15 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   HIP_TRY(hipSetDevice(dev_));
   // the pull tiers alone copy paths out to the host (they must come first)
   if (out.host_ol && !pull_first(rhs, semantics)) return hipErrorInvalidValue;
-  auto snap_first = [&]() -> hipError_t {
-    if (!out.first_status || in.num_strings == 0) return hipSuccess;
-    return hipMemcpyAsync(out.first_status, out.status, (size_t)in.num_strings * 4,
-                          hipMemcpyDeviceToDevice, stream);
-  };
   unsigned int* counter = (unsigned int*)scratch(kCounter, kCounterBytes);
   if (!counter) return hipErrorOutOfMemory;
   HIP_TRY(hipMemsetAsync(counter, 0, 64, stream));
   HIP_TRY(hipMemsetAsync(out.cursor, 0, sizeof(unsigned long long), stream));
   if (in.num_strings == 0) return hipSuccess;
   // every string starts as INTERNAL: a string no kernel finished can never read as a result
-  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)out.status, kPathInternal, in.num_strings, stream));
+  // (after launch_pull_part the statuses are the pull tier's)
+  if (!after_pull_)
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)out.status, kPathInternal, in.num_strings, stream));
 
   // Eager semantics on a layered lattice -> eager-layered engine.
   if (semantics == 1) {
@@ -758,8 +786,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     // [6] |list_wa|; [0..2] item counters of tiers A, B, C; [3] |list_ab|; [4] |list_bc|
     if (use_p) {
       EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back_p, back_cap_w, wd};
-      HIP_TRY(launch_eager_pull(rhs, in, n, counter + 14, lp, out, grid_p, stream));
-      HIP_TRY(snap_first());
+      if (!after_pull_) HIP_TRY(launch_eager_pull(rhs, in, n, counter + 14, lp, out, grid_p, stream));
       // test hook: FSTAMD_EAGER_ONLY_FIRST leaves tier P's OVERFLOW / UNSUPPORTED strings
       // as they are, so a test can tell what the tier itself took
       if (std::getenv("FSTAMD_EAGER_ONLY_FIRST")) {
@@ -1086,8 +1113,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
     uint32_t* lp_count = nullptr;
     if (use_lp) {
       if (stats) stats->engine = 7;
-      HIP_TRY(run_lazy_pull(rhs, in, n, out, stream, &lp_list, &lp_count));
-      HIP_TRY(snap_first());
+      HIP_TRY(run_lazy_pull(rhs, in, n, out, stream, &lp_list, &lp_count, !after_pull_));
       if (std::getenv("FSTAMD_LAZY_ONLY_FIRST")) {  // test hook: what the pull took alone
         if (stats) {
           HIP_TRY(hipEventRecord(ev1_, stream));
@@ -1202,7 +1228,7 @@ __global__ void collect_list_kernel(const uint32_t* in_list, const uint32_t* in_
 // clean by every string, so they are initialised only when (re)allocated.
 hipError_t DeviceEngine::run_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                                        const BatchOutDev& out, hipStream_t stream,
-                                       uint32_t** list, uint32_t** count_dev) {
+                                       uint32_t** list, uint32_t** count_dev, bool launch) {
   unsigned int* ctr = (unsigned int*)scratch(kCounter, kCounterBytes);  // [34..35] are ours
   if (!ctr) return hipErrorOutOfMemory;
   // kChaseBatch back slabs per wave, kPullW slots per layer (as tier P)
@@ -1218,13 +1244,35 @@ hipError_t DeviceEngine::run_lazy_pull(const DeviceFst& rhs, const ChainInput& i
   if (!back || !lst) return hipErrorOutOfMemory;
   HIP_TRY(hipMemsetAsync(ctr + 34, 0, 8, stream));
   EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back, back_cap, watchdog_ticks()};
-  HIP_TRY(launch_lazy_pull(rhs, in, n, ctr + 34, lp, out, grid, stream));
+  if (launch) HIP_TRY(launch_lazy_pull(rhs, in, n, ctr + 34, lp, out, grid, stream));
   collect_status_kernel<<<(in.num_strings + 255) / 256, 256, 0, stream>>>(
       out.status, in.num_strings, kPathOverflow, lst, ctr + 35);
   HIP_TRY(hipGetLastError());
   *list = lst;
   *count_dev = ctr + 35;
   return hipSuccess;
+}
+
+hipError_t DeviceEngine::launch_pull_part(const DeviceFst& rhs, const ChainInput& in,
+                                          uint32_t n, int semantics, const BatchOutDev& out,
+                                          hipStream_t stream, unsigned int* item_ctr) {
+  HIP_TRY(hipSetDevice(dev_));
+  if (!pull_first(rhs, semantics)) return hipErrorInvalidValue;
+  if (in.num_strings == 0) return hipSuccess;
+  const bool lazy = semantics != 1;
+  const int per_cu = lazy ? lazy_pull_waves_per_cu(rhs, in.max_len) : pull_waves_per_cu(rhs, in.max_len);
+  const uint32_t back_cap =
+      (uint32_t)std::min<uint64_t>((uint64_t)(in.max_len + 1) * kPullW, 1u << 22);
+  // the back slabs sized for a full grid whatever this part's size, so no later part
+  // reallocates them (a free waits for the device) while an earlier one runs
+  uint32_t full = (uint32_t)std::max<uint64_t>((uint64_t)per_cu * num_cus_, 1);
+  while (full > 1 && (uint64_t)full * kChaseBatch * back_cap * 8 > (24ull << 30)) full /= 2;
+  uint2* back = (uint2*)scratch(lazy ? kLpBack : kPullBack, (size_t)full * kChaseBatch * back_cap * 8);
+  if (!back) return hipErrorOutOfMemory;
+  const uint32_t grid = std::max<uint32_t>(std::min<uint32_t>(full, in.num_strings), 1);
+  EagerLaunch lp{nullptr, nullptr, in.num_strings, nullptr, 0, 0, back, back_cap, watchdog_ticks()};
+  return lazy ? launch_lazy_pull(rhs, in, n, item_ctr, lp, out, grid, stream)
+              : launch_eager_pull(rhs, in, n, item_ctr, lp, out, grid, stream);
 }
 
 hipError_t DeviceEngine::run_lazy_layered(const DeviceFst& rhs, const ChainInput& in,

@@ -323,6 +323,20 @@ class DeviceEngine {
   static bool pull_first(const DeviceFst& rhs, int semantics);
   // kernel_ms of a deferred LaunchStats, once the caller has synchronised the stream
   hipError_t finish_deferred(LaunchStats* stats);
+  // The streamed host batch's parts (c_api.cpp run_streamed): the pull tier alone on `in`
+  // (pull_first must hold), no fills or copies on `stream` (a fill or copy is a blit that
+  // waits for CU slots behind the other engine's persistent kernel) and no host
+  // synchronisation; item_ctr zeroed and statuses filled by the caller.  The later tiers
+  // then run once over the whole batch: run_chain with set_after_pull(true).
+  hipError_t launch_pull_part(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
+                              int semantics, const BatchOutDev& out, hipStream_t stream,
+                              unsigned int* item_ctr);
+  // run_chain after launch_pull_part: the statuses are the pull tier's (no INTERNAL fill,
+  // no pull launch); the later tiers take the strings it handed on.
+  void set_after_pull(bool v) { after_pull_ = v; }
+  // Out of HBM: the workspaces of the device's idle engines (kept per engine between calls)
+  // go back to the device.
+  static void trim_idle(int dev);
   hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
   // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp), on
@@ -361,6 +375,8 @@ class DeviceEngine {
  private:
   explicit DeviceEngine(int dev);
   hipStream_t stream_ = nullptr;   // the engine's own stream (non-blocking)
+  bool after_pull_ = false;        // run_chain: the pull tier already ran (set_after_pull)
+  void free_scratch();             // every workspace back to the device (an idle engine)
   hipEvent_t done_ = nullptr;      // recorded when a lease ends (on the stream it used)
   hipStream_t done_stream_ = nullptr;
   bool done_valid_ = false;
@@ -381,7 +397,7 @@ class DeviceEngine {
   // the strings it hands on (OVERFLOW) are listed in *list, their count at *count_dev.
   hipError_t run_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                            const BatchOutDev& out, hipStream_t stream, uint32_t** list,
-                           uint32_t** count_dev);
+                           uint32_t** count_dev, bool launch = true);
   // composeShortestPath as a dense-indexed exact replay (kernels/lazy_dense.hpp), for rhs
   // with input epsilons; strings it does not take end UNSUPPORTED / OVERFLOW for
   // run_bfs_chain.  *ran = false: it took none (the lattice exceeds its dense index).

@@ -162,6 +162,7 @@ struct EagerLaunch {
 __device__ __forceinline__ void write_status(const BatchOutDev& out, uint32_t si, int32_t st,
                                              uint32_t tuples, uint32_t relax) {
   out.status[si] = st;
+  if (out.first_status) out.first_status[si] = st;  // the streamed batch's parts (pull tiers)
   out.path_len[si] = 0;
   out.path_off[si] = 0;
   out.final_w[si] = w_zero();

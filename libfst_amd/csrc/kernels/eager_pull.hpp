@@ -326,6 +326,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     }
     if (lane < njobs) {
       out.status[jb.si] = kPathOk;
+      if (out.first_status) out.first_status[jb.si] = kPathOk;
       out.path_len[jb.si] = jb.L;
       out.path_off[jb.si] = jb.o;
       out.final_w[jb.si] = jb.fw;  // compose.zig:73: times(One, fw2) == fw2

@@ -77,7 +77,7 @@ def main():
                               "kernel_ms": float(np.median(ks[1:]))}), flush=True)
         os.environ.pop("FSTAMD_STREAM_AB")
     if "--cuts" in sys.argv:  # streamed-batch part cuts (FSTAMD_STREAM_CUTS), timing only
-        for cuts in ("167", "23,163", "125", "200", "167", "100,400"):
+        for cuts in os.environ.get("E2E_CUTS", "167;23,163;125;200;167;100,400").split(";"):
             os.environ["FSTAMD_STREAM_CUTS"] = cuts
             ts = []
             for i in range(6):
