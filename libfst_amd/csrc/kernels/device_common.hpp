@@ -63,11 +63,18 @@ __device__ __forceinline__ unsigned long long reserve_path(const BatchOutDev& ou
 // Streamed host batches (BatchOutDev::host_ol): after a batched chase, the wave copies the
 // finished paths' olabels and weights from their arena slots to the host-mapped result,
 // one string at a time so every store writes whole lines (the chase's own stores are one
-// lane per string, scattered).  The chase's stores are drained and this CU's L1 dropped
-// first (agent acquire: s_waitcnt vmcnt(0) + buffer_inv sc1), so the reads see them.
+// lane per string, scattered).  The chase's stores come from other lanes of this same wave,
+// so a work-group-scope fence orders them before the reads (on gfx950 it emits nothing: a
+// wave's vector memory operations go through one L1 in order).  Round 5 first used an
+// agent-scope acquire here -- s_waitcnt vmcnt(0) + buffer_inv sc1 per chase, a cache
+// invalidate every 16 strings on every wave.
 __device__ __forceinline__ void copy_out_paths(const BatchOutDev& out, uint32_t njobs,
                                                uint64_t my_o, uint32_t my_L, uint32_t lane) {
+#ifdef FSTAMD_COPYOUT_AGENT  // A/B builds: round 5's first fence
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+#endif
   for (uint32_t j = 0; j < njobs; ++j) {  // uniform
     const uint32_t Lj = __builtin_amdgcn_readlane(my_L, j);
     const uint64_t oj = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_o >> 32), j) << 32) |
