@@ -1223,27 +1223,32 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
   for (size_t p = 0; p < parts; ++p)
     if (pr[p].err != FST_OK) return pr[p].err;
+  // statuses, final weights and the pull tier's statuses in one download each
+  auto download = [&](bool with_first) {
+    return num == 0 ||
+           (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost, sA) ==
+                hipSuccess &&
+            hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost, sA) ==
+                hipSuccess &&
+            (!with_first || hipMemcpyAsync(first.data(), d_first.p, num * 4ull,
+                                           hipMemcpyDeviceToHost, sA) == hipSuccess) &&
+            hipStreamSynchronize(sA) == hipSuccess);
+  };
+  if (!download(true)) return FST_OOM;
   // the later tiers, once, over the strings the pull tier handed on (in the device arena,
-  // the same slots)
-  {
+  // the same slots) -- only when it handed some on (the metric: none), then the statuses
+  // and final weights again
+  bool handed = false;
+  for (uint32_t i = 0; i < num && !handed; ++i) handed = first[i] != kPathOk && first[i] != kPathEmpty;
+  if (handed) {
     ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
     BatchOutDev v = o.v;
     v.slots = (const uint64_t*)d_off.p;
     EA->set_after_pull(true);
     const hipError_t e = EA->run_chain(*D, in, n, semantics, v, sA, nullptr);
     EA->set_after_pull(false);
-    if (e != hipSuccess) return FST_OOM;
+    if (e != hipSuccess || !download(false)) return FST_OOM;
   }
-  // statuses, final weights and the pull tier's statuses in one download each
-  if (num && (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost, sA) !=
-                  hipSuccess ||
-              hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost,
-                             sA) != hipSuccess ||
-              hipMemcpyAsync(first.data(), d_first.p, num * 4ull, hipMemcpyDeviceToHost, sA) !=
-                  hipSuccess))
-    return FST_OOM;
-  for (hipStream_t x : {up, sA, sB})
-    if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
   Th.join();
   LaunchStats agg{};  // (the parts overlap on two streams: their wall time, not a sum)
   agg.engine = semantics == 1 ? 0 : 7;
