@@ -83,6 +83,7 @@ struct TinyLds {
   uint32_t ccode[64];
   uint32_t cid[64];
   uint16_t qid[N];             // the frontier (unordered), then the path's ids
+  uint8_t own[256];            // a chunk's lane per key hash (the all-distinct test)
 };
 
 struct TyCand {
@@ -402,7 +403,9 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         }
         // lookup (getOrCreate's get): the slot names an id, the id's key decides
         uint32_t tid = kNoState;
-        uint32_t slot = hmix(x.key) & hmask;
+        const uint32_t h0 = hmix(x.key);
+        uint32_t slot = h0 & hmask;
+        if (act) S.own[h0 & 255u] = (uint8_t)lane;
         if (act) {
           for (uint32_t probe = 0; probe <= hmask; ++probe) {
             const uint32_t v = S.hs[slot];
@@ -421,7 +424,17 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         // order) and the lane that folds the group's relaxations
         unsigned long long gmask = 0;
         uint32_t leader = lane;
-        {
+        // the common case first: every active lane wrote its own entry of the 256-entry
+        // owner table, so no two share a key (two lanes of one key share an entry; keys that
+        // merely collide take the loop below, which is exact in any case)
+#ifdef FSTAMD_TY_NOFAST  // A/B builds: always the loop
+        const bool single = false;
+#else
+        const bool single = !__ballot(act && S.own[h0 & 255u] != lane);
+#endif
+        if (single) {
+          gmask = act ? 1ull << lane : 0ull;
+        } else {
           unsigned long long pend = __ballot(act);
           while (pend) {
             const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
@@ -511,11 +524,13 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
 
         // group by target: the first lane of each group folds its members in lane order
         const double nd = w_times(cur_dist, x.w);
-        S.cnd[lane] = nd;
-        S.col[lane] = x.ol;
-        S.ccode[lane] = x.code;
-        S.carc[lane] = x.arc;
-        wave_fence();
+        if (!single) {  // the groups' members, for their leaders
+          S.cnd[lane] = nd;
+          S.col[lane] = x.ol;
+          S.ccode[lane] = x.code;
+          S.carc[lane] = x.arc;
+          wave_fence();
+        }
         bool push = false, app = false;
         if (gmask) {  // group leader
           const uint32_t t = tid;
@@ -524,7 +539,15 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           uint32_t bol = 0;
           bool bol_known = false;
           bool took = false;
-          unsigned long long m = gmask;
+          if (single) {  // the group is this lane
+            if (tiny_take(rhs, nd, (x.code & kTyConsumed) ? P.label : kEpsilon, x.ol, od, b, pid,
+                          P.label, bol, bol_known)) {
+              od = nd;
+              b = make_uint2(pid | (b.x & kTyKeep) | kTyHasBack | x.code, x.arc);
+              took = true;
+            }
+          }
+          unsigned long long m = single ? 0ull : gmask;
           while (m) {
             const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
             m &= m - 1;
