@@ -74,8 +74,8 @@ struct TinyLds {
   uint4 span[kCache ? N : 1];
   unsigned long long nkey[N];  // (s2 << 32) | (s1 << 2) | filter
   double ndist[N];
-  double cnd[64];              // one chunk's candidates, read by the group leaders
-  double cw[64];
+  double cnd[64];              // one chunk's candidates, read by the group leaders (the
+                               // arc weights on the self-loop path)
   uint2 nback[N];
   uint32_t hs[H];
   uint32_t carc[64];
@@ -485,7 +485,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         const unsigned long long selfm = __ballot(act && tid == pid);
         if (selfm) {
           S.cid[lane] = tid;
-          S.cw[lane] = x.w;
+          S.cnd[lane] = x.w;
           S.col[lane] = x.ol;
           S.ccode[lane] = x.code;
           S.carc[lane] = x.arc;
@@ -494,7 +494,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
           if (lane == 0) {
             for (uint32_t i = 0; i < cnt; ++i) {
               const uint32_t t = S.cid[i];
-              const double nd = w_times(cur_dist, S.cw[i]);
+              const double nd = w_times(cur_dist, S.cnd[i]);
               const double od = S.ndist[t];
               const uint2 b = S.nback[t];
               const uint32_t code = S.ccode[i];
