@@ -25,6 +25,8 @@
 //    are the same bits.  Frontier size <= tuples: no queue overflow.
 //  * one loop groups a chunk's candidates by tuple key: its leaders are the first-touch
 //    owners of new tuples (getOrCreate in lane order) and the folding lanes alike.
+// LDS indices that come from the tables themselves pass FB() (sites 170-181: checked and
+// clamped in DEBUG_BOUNDS builds).
 // Sizes: tier t holds 64 << t tuples at 34 B; 1 (128) = 5.9 KB, 2 (256) = 10.2 KB, 3 (512)
 // = 18.9 KB, 4 (1024) = 36.4 KB.  A string that outgrows its tier ends OVERFLOW and the host reruns
 // it in the next (DeviceEngine::run_chain).
@@ -254,7 +256,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         const uint32_t cc = c0 + lane;
         if (cc < qn) {
           const uint32_t id = S.qid[cc];
-          const double d = S.ndist[id];
+          const double d = S.ndist[FB(id, N, 170)];
           if (bi == kNoState || qless(d, id, bd, bi)) {
             bd = d;
             bi = id;
@@ -270,7 +272,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       const uint32_t wl = (uint32_t)__ffsll((long long)__ballot(c1 && bi == pid)) - 1;
       const uint32_t ppos = __builtin_amdgcn_readlane(bp, wl);
       --qn;
-      if (lane == 0) S.qid[ppos] = S.qid[qn];
+      if (lane == 0) S.qid[FB(ppos, N, 171)] = S.qid[FB(qn, N, 171)];
       wave_fence();
       TY_T(0);
 #ifdef FSTAMD_TINY_PROF
@@ -280,7 +282,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         fail = kPathInternal;
         break;
       }
-      const uint2 pb = S.nback[pid];
+      const uint2 pb = S.nback[FB(pid, N, 172)];
       const double pdist = S.ndist[pid];
       if ((pb.x & kTySettled) || !(pb.x & kTyInQ)) {
         fail = kPathInternal;
@@ -411,7 +413,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
             const uint32_t v = S.hs[slot];
             if ((v >> 16) != gen) break;
             const uint32_t id = v & 0xFFFFu;
-            if (S.nkey[id] == x.key) {
+            if (S.nkey[FB(id, N, 173)] == x.key) {
               tid = id;
               break;
             }
@@ -495,7 +497,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
             for (uint32_t i = 0; i < cnt; ++i) {
               const uint32_t t = S.cid[i];
               const double nd = w_times(cur_dist, S.cnd[i]);
-              const double od = S.ndist[t];
+              const double od = S.ndist[FB(t, N, 174)];
               const uint2 b = S.nback[t];
               const uint32_t code = S.ccode[i];
               uint32_t bol = 0;
@@ -507,7 +509,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
                 S.nback[t] = make_uint2(pid | (b.x & kTyKeep) | (add ? kTyInQ : 0u) | kTyHasBack |
                                             code, S.carc[i]);
                 if (t == pid) cur_dist = nd;
-                if (add) S.qid[qn++] = (uint16_t)t;
+                if (add) S.qid[FB(qn++, N, 175)] = (uint16_t)t;
                 if (!(b.x & kTySettled)) ++pushes;
               }
             }
@@ -534,7 +536,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         bool push = false, app = false;
         if (gmask) {  // group leader
           const uint32_t t = tid;
-          double od = S.ndist[t];
+          double od = S.ndist[FB(t, N, 176)];
           uint2 b = S.nback[t];
           uint32_t bol = 0;
           bool bol_known = false;
@@ -575,7 +577,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
         // the frontier needs nothing: the pop reads dist[id])
         pushes += (uint32_t)__popcll(__ballot(push));
         const unsigned long long am = __ballot(app);
-        if (app) S.qid[qn + (uint32_t)__popcll(am & lanemask_lt())] = (uint16_t)tid;
+        if (app) S.qid[FB(qn + (uint32_t)__popcll(am & lanemask_lt()), N, 177)] = (uint16_t)tid;
         qn += (uint32_t)__popcll(am);
         if constexpr (TinyLds<kTier>::kCache) {
           if (is_new_leader) S.span[tid] = new_span;
@@ -596,7 +598,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       } else {
         uint32_t cur = best_id;
         while (cur != 0) {  // init_id == 0
-          const uint2 b = S.nback[cur];
+          const uint2 b = S.nback[FB(cur, N, 178)];
           if (!(b.x & kTyHasBack)) {
             st = kPathEmpty;
             break;
@@ -605,7 +607,7 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
             st = kPathCycle;
             break;
           }
-          S.qid[P - 1] = (uint16_t)cur;  // the heap is empty: its ids hold the path
+          S.qid[FB(P - 1, N, 179)] = (uint16_t)cur;  // the heap is empty: its ids hold the path
           cur = b.x & kTyPrev;
         }
         if (st == kPathOk) {
@@ -621,11 +623,11 @@ lazy_tiny_kernel(RhsView rhs, ChainInput chain, uint32_t n_best, unsigned int* n
       o = __shfl(o, 0, 64);
       for (uint32_t k = lane; k < P; k += 64) {
         const uint32_t id = S.qid[k];
-        const uint2 b = S.nback[id];
+        const uint2 b = S.nback[FB(id, N, 180)];
         const uint32_t prev = b.x & kTyPrev;
         uint32_t il = kEpsilon, ol = kEpsilon;
         double aw = w_one();
-        if (b.x & kTyConsumed) il = cl.labels[(uint32_t)(S.nkey[prev] & 0xFFFFFFFFull) >> 2];
+        if (b.x & kTyConsumed) il = cl.labels[(uint32_t)(S.nkey[FB(prev, N, 181)] & 0xFFFFFFFFull) >> 2];
         if (b.x & kTyArc) {
           const ArcRec r = rhs.rec[b.y];
           ol = r.olabel;
