@@ -80,8 +80,13 @@ __device__ __forceinline__ void copy_out_paths(const BatchOutDev& out, uint32_t 
     const uint64_t oj = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_o >> 32), j) << 32) |
                         (uint32_t)__builtin_amdgcn_readlane((uint32_t)my_o, j);
     for (uint32_t x = lane; x < Lj; x += 64) {
+#ifdef FSTAMD_COPYOUT_PLAIN  // A/B builds
+      out.host_ol[oj + x] = out.out_ol[oj + x];
+      out.host_w[oj + x] = out.out_w[oj + x];
+#else
       __builtin_nontemporal_store(out.out_ol[oj + x], out.host_ol + oj + x);
       __builtin_nontemporal_store(out.out_w[oj + x], out.host_w + oj + x);
+#endif
     }
   }
 }
