@@ -891,6 +891,8 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   const bool force_rounds = le && std::strcmp(le, "rounds") == 0;
   const bool force_replay = le && std::strcmp(le, "replay") == 0;
   const bool force_dense = le && std::strcmp(le, "dense") == 0;
+  // "lds": the LDS replay first whatever the rhs (tests: rhs without input epsilons)
+  const bool force_lds = le && std::strcmp(le, "lds") == 0;
   // The hashed replay (below) starts small lattices with its tables in LDS, then HBM for
   // what outgrows them; FSTAMD_LAZY_TINY=0 skips that.  (As the engine for config 4's small
   // epsilon lattices it measured level with the dense replay, 15.8 vs 15.0 ms per two-stage
@@ -899,7 +901,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
   const bool tiny_ok = !(lte && std::strcmp(lte, "0") == 0) &&
                        (uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384;
   const bool exact_ok = rhs.nonneg && rhs.finite && !force_replay;
-  const bool use_dense = exact_ok && !force_rounds && (force_dense || rhs.has_eps);
+  const bool use_dense = exact_ok && !force_rounds && (force_dense || force_lds || rhs.has_eps);
   const bool use_rounds = exact_ok && !use_dense;
   if (use_dense) {
     if (stats) {

@@ -19,11 +19,18 @@ from test_gpu_parity import LAZY, check, csr, load_blob, random_rhs
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["rounds", "general", "replay", "replay_hbm", "dense"])
+@pytest.fixture(params=["rounds", "general", "replay", "replay_hbm", "dense", "lds", "lds_chain"])
 def engine(request, monkeypatch):
     monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
     monkeypatch.delenv("FSTAMD_LAZY_LAYERED", raising=False)
     monkeypatch.delenv("FSTAMD_LAZY_TINY", raising=False)
+    if request.param.startswith("lds"):  # the LDS replay (kernels/lazy_tiny.hpp) first
+        monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "lds")
+        if request.param == "lds_chain":  # 128 tuples first, then 256, 512, 1024, HBM;
+            # 4 waves: each takes many strings (tables reused across strings)
+            monkeypatch.setenv("FSTAMD_LAZY_TINY_START", "1")
+            monkeypatch.setenv("FSTAMD_TINY_WAVES", "4")
+        return "dense"
     if request.param == "replay_hbm":  # the hashed replay without its LDS first launch
         monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "replay")
         monkeypatch.setenv("FSTAMD_LAZY_TINY", "0")
