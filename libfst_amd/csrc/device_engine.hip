@@ -613,7 +613,6 @@ hipError_t DeviceEngine::finish_deferred(LaunchStats* stats) {
 }
 
 namespace {
-bool tiny_old();
 template <int T>
 int lazy_tiny_per_cu();
 }  // namespace
@@ -940,7 +939,7 @@ hipError_t DeviceEngine::run_chain(const DeviceFst& rhs, const ChainInput& in, u
       // batches) starts every string there: one wave per string whichever the size, so a
       // long utterance no longer pays a replay at 256 tuples before its rerun at 512 or 1024
       // (36 B per tuple: 1024 tuples are 38 KB, 4 waves per CU)
-      const bool direct = !(ts && *ts) && !tiny_old() &&
+      const bool direct = !(ts && *ts) &&
                           (uint64_t)num <= (uint64_t)num_cus_ * lazy_tiny_per_cu<4>();
       if (direct) {
         HIP_TRY(run_lazy_tiny(rhs, in, n, out, stream, 4, nullptr, num, c + 2, &g));
@@ -1399,22 +1398,12 @@ hipError_t DeviceEngine::launch_lazy_hashed(const DeviceFst& rhs, const ChainInp
 }
 
 namespace {
-// FSTAMD_TINY_OLD=1: the LDS replays of round 5 (lazy_wave_kernel's tiny tiers, 108 B per
-// tuple) instead of lazy_tiny_kernel (36 B), for A/B runs
-bool tiny_old() {
-  static const bool v = [] {
-    const char* e = std::getenv("FSTAMD_TINY_OLD");
-    return e && std::strcmp(e, "1") == 0;
-  }();
-  return v;
-}
 template <int T>
 int lazy_tiny_per_cu() {  // resident LDS-replay waves per CU, asked of the runtime once
   static const int occ = [] {
     int o = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &o, tiny_old() ? (const void*)lazy_wave_kernel<false, T>
-                           : (const void*)lazy_tiny_kernel<T>, 64, 0) != hipSuccess)
+            &o, (const void*)lazy_tiny_kernel<T>, 64, 0) != hipSuccess)
       o = 1;
     return std::max(o, 1);
   }();
@@ -1426,48 +1415,29 @@ hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& i
                                        const BatchOutDev& out, hipStream_t stream, int tier,
                                        const uint32_t* items, uint32_t num_items,
                                        unsigned int* ctr, uint32_t* grid_out) {
+  // (lazy_tiny_kernel sizes its tables from the tier; of LazyWs it reads the watchdog and
+  // the first hash generation)
   LazyWs ws{};
-  ws.hcap = lz_tiny_h(tier);
-  ws.ncap = lz_tiny_n(tier);
-  ws.qcap = lz_tiny_q(tier);
-  ws.gcap = 0;
-  ws.stamp_base = 0;  // stamps from 1 per launch: the LDS table starts zeroed
   // test knobs: FSTAMD_TINY_GEN0 = the hash generation lazy_tiny_kernel starts from (its wrap
   // at 65536 strings per wave, within reach); FSTAMD_TINY_WAVES caps the grid
   const char* eg = std::getenv("FSTAMD_TINY_GEN0");
   const char* ew = std::getenv("FSTAMD_TINY_WAVES");
-  const uint32_t gen0 = eg ? (uint32_t)std::strtoul(eg, nullptr, 10) & 0xFFFFu : 0u;
+  ws.stamp_base = eg ? (uint32_t)std::strtoul(eg, nullptr, 10) & 0xFFFFu : 0u;
   const uint32_t cap_waves = ew ? (uint32_t)std::strtoul(ew, nullptr, 10) : 0u;
-  if (!tiny_old()) ws.stamp_base = gen0;
-  ws.max_pops = ws.qcap + 1;
   ws.wd_ticks = watchdog_ticks();
   const int occ = tier == 1 ? lazy_tiny_per_cu<1>() : tier == 2 ? lazy_tiny_per_cu<2>()
                  : tier == 3 ? lazy_tiny_per_cu<3>() : lazy_tiny_per_cu<4>();
   uint32_t grid =
       (uint32_t)std::min<uint64_t>((uint64_t)num_cus_ * occ, std::max(num_items, 1u));
   if (cap_waves) grid = std::min(grid, cap_waves);
-  GraphInput none{};
-  if (!tiny_old()) {
-    if (tier == 1)
-      lazy_tiny_kernel<1><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
-    else if (tier == 2)
-      lazy_tiny_kernel<2><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
-    else if (tier == 3)
-      lazy_tiny_kernel<3><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
-    else
-      lazy_tiny_kernel<4><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
-  } else if (tier == 1)
-    lazy_wave_kernel<false, 1><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
-                                                         num_items, ws, out);
+  if (tier == 1)
+    lazy_tiny_kernel<1><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
   else if (tier == 2)
-    lazy_wave_kernel<false, 2><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
-                                                         num_items, ws, out);
+    lazy_tiny_kernel<2><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
   else if (tier == 3)
-    lazy_wave_kernel<false, 3><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
-                                                         num_items, ws, out);
+    lazy_tiny_kernel<3><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
   else
-    lazy_wave_kernel<false, 4><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, ctr, items,
-                                                         num_items, ws, out);
+    lazy_tiny_kernel<4><<<grid, 64, 0, stream>>>(rhs.view, in, n, ctr, items, num_items, ws, out);
   HIP_TRY(hipGetLastError());
 #ifdef FSTAMD_TINY_PROF
   {

@@ -405,9 +405,9 @@ class DeviceEngine {
   hipError_t run_lazy_dense(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
                             const BatchOutDev& out, hipStream_t stream, bool* ran,
                             const uint32_t* subset_dev = nullptr, uint32_t subset_n = 0);
-  // composeShortestPath with the wave's tables in LDS (kernels/lazy_wave.hpp, kTiny = tier:
-  // 1 = 128 tuples, 2 = 256) over a device list of strings (nullptr: all); strings whose
-  // lattice outgrows it end OVERFLOW.
+  // composeShortestPath with the wave's tables in LDS (kernels/lazy_tiny.hpp, tier t holds
+  // 64 << t tuples: 1 = 128 ... 4 = 1024) over a device list of strings (nullptr: all);
+  // strings whose lattice outgrows it end OVERFLOW.
   // The band replay (kernels/lazy_band.hpp); *ran = false when the rhs or the batch is not
   // its (arcs going backwards, lengths > 4095); strings it hands on end OVERFLOW.  capped:
   // back pointers only for the first 2 x window states past the start (the early exit's

@@ -298,66 +298,25 @@ struct LazyLds {
 // 18.4 ms per call, 6 and 8 with spills 20.4 ms)
 #define FSTAMD_REPLAY_WAVES 4
 #endif
-// The tiny replay (kTiny): small lattices (config 4's tagger / verbalizer: 43 / 72 tuples
-// per utterance on average) keep the wave's hash, node arrays and heap in LDS instead of
-// HBM slabs, ~15 KB, 10 waves per CU; strings that outgrow it report OVERFLOW and are rerun
-// in HBM.  The host sets ws.{hcap, ncap, qcap, max_pops} to these caps for that launch.
-// Two LDS sizes: kTiny 1 = 128 tuples (~15 KB, 10 waves per CU), 2 = 256 tuples (~29 KB,
-// 5 per CU) for what outgrows the first (a WeText-scale tagger's utterances: ~140 tuples on
-// average, ~300 at most, libfst_amd/wetext_standin.py).
-// Round 5: 3 = 512 tuples (~55 KB, 2 waves per CU) and 4 = 1024 (~110 KB, 1 per CU) for the
-// long utterances of small batches (coalesced single calls), DeviceEngine::run_chain.
+// LDS sizes of the LDS replay (kernels/lazy_tiny.hpp): size t holds 64 << t tuples.
 constexpr uint32_t lz_tiny_n(int t) { return 64u << t; }
-constexpr uint32_t lz_tiny_h(int t) { return 2 * lz_tiny_n(t); }
-constexpr uint32_t lz_tiny_q(int t) { return 3 * lz_tiny_n(t); }
-constexpr uint32_t kLzTinyN = lz_tiny_n(1), kLzTinyH = lz_tiny_h(1), kLzTinyQ = lz_tiny_q(1);
 
-template <bool kGraph, int kTiny = 0>
-__global__ void __launch_bounds__(64, kTiny == 1 ? 3 : kTiny >= 2 ? 1 : FSTAMD_REPLAY_WAVES)
+template <bool kGraph>
+__global__ void __launch_bounds__(64, FSTAMD_REPLAY_WAVES)
 lazy_wave_kernel(RhsView rhs, ChainInput chain, GraphInput graph, uint32_t n_best,
                  unsigned int* next_item, const uint32_t* items, uint32_t num_items, LazyWs ws,
                  BatchOutDev out) {
-  static_assert(!kTiny || !kGraph, "the tiny replay is the chain batch's");
   __shared__ LazyLds S;
   const uint32_t lane = lane_id();
   const size_t w = blockIdx.x;
-  uint4* hslot;
-  unsigned long long* nkey;
-  double* ndist;
-  uint4* nback;
-  double* nbw;
-  double* qd;
-  uint32_t* qid;
-  uint4* tbl = nullptr;
-  if constexpr (kTiny != 0) {
-    constexpr uint32_t TN = lz_tiny_n(kTiny), TH = lz_tiny_h(kTiny), TQ = lz_tiny_q(kTiny);
-    __shared__ uint4 t_hslot[TH];
-    __shared__ unsigned long long t_nkey[TN];
-    __shared__ double t_ndist[TN];
-    __shared__ uint4 t_nback[TN];
-    __shared__ double t_nbw[TN];
-    __shared__ double t_qd[TQ];
-    __shared__ uint32_t t_qid[TQ];
-    hslot = t_hslot;
-    nkey = t_nkey;
-    ndist = t_ndist;
-    nback = t_nback;
-    nbw = t_nbw;
-    qd = t_qd;
-    qid = t_qid;
-    // stamps start at ws.stamp_base + 1 > 0: a zeroed table is empty for every string
-    for (uint32_t i = lane; i < TH; i += 64) t_hslot[i] = make_uint4(0u, 0u, 0u, 0u);
-    wave_fence();
-  } else {
-    hslot = ws.hslot + w * ws.hcap;
-    nkey = ws.nkey + w * ws.ncap;
-    ndist = ws.ndist + w * ws.ncap;
-    nback = ws.nback + w * ws.ncap;
-    nbw = ws.nbw + w * ws.ncap;
-    qd = ws.qd + w * ws.qcap;
-    qid = ws.qid + w * ws.qcap;
-    tbl = ws.gscratch + w * ws.gcap;
-  }
+  uint4* const hslot = ws.hslot + w * ws.hcap;
+  unsigned long long* const nkey = ws.nkey + w * ws.ncap;
+  double* const ndist = ws.ndist + w * ws.ncap;
+  uint4* const nback = ws.nback + w * ws.ncap;
+  double* const nbw = ws.nbw + w * ws.ncap;
+  double* const qd = ws.qd + w * ws.qcap;
+  uint32_t* const qid = ws.qid + w * ws.qcap;
+  uint4* const tbl = ws.gscratch + w * ws.gcap;
   const uint32_t hmask = ws.hcap - 1;
   // per-string watchdog: both are reset when a string starts, so every string gets the
   // full limit however long the launch has been running
