@@ -351,8 +351,9 @@ def cpu_baseline(args, blob_bytes, sem, seconds=None):
 def fractional_ambiguous(T, B, delta=0.5):
     """The metric's ambiguous-chain rhs (bench/optimize-bench.zig:250-277) with every arc
     weight + delta (a WeText-like fractional grammar weight): built through the library's
-    MutableFst API and frozen (fst_freeze).  Distances stop being integers, so the pull
-    tiers take their f64 cells (src/weight.zig:15-37 semantics throughout)."""
+    MutableFst API and frozen (fst_freeze).  Distances stop being integers: a dyadic delta
+    (0.5) keeps the pull tiers' integer records (weights scaled by 2, exact), any other
+    (0.1) takes their f64 cells (src/weight.zig:15-37 semantics throughout)."""
     m = F.MutableFst()
     for _ in range(T + 1):
         m.add_state()
@@ -606,14 +607,16 @@ def main():
                         {"FSTAMD_LP_F64": "1"}),
             "note": "same metric batch and rhs, the pull kernels forced to f64 cells "
                     "(FSTAMD_P_F64 / FSTAMD_LP_F64), device-resident"}
-        fr = fractional_ambiguous(args.transducer_len, args.branches)
-        fr_blob = D.blob_bytes(fr)
-        extra["fractional_weights"] = {
-            "eager": leg(batch, fr, E, local, world, total_per_step, fr_blob),
-            "lazy": leg(batch, fr, Lz, local, world, total_per_step, fr_blob),
-            "rhs": f"ambiguous chain T={args.transducer_len} B={args.branches}, every arc "
-                   "weight + 0.5 (f64 cells), device-resident"}
-        del fr
+        for key, delta, how in (("fractional_weights", 0.5, "dyadic: integer records "
+                                 "scaled by 2"), ("non_dyadic_weights", 0.1, "f64 cells")):
+            fr = fractional_ambiguous(args.transducer_len, args.branches, delta)
+            fr_blob = D.blob_bytes(fr)
+            extra[key] = {
+                "eager": leg(batch, fr, E, local, world, total_per_step, fr_blob),
+                "lazy": leg(batch, fr, Lz, local, world, total_per_step, fr_blob),
+                "rhs": f"ambiguous chain T={args.transducer_len} B={args.branches}, every arc "
+                       f"weight + {delta} ({how}), device-resident"}
+            del fr
     del batch
 
     if rank == 0:

@@ -101,6 +101,10 @@ struct RevView {
   // + rbias8 in the high half, the key bits and weight in the low half), else null
   const uint32_t* rrec4;
   uint32_t rbias8;
+  // 2^-k: the compact records (rrec32 / rrec8 / rrec4) hold every weight times 2^k, the
+  // smallest power of two that makes them all integers (DeviceFst::int_wmax); the kernels
+  // multiply back what they output (exact).  1 for integer weights.
+  double winv;
 };
 constexpr double kRec8WMax = 7.0;
 
@@ -126,7 +130,8 @@ struct DeviceFst {
   // within a same-ilabel run, candidate order = olabel order (relax's (id, il, ol) rule
   // then reduces to (id, candidate))
   bool lazy_pull_ok = false;
-  double int_wmax = -1.0;    // largest arc weight when every one is an integer >= 0, else -1
+  double int_wmax = -1.0;    // largest arc weight times RevView::winv^-1 when every scaled
+                             // weight is an integer >= 0 below 2^24, else -1
   // Routing hints learnt from earlier batches on this rhs: a small-lattice (LDS) tier that
   // handed on nearly every string is skipped next time (config 3's lattices never fit).
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};

@@ -1,6 +1,7 @@
 // eager_pull.hip -- the pull tier's reverse arc mirror (host build + upload) and launches.
 // Kernel and proof: kernels/eager_pull.hpp.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -46,11 +47,26 @@ const void* pull_kernel_for(const RevView& rv) {
 }
 // the 8-B records when the rhs has them (every weight an integer <= kRec8WMax)
 bool use_rec8(const RevView& rv) { return rv.rrec8 && !std::getenv("FSTAMD_NO_REC8"); }
-const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
-  if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64")) return pull_kernel_for<0>(rhs.rev);
-  if (rhs.rev.rrec4 && use_rec8(rhs.rev) && !std::getenv("FSTAMD_NO_REC4"))
-    return pull_kernel_for<3>(rhs.rev);
-  return use_rec8(rhs.rev) ? pull_kernel_for<2>(rhs.rev) : pull_kernel_for<1>(rhs.rev);
+// FSTAMD_ROUTE_LOG: which records the pull kernel reads (0 RevRec / f64 cells, 1 rrec32,
+// 2 rrec8, 3 rrec4) and the weight scale 2^k of the integer records (tests)
+int route_rk(const char* sem, int rk, const RevView& rv, bool log) {
+  if (log && std::getenv("FSTAMD_ROUTE_LOG"))
+    std::fprintf(stderr, "[libfst_amd route] %s pull: records %d, weight scale %g\n", sem, rk,
+                 rk ? 1.0 / rv.winv : 1.0);
+  return rk;
+}
+int pull_rk(const DeviceFst& rhs, uint32_t max_len) {
+  if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64")) return 0;
+  if (rhs.rev.rrec4 && use_rec8(rhs.rev) && !std::getenv("FSTAMD_NO_REC4")) return 3;
+  return use_rec8(rhs.rev) ? 2 : 1;
+}
+const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len, bool log = false) {
+  switch (route_rk("eager", pull_rk(rhs, max_len), rhs.rev, log)) {
+    case 0: return pull_kernel_for<0>(rhs.rev);
+    case 3: return pull_kernel_for<3>(rhs.rev);
+    case 2: return pull_kernel_for<2>(rhs.rev);
+    default: return pull_kernel_for<1>(rhs.rev);
+  }
 }
 // Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 5 with f32 cells (7.4 KB;
 // round 3: 4 at 10.2 KB) when every distance is an integer below 2^24.
@@ -74,9 +90,13 @@ const void* lazy_pull_kernel_for(const RevView& rv) {
     default: return lazy_pull_ptr<8, RK>(dir);
   }
 }
-const void* lazy_pull_kernel_for(const DeviceFst& rhs, uint32_t max_len) {
-  if (!lazy_pull_f32(rhs, max_len)) return lazy_pull_kernel_for<0>(rhs.rev);
-  return use_rec8(rhs.rev) ? lazy_pull_kernel_for<2>(rhs.rev) : lazy_pull_kernel_for<1>(rhs.rev);
+const void* lazy_pull_kernel_for(const DeviceFst& rhs, uint32_t max_len, bool log = false) {
+  const int rk = !lazy_pull_f32(rhs, max_len) ? 0 : use_rec8(rhs.rev) ? 2 : 1;
+  switch (route_rk("lazy", rk, rhs.rev, log)) {
+    case 0: return lazy_pull_kernel_for<0>(rhs.rev);
+    case 2: return lazy_pull_kernel_for<2>(rhs.rev);
+    default: return lazy_pull_kernel_for<1>(rhs.rev);
+  }
 }
 }  // namespace
 
@@ -224,13 +244,26 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     while ((1u << gsearch) < max_groups + 1) ++gsearch;
 
   // integer arc weights in [0, 2^24): the pull tiers may keep their cells' distances in f32
-  // (exact while L * int_wmax < 2^24, pull_f32), reading the f32 copy of the records
-  d->int_wmax = 0.0;
-  for (uint32_t a = 0; a < na && d->int_wmax >= 0.0; ++a) {
-    const double w = pa[a].weight;
-    if (!(w >= 0.0) || w != __builtin_trunc(w) || w >= 16777216.0) d->int_wmax = -1.0;
-    else d->int_wmax = std::max(d->int_wmax, w);
+  // (exact while L * int_wmax < 2^24, pull_f32), reading the f32 copy of the records.
+  // Dyadic weights (0.5, 1.25, ...: integers after a power-of-two scale 2^k, k <= 8) take
+  // the same tiers: f64 sums of such weights are exact (multiples of 2^-k far below 2^53),
+  // so integer sums of the scaled weights order and tie exactly as the reference's f64 sums,
+  // and the kernels multiply by 2^-k (RevView::winv, exact) only what they output.
+  double wscale = 0.0;
+  for (int k = 0; k <= 8 && wscale == 0.0; ++k) {
+    const double sc = (double)(1u << k);
+    bool ok = true;
+    for (uint32_t a = 0; a < na && ok; ++a) {
+      const double w = pa[a].weight * sc;  // (exact: a power of two)
+      ok = w >= 0.0 && w == __builtin_trunc(w) && w < 16777216.0;
+    }
+    if (ok) wscale = sc;
   }
+  d->int_wmax = wscale > 0.0 ? 0.0 : -1.0;
+  for (uint32_t a = 0; a < na && d->int_wmax >= 0.0; ++a)
+    d->int_wmax = std::max(d->int_wmax, pa[a].weight * wscale);
+  if (wscale == 0.0) wscale = 1.0;
+  auto wsc = [wscale](double w) { return (uint32_t)(w * wscale); };  // scaled integer weight
   // direct layout: per state one 4-B row word ilabel | min(nblocks, 255) << 24 (labels
   // below 2^24, else the layout is indirect), and {block 1's record, nblocks} for hub rows
   std::vector<uint32_t> rlab;
@@ -248,7 +281,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   if (d->int_wmax >= 0.0 && d->int_wmax <= kRec8WMax) {
     rrec8.resize(rrec.size());
     for (size_t r = 0; r < rrec.size(); ++r)
-      rrec8[r] = make_uint2(rrec[r].src, rrec[r].y | (uint32_t)rrec[r].weight);
+      rrec8[r] = make_uint2(rrec[r].src, rrec[r].y | wsc(rrec[r].weight));
   }
   // 4-B records for tier P: {8 * (t - source + bias) << 16 | j << 13 | m << 9 | pos << 8 |
   // weight} -- the source as an offset from the target (every arc stays within the rhs's
@@ -280,7 +313,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       for (size_t r = 0; r < rrec.size(); ++r) {
         const uint32_t y = rrec[r].y;
         const uint32_t low = (((y >> 17) & 7u) << 13) | (((y >> 13) & 15u) << 9) |
-                             (((y >> 12) & 1u) << 8) | (uint32_t)rrec[r].weight;
+                             (((y >> 12) & 1u) << 8) | wsc(rrec[r].weight);
         if (rrec[r].src == 0xFFFFFFF8u) {
           rrec4[r] = 0xFFFF0000u;
         } else {
@@ -293,7 +326,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   if (d->int_wmax >= 0.0) {
     rrec32.resize(rrec.size());
     for (size_t r = 0; r < rrec.size(); ++r)  // the weight: an integer below 2^24
-      rrec32[r] = make_uint4(rrec[r].src, rrec[r].y, (uint32_t)rrec[r].weight, rolab[r]);
+      rrec32[r] = make_uint4(rrec[r].src, rrec[r].y, wsc(rrec[r].weight), rolab[r]);
   }
   auto up = [&](int i, const void* src_p, size_t bytes) -> bool {
     if (bytes == 0) bytes = 16;
@@ -318,7 +351,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
                    (const RevRec*)d->rev_bufs[2], (const uint32_t*)d->rev_bufs[3], kp, gsearch,
                    direct ? 1u : 0u, (const uint4*)d->rev_bufs[4], (const uint2*)d->rev_bufs[5],
                    (const uint32_t*)d->rev_bufs[6], (const uint2*)d->rev_bufs[7],
-                   (uint32_t)(nblocks * kp), (const uint32_t*)d->rev_bufs[8], rbias8};
+                   (uint32_t)(nblocks * kp), (const uint32_t*)d->rev_bufs[8], rbias8,
+                   1.0 / wscale};
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;
@@ -341,7 +375,7 @@ hipError_t launch_eager_pull(const DeviceFst& rhs, const ChainInput& in, uint32_
                              const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
   void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
                   (void*)&next_item, (void*)&lp, (void*)&out};
-  return hipLaunchKernel(pull_kernel_for(rhs, in.max_len), dim3(grid), dim3(64), args, 0, stream);
+  return hipLaunchKernel(pull_kernel_for(rhs, in.max_len, true), dim3(grid), dim3(64), args, 0, stream);
 }
 
 bool lazy_pull_f32(const DeviceFst& rhs, uint32_t max_len) {
@@ -362,7 +396,7 @@ hipError_t launch_lazy_pull(const DeviceFst& rhs, const ChainInput& in, uint32_t
                             const BatchOutDev& out, uint32_t grid, hipStream_t stream) {
   void* args[] = {(void*)&rhs.view, (void*)&rhs.rev, (void*)&in, (void*)&n_best,
                   (void*)&next_item, (void*)&lp, (void*)&out};
-  return hipLaunchKernel(lazy_pull_kernel_for(rhs, in.max_len), dim3(grid), dim3(64), args, 0,
+  return hipLaunchKernel(lazy_pull_kernel_for(rhs, in.max_len, true), dim3(grid), dim3(64), args, 0,
                          stream);
 }
 

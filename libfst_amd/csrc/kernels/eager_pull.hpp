@@ -302,18 +302,18 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if constexpr (RK == 3) {
           const uint32_t r = rv.rrec4[b];
           out.out_ol[jb.o + k] = rv.rolab[b];
-          out.out_w[jb.o + k] = (double)(r & 0xFFu);  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)(r & 0xFFu) * rv.winv;  // exact: the f64 weight
           tcur -= (uint32_t)(((int32_t)(r >> 16) - (int32_t)rv.rbias8) >> 3);  // the source
           src8 = tcur << 3;
         } else if constexpr (RK == 2) {
           const uint2 r = rv.rrec8[b];
           out.out_ol[jb.o + k] = rv.rolab[b];
-          out.out_w[jb.o + k] = (double)rec8_weight(r.y);  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)rec8_weight(r.y) * rv.winv;  // exact: the f64 weight
           src8 = r.x;
         } else if constexpr (F32) {
           const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
-          out.out_w[jb.o + k] = (double)r.z;  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)r.z * rv.winv;  // exact: the f64 weight
           src8 = r.x;
         } else {
           const RevRec r = rv.rrec[b];
@@ -585,8 +585,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
             if (!w_is_zero((double)bd[e]) && !w_is_zero(fw2)) {
-              // times(d, times(One, fw2)), in f64 (f32 cells hold d exactly)
-              const unsigned long long kk = okey((double)bd[e] + fw2);
+              // times(d, times(One, fw2)), in f64 (f32 cells hold d exactly, scaled by 2^k)
+              const unsigned long long kk = okey((double)bd[e] * (RK ? rv.winv : 1.0) + fw2);
               const uint32_t pp = (rank << 9) | i;
               if (kk < mykey || (kk == mykey && pp < myp)) {
                 mykey = kk;

@@ -223,12 +223,12 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if constexpr (RK == 2) {
           const uint2 r = rv.rrec8[b];
           out.out_ol[jb.o + k] = rv.rolab[b];
-          out.out_w[jb.o + k] = (double)rec8_weight(r.y);  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)rec8_weight(r.y) * rv.winv;  // exact: the f64 weight
           src8 = r.x;
         } else if constexpr (F32) {
           const uint4 r = rv.rrec32[b];
           out.out_ol[jb.o + k] = r.w;
-          out.out_w[jb.o + k] = (double)r.z;  // exact: the f64 weight
+          out.out_w[jb.o + k] = (double)r.z * rv.winv;  // exact: the f64 weight
           src8 = r.x;
         } else {
           const RevRec r = rv.rrec[b];
@@ -611,7 +611,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 72)];
             if (!w_is_zero(fw2)) {
-              const unsigned long long kk = okey((double)dx + fw2);
+              const unsigned long long kk = okey((double)dx * (RK ? rv.winv : 1.0) + fw2);
               const uint32_t pp = (rank << 9) | i;
               if (kk < mykey || (kk == mykey && pp < myp)) {
                 mykey = kk;

@@ -164,3 +164,96 @@ def test_long_backward_arc_and_the_rec4_bias(sem, back, monkeypatch):
     check(blob, *csr(seqs), sem)
     monkeypatch.setenv("FSTAMD_NO_REC4", "1")
     check(blob, *csr(seqs), sem)
+
+
+def dyadic_rhs(rng, ns, den, nmax, final=None):
+    """banded_int_rhs with every arc weight n / den, n in [0, nmax] (one arc 1 / den, so
+    den is the smallest scale that makes them integers); finals as given, or k / 4."""
+    f = O.Fst()
+    for _ in range(ns):
+        fw = final if final is not None else float(rng.integers(0, 9)) / 4
+        f.add_state(fw if rng.random() < 0.7 else float("inf"))
+    f.start = 0
+    for s in range(ns):
+        for _ in range(3):
+            t = min(ns - 1, s + int(rng.integers(0, 4)))
+            n = nmax if rng.random() < 0.5 else int(rng.integers(0, nmax + 1))
+            f.add_arc(s, int(rng.integers(1, 4)), int(rng.integers(1, 9)), n / den, t)
+    f.add_arc(0, 1, 1, 1.0 / den, 0)
+    return f
+
+
+def routed_records(err, sem):
+    tag = "[libfst_amd route] %s pull: records " % ("eager" if sem == EAGER else "lazy")
+    got = [ln[len(tag):].split(", weight scale ") for ln in err.splitlines() if ln.startswith(tag)]
+    assert got, err
+    return {(int(r), float(s)) for r, s in got}
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+@pytest.mark.parametrize("den,nmax", [(2, 7), (4, 31), (256, 255), (256, 9000)])
+def test_dyadic_weights_take_the_integer_records(sem, den, nmax, monkeypatch, capfd):
+    # weights n / 2^k (grammar costs like 0.5, 1.25): the mirror scales them by 2^k into the
+    # integer records; every f64 sum of them is exact, so integer sums order and tie as the
+    # reference's f64 ones, and the kernels unscale (exactly) only what they output
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    rng = np.random.default_rng(90 + den + nmax)
+    blob = O.freeze(dyadic_rhs(rng, 180, den, nmax))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 50)))] for _ in range(300)]
+    capfd.readouterr()
+    check(blob, *csr(seqs), sem)
+    # the compact records (tier P's 4-B / the 8-B ones) up to 7, the 16-B ones above; the
+    # lazy f32 cells only up to 255 (kLpF32WMax), f64 cells (scale 1) past it
+    # (tier P's 4-B records need the direct layout as well: 3 or 2 for eager)
+    if nmax <= 7:
+        want = {(3, den), (2, den)} if sem == EAGER else {(2, den)}
+    else:
+        want = {(1, den)} if sem == EAGER or nmax <= 255 else {(0, 1.0)}
+    got = routed_records(capfd.readouterr().err, sem)
+    assert len(got) == 1 and got <= want, got
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+@pytest.mark.parametrize("den", [3, 10, 512])
+def test_non_dyadic_weights_take_the_f64_cells(sem, den, monkeypatch, capfd):
+    # 1/3, 0.1 and 2^-9 (past the largest scale, 2^8): no integer records, f64 cells
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    rng = np.random.default_rng(95 + den)
+    blob = O.freeze(dyadic_rhs(rng, 150, den, 7))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 40)))] for _ in range(200)]
+    capfd.readouterr()
+    check(blob, *csr(seqs), sem)
+    assert routed_records(capfd.readouterr().err, sem) == {(0, 1.0)}
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_dyadic_weights_with_non_dyadic_finals(sem, monkeypatch, capfd):
+    # the best final adds a final weight of 0.1 to the unscaled distance in f64, as the
+    # reference does; ties between finals broken by id
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    rng = np.random.default_rng(97)
+    blob = O.freeze(dyadic_rhs(rng, 160, 8, 7, final=0.1))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 45)))] for _ in range(300)]
+    capfd.readouterr()
+    check(blob, *csr(seqs), sem)
+    got = routed_records(capfd.readouterr().err, sem)
+    assert len(got) == 1 and got <= ({(3, 8.0), (2, 8.0)} if sem == EAGER else {(2, 8.0)}), got
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_dyadic_distances_up_to_2p24(sem, monkeypatch, capfd):
+    # scaled distances up to 2^24 - 1 keep the f32 cells; one string more takes f64 cells
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    rng = np.random.default_rng(98)
+    max_len = 63
+    nmax = (1 << 24) // max_len
+    blob = O.freeze(dyadic_rhs(rng, 200, 64, nmax))
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(40, max_len + 1)))]
+            for _ in range(300)]
+    seqs.append([1] * max_len)
+    capfd.readouterr()
+    check(blob, *csr(seqs), sem)
+    rk = {r for r, _ in routed_records(capfd.readouterr().err, sem)}
+    assert rk == ({1} if sem == EAGER else {0})  # lazy f32 cells need weights <= 255
+    check(blob, *csr(seqs + [[1] * (max_len + 1)]), sem)
+    assert routed_records(capfd.readouterr().err, sem) == {(0, 1.0)}
