@@ -35,8 +35,6 @@
 
 extern "C" __device__ double __ockl_wfred_min_f64(double);
 extern "C" __device__ double __ockl_wfred_max_f64(double);
-extern "C" __device__ float __ockl_wfred_min_f32(float);
-extern "C" __device__ float __ockl_wfred_max_f32(float);
 extern "C" __device__ unsigned long long __ockl_wfred_or_u64(unsigned long long);
 
 namespace fstamd {
@@ -53,9 +51,9 @@ constexpr int lp_bins() { return sizeof(DT) == 4 ? 128 : 256; }
 constexpr double kLpF32WMax = 255.0;
 constexpr int kLpChase = 15;  // backtraces batched per wave (<= kChaseBatch: slabs)
 
-// DT: the cells' distance storage.  double in general; float when every distance is an
-// integer below 2^24 (integer arc weights with L * max weight < 2^24, checked on the host:
-// DeviceFst::int_wmax), which is exact and saves 2.5 KB, so 4 waves fit per SIMD.
+// DT: the cells' distance storage.  double in general; uint32_t when every distance is an
+// integer below 2^24 (integer -- or 2^k-scaled dyadic -- arc weights with L * max weight
+// < 2^24, checked on the host: DeviceFst::int_wmax), which is exact and saves 2.5 KB.
 // The current layer's cells (slot W never holds a tuple) in arrays of 8-B entries addressed
 // by one byte offset o = 8 * slot.  Per cell: the distance d (+inf: no tuple), the id-rank
 // word idw = id rank << 20 (kLpAbsent: no tuple), the pop word pw = pop rank << 20 | run
@@ -82,7 +80,9 @@ struct LazyPullCells {  // f64 distances: d, {idw, pw}, tb
     *w = (*w & kLpRunMask) | (q << 20);
   }
 };
-// f32 distances (exact: integers below 2^24): {d, idw} (8 B) and one 4-B pop word
+// integer distances (below 2^24; the F32 kernels, named for round 3's f32 cells -- u32
+// since round 5: the add takes the 8-B record's weight byte as an operand, no conversion;
+// kDistAbsent for no tuple): {d, idw} (8 B) and one 4-B pop word
 // pw = pop rank << 20 | (255 - (d - tb)) << 12 | run, so the merge reads one 8-B word per in-arc
 // (as tier P).  d - tb lies in [0, the largest arc weight]: the first toucher u* pops no
 // later than a tight in-neighbour (d(u*) <= d), and d <= d(u*) + w; the start's tb = -1
@@ -90,11 +90,11 @@ struct LazyPullCells {  // f64 distances: d, {idw, pw}, tb
 // the pop word of an f32 cell: pop rank << 20 | cf << 12 | run, cf = 255 - (d - tb)
 constexpr uint32_t kLpCfShift = 12, kLpCfMask = 0xFFu, kLpCkeyMask = 0xFFFFFu;
 template <int W>
-struct LazyPullCells<W, float> {
-  uint2 a[W + 1];                  // {f32 bits of d, idw}
+struct LazyPullCells<W, uint32_t> {
+  uint2 a[W + 1];                  // {d, idw}
   uint32_t b[W + 1];               // pw
   __device__ __forceinline__ uint2 get_a(uint32_t o) const { return *(const uint2*)((const char*)a + FB(o, 8 * (W + 1), 106)); }
-  __device__ __forceinline__ float get_d(uint32_t o) const { return __uint_as_float(get_a(o).x); }
+  __device__ __forceinline__ uint32_t get_d(uint32_t o) const { return get_a(o).x; }
   __device__ __forceinline__ uint32_t get_idw(uint32_t o) const { return get_a(o).y; }
   __device__ __forceinline__ uint32_t get_pw(uint32_t o) const {
     return *(const uint32_t*)((const char*)b + (FB(o, 8 * (W + 1), 107) >> 1));
@@ -103,19 +103,16 @@ struct LazyPullCells<W, float> {
   __device__ __forceinline__ uint32_t get_delta(uint32_t o) const {
     return kLpCfMask - ((get_pw(o) >> kLpCfShift) & kLpCfMask);
   }
-  __device__ __forceinline__ float get_tb(uint32_t o) const {
-    return get_d(o) - (float)get_delta(o);
-  }
-  // pw carries the run in its low 12 bits; tb enters as d - delta
-  __device__ __forceinline__ void set(uint32_t i, float dd, uint32_t idw, uint32_t pw, float t) {
+  // an empty slot (the cells carry no tb: d - delta)
+  __device__ __forceinline__ void set(uint32_t i, uint32_t dd, uint32_t idw, uint32_t pw, uint32_t) {
     i = FB(i, W + 1, 108);
-    a[i] = make_uint2(__float_as_uint(dd), idw);
-    b[i] = pw < kLpAbsent ? pw | ((kLpCfMask - (uint32_t)(dd - t)) << kLpCfShift) : pw;
+    a[i] = make_uint2(dd, idw);
+    b[i] = pw;
   }
-  // the same with delta already known (pw | delta << 12)
-  __device__ __forceinline__ void set_packed(uint32_t i, float dd, uint32_t idw, uint32_t pwd) {
+  // pw carries the run in its low 12 bits and cf = 255 - (d - tb) above it
+  __device__ __forceinline__ void set_packed(uint32_t i, uint32_t dd, uint32_t idw, uint32_t pwd) {
     i = FB(i, W + 1, 109);
-    a[i] = make_uint2(__float_as_uint(dd), idw);
+    a[i] = make_uint2(dd, idw);
     b[i] = pwd;
   }
   __device__ __forceinline__ void set_pop(uint32_t i, uint32_t q) {
@@ -157,7 +154,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   constexpr bool F32 = RK != 0;
   // DT: the distance type of cells and of the merge's arithmetic (f32: exact for the
   // integer distances below 2^24 the host checked)
-  using DT = typename std::conditional<F32, float, double>::type;
+  using DT = typename std::conditional<F32, uint32_t, double>::type;
   // records: RevRec, or with f32 cells RevView::rrec32 {src, y, f32 weight, olabel} or
   // RevView::rrec8 {src, y | weight}.  The keys carry y: with rrec8 the weight sits in their
   // low 3 bits, so a cell offset taken from a key is masked with 0xFF8
@@ -173,8 +170,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     else return r.src;
   };
   auto r_w = [](const RT& r) -> DT {
-    if constexpr (RK == 2) return (float)rec8_weight(r.y);
-    else if constexpr (F32) return (float)r.z;  // (rrec32 holds the integer weight)
+    if constexpr (RK == 2) return rec8_weight(r.y);
+    else if constexpr (F32) return r.z;  // (rrec32 holds the integer weight)
     else return r.weight;
   };
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
@@ -186,13 +183,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   if (threadIdx.x == 1000) pad_[0] = 0;
 #endif
   const uint32_t lane = threadIdx.x;
-  const DT kInf = (DT)__builtin_huge_val();
-  // min of two distances >= +0 (no NaN: finite weights): on f32, the integer min of the
-  // bit patterns (one v_min_u32, no NaN quieting of the operands)
-  auto lp_dmin = [](DT x, DT y) -> DT {
-    if constexpr (F32) return __uint_as_float(min(__float_as_uint(x), __float_as_uint(y)));
-    else return fmin(x, y);
-  };
+  const DT kInf = dist_inf<DT>();
+  // min of two distances >= +0 (no NaN: finite weights)
+  auto lp_dmin = [](DT x, DT y) -> DT { return dist_min(x, y); };
   uint2* const slabs = lp.back_ws + (size_t)blockIdx.x * kChaseBatch * lp.back_cap;
   uint32_t njobs = 0;
 
@@ -256,7 +249,14 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   const uint32_t num_items = __builtin_amdgcn_readfirstlane(
       lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
-  const bool want_work = out.work != nullptr;
+  // (an SGPR word made opaque at each test: as a bool the compiler kept it as a spilled lane
+  // mask and rebuilt it per row with two readlanes, a select and a compare)
+  const uint32_t want_work_w = __builtin_amdgcn_readfirstlane(out.work != nullptr ? 1u : 0u);
+  auto want_work = [&]() -> bool {
+    uint32_t w = __builtin_amdgcn_readfirstlane(want_work_w);
+    asm volatile("" : "+s"(w));
+    return w != 0u;
+  };
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
@@ -289,7 +289,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll 1
     for (uint32_t i = lane; i < wlast; i += 64) CL.set(i, kInf, kLpAbsent, kLpAbsent, kInf);
     wave_lds_sync();
-    if (lane == 0) CL.set(0, (DT)w_one(), 0u, 0u, (DT)-1.0);
+    if (lane == 0) {
+      if constexpr (F32) CL.set_packed(0, 0u, 0u, (kLpCfMask - 1u) << kLpCfShift);  // d - tb = 1
+      else CL.set(0, (DT)w_one(), 0u, 0u, (DT)-1.0);
+    }
     wave_lds_sync();
     uint32_t tmin = rhs.start, wk = 1, base = 0, n_cur = 1;
     uint32_t cmin = rhs.start, cmax = rhs.start;
@@ -399,12 +402,26 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             b = lp_dmin(b, nd[m]);
           }
         }
-        if (want_work) {  // (one uniform branch per row; an absent source's key >= kLpAbsent)
+        if (want_work()) {  // (one uniform branch per row; an absent source's key >= kLpAbsent)
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(bpk[m] < kLpAbsent));
         }
-        // (tier P's sign-bit back key, on the f32 bit patterns, measured 2 % slower here)
-        uint32_t c = tight_min<KP>(nd, b, bpk);
+        // the back key: tier P's sign-bit form on the integer cells (b - nd has its sign bit
+        // set exactly for the non-tight in-arcs, a real key's bit 31 is clear; round 5: the
+        // u32 cells and this key 46.7 -> 45.3 ms per 1M metric strings, A/B on one box; on
+        // round 4's f32 bit patterns it was 2 % slower than the select tree)
+        uint32_t c;
+#ifndef FSTAMD_LP_TIGHTSEL  // A/B: the select tree (tight_min) on every cell type
+        if constexpr (F32) {
+          c = kEmptyKey;
+#pragma unroll
+          for (int m = 0; m < KP; ++m) c = min(c, bpk[m] | ((b - nd[m]) & 0x80000000u));
+        } else {
+          c = tight_min<KP>(nd, b, bpk);
+        }
+#else
+        c = tight_min<KP>(nd, b, bpk);
+#endif
         uint32_t ra = rec0 + ((c >> 13) & 15u);
         if (hubs) {  // the further blocks: first toucher, distance, back-pointer
           // (block 1's record, loaded here: a branch before the row's record loads would
@@ -430,7 +447,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                 c = p2;
                 ra = rxx + m;
               }
-              if (want_work) relax += (uint32_t)__popcll(__ballot(iw < kLpAbsent));
+              if (want_work()) relax += (uint32_t)__popcll(__ballot(iw < kLpAbsent));
             }
           }
         }
@@ -500,6 +517,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const uint32_t o = bpk[m] & 0xFF8u;
             DT tbm = 0;
             if constexpr (!F32) tbm = CL.get_tb(o);
+            // (short-circuit: two exec-mask branches per in-arc, but the LDS read only for
+            // tight 0-weight in-arcs; the bitwise form that reads every pop word measured
+            // 2 % slower, round 5)
             cert |= nd[m] == b && ((bpk[m] & kRevPos) || certifies(CL.get_pw(o), tbm));
           }
           if (hubs) {  // the further blocks' tight in-arcs
@@ -587,11 +607,13 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         // pop rank: identity until the sort below fills it in
         DT dx;
         if constexpr (F32) {
+          // (branch-free: an absent slot's words are OR-ed with kLpAbsent, which covers
+          // rank << 20; readers of an absent cell's pop word look only at those high bits)
+          const uint32_t gone = pres ? 0u : kLpAbsent;
           dx = pres ? (DT)(bdp[e] & 0xFFFFFFu) : kInf;
-          CL.set_packed(i, dx, pres ? rank << 20 : kLpAbsent,
-                        pres ? (rank << 20) | ((bdp[e] >> 24) << kLpCfShift) |
-                                   (fst[e] & kLpRunMask)
-                             : kLpAbsent);
+          CL.set_packed(i, dx, (rank << 20) | gone,
+                        (rank << 20) | ((bdp[e] >> 24) << kLpCfShift) | (fst[e] & kLpRunMask) |
+                            gone);
         } else {
           dx = bd[e];
           CL.set(i, pres ? bd[e] : kInf, pres ? rank << 20 : kLpAbsent,
@@ -599,7 +621,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         // (f32 cells: the distance's bits, ordered as the non-negative distances are; P4
         // rebuilds the slots from the cells' id-rank words when the layer needs its sort)
-        if (pres && sort) S.ord0[FB(rank, W, 118)] = F32 ? __float_as_uint((float)dx) : i;
+        if (pres && sort) S.ord0[FB(rank, W, 118)] = F32 ? (uint32_t)dx : i;
         const unsigned long long pm = __ballot(pres);
         if (pm) {
           lo_slot = min(lo_slot, (uint32_t)e * 64 + (uint32_t)__builtin_ctzll(pm));
@@ -662,7 +684,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         // keys: integer distances with d - dmin < 2^23 (ik) sort by d - dmin, others by
         // their f64 bit patterns; dmin / dmax over the layer, then key << 9 | slot in ord0
-        DT mn = kInf, mx = -kInf;
+        DT mn = kInf, mx = F32 ? (DT)0 : -kInf;
         bool nonint = false;
         uint32_t cs[EW];
         DT cd[EW];
@@ -675,14 +697,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           if (q < n_next) {
             cs[e] = S.ord0[FB(q, W, 122)];
             cd[e] = CL.get_d(8 * cs[e]);
-            mn = fmin(mn, cd[e]);
-            mx = fmax(mx, cd[e]);
+            mn = dist_min(mn, cd[e]);
+            if constexpr (F32) mx = max(mx, cd[e]);
+            else mx = fmax(mx, cd[e]);
             if (!F32) nonint |= cd[e] != __builtin_trunc(cd[e]);
           }
         }
         if constexpr (F32) {
-          mn = __ockl_wfred_min_f32(mn);
-          mx = __ockl_wfred_max_f32(mx);
+          mn = __ockl_wfred_min_u32(mn);
+          mx = __ockl_wfred_max_u32(mx);
         } else {
           mn = __ockl_wfred_min_f64(mn);
           mx = __ockl_wfred_max_f64(mx);
