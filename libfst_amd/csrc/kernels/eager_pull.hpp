@@ -561,13 +561,16 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       for (int e = 0; e < EW; ++e) {
         if ((uint32_t)e >= rows_w) continue;  // uniform
         const uint32_t i = (uint32_t)e * 64 + lane;
-        const bool pres = (uint32_t)e < rows_n && fst[e] < kPullAbsent;
-        uint32_t rank = 0;
-        if ((uint32_t)e < rows_n) {
-          const uint32_t key = pres ? fst[e] >> kFirstShift : 0u;
-          const uint2 p = reinterpret_cast<const uint2*>(S.pre)[FB(key >> 5, 2 * kWords, 162)];
-          rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
+        if ((uint32_t)e >= rows_n) {  // uniform: a row past the next layer's window, emptied
+          set_cell(i, bd[e], kPullAbsent);
+          continue;
         }
+        // (the row test as its own uniform branch: folded into pres, the compiler kept it
+        // as a lane mask and rebuilt masks from it per row, 2 VALU each)
+        const bool pres = fst[e] < kPullAbsent;
+        const uint32_t key = pres ? fst[e] >> kFirstShift : 0u;
+        const uint2 p = reinterpret_cast<const uint2*>(S.pre)[FB(key >> 5, 2 * kWords, 162)];
+        const uint32_t rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
         // (an absent slot keeps its merged distance, +inf or >= kDistAbsent: no select; the
         // rank word alone marks it absent)
         set_cell(i, bd[e], pres ? rank << kRankShift : kPullAbsent);
