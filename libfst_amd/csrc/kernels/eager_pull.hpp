@@ -341,7 +341,14 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   const uint32_t num_items = __builtin_amdgcn_readfirstlane(
       lp.num_items_dev ? *lp.num_items_dev : lp.num_items);
-  const bool want_work = out.work != nullptr;
+  // (an SGPR word made opaque at each test: as a bool the compiler kept it as a spilled lane
+  // mask, reloaded per row with two readlanes)
+  const uint32_t want_work_w = __builtin_amdgcn_readfirstlane(out.work != nullptr ? 1u : 0u);
+  auto want_work = [&]() -> bool {
+    uint32_t w = __builtin_amdgcn_readfirstlane(want_work_w);
+    asm volatile("" : "+s"(w));
+    return w != 0u;
+  };
 
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) set_cell(i, kInf, kPullAbsent);
@@ -480,7 +487,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll
           for (int m = 0; m < KP; ++m) c = min(c, nd[m] == b ? pk[m] : kEmptyKey);
         }
-        if (want_work) {
+        if (want_work()) {
 #pragma unroll
           for (int m = 0; m < KP; ++m) relax += (uint32_t)__popcll(__ballot(rw[m] < kPullAbsent));
         }
@@ -513,7 +520,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                 c = p2;
                 ra = RK == 3 ? x * KP + m : rx + m;
               }
-              if (want_work) relax += (uint32_t)__popcll(__ballot(w2 < kPullAbsent));
+              if (want_work()) relax += (uint32_t)__popcll(__ballot(w2 < kPullAbsent));
             }
           }
         }
@@ -567,8 +574,11 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         // (the row test as its own uniform branch: folded into pres, the compiler kept it
         // as a lane mask and rebuilt masks from it per row, 2 VALU each)
-        const bool pres = fst[e] < kPullAbsent;
-        const uint32_t key = pres ? fst[e] >> kFirstShift : 0u;
+        uint32_t fe = fst[e];
+        asm volatile("" : "+v"(fe));  // (a fresh compare here: P1's, kept across P2 under
+                                      // another exec mask, was rebuilt with 2 VALU)
+        const bool pres = fe < kPullAbsent;
+        const uint32_t key = pres ? fe >> kFirstShift : 0u;
         const uint2 p = reinterpret_cast<const uint2*>(S.pre)[FB(key >> 5, 2 * kWords, 162)];
         const uint32_t rank = p.x + (uint32_t)__popc(p.y & ((1u << (key & 31u)) - 1u));
         // (an absent slot keeps its merged distance, +inf or >= kDistAbsent: no select; the
