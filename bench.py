@@ -608,7 +608,8 @@ def main():
             "note": "same metric batch and rhs, the pull kernels forced to f64 cells "
                     "(FSTAMD_P_F64 / FSTAMD_LP_F64), device-resident"}
         for key, delta, how in (("fractional_weights", 0.5, "dyadic: integer records "
-                                 "scaled by 2"), ("non_dyadic_weights", 0.1, "f64 cells")):
+                                 "scaled by 2"), ("non_dyadic_weights", 0.1,
+                                 "f64 cells; eager: 4-B records indexing a weight table")):
             fr = fractional_ambiguous(args.transducer_len, args.branches, delta)
             fr_blob = D.blob_bytes(fr)
             extra[key] = {

@@ -103,9 +103,19 @@ struct RevView {
   uint32_t rbias8;
   // 2^-k: the compact records (rrec32 / rrec8 / rrec4) hold every weight times 2^k, the
   // smallest power of two that makes them all integers (DeviceFst::int_wmax); the kernels
-  // multiply back what they output (exact).  1 for integer weights.
+  // multiply back what they output (exact).  1 for integer weights.  (The view's layout
+  // steers tier P's register allocation: one more 8-B field here cost it 3 %, so the weight
+  // table below has no pointer of its own.)
   double winv;
+  // (weights no such scale makes integers, DeviceFst::widx: rrec4's low byte indexes a
+  // table of the rhs's distinct arc weights stored after the records, rv_weight_table)
 };
+constexpr uint32_t kPullWt = 64;  // (a power of two: the kernels mask the index)
+// the weight table of an rhs with DeviceFst::widx: kPullWt doubles right after the
+// rrec4 records (their count rounded up to 8-B alignment)
+__host__ __device__ inline const double* rv_weight_table(const RevView& rv) {
+  return reinterpret_cast<const double*>(rv.rrec4 + ((rv.nrec + 1u) & ~1u));
+}
 constexpr double kRec8WMax = 7.0;
 
 struct DeviceFst {
@@ -132,6 +142,7 @@ struct DeviceFst {
   bool lazy_pull_ok = false;
   double int_wmax = -1.0;    // largest arc weight times RevView::winv^-1 when every scaled
                              // weight is an integer >= 0 below 2^24, else -1
+  bool widx = false;         // rrec4 holds weight-table indices (RK 4; rv_weight_table)
   // Routing hints learnt from earlier batches on this rhs: a small-lattice (LDS) tier that
   // handed on nearly every string is skipped next time (config 3's lattices never fit).
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};

@@ -1,9 +1,11 @@
 // eager_pull.hip -- the pull tier's reverse arc mirror (host build + upload) and launches.
 // Kernel and proof: kernels/eager_pull.hpp.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "device_engine.hpp"
@@ -38,7 +40,8 @@ const void* pull_kernel_ptr(bool direct) {
 template <int RK>
 const void* pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
-  constexpr int wv = RK >= 2 ? FSTAMD_PULL_WAVES_R8 : RK ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
+  constexpr int wv = RK == 4 ? FSTAMD_PULL_WAVES_SMALL  // (f64 cells)
+                   : RK >= 2 ? FSTAMD_PULL_WAVES_R8 : RK ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
   switch (rv.kp) {
     case 4: return pull_kernel_ptr<4, wv, RK>(dir);
     case 5: return pull_kernel_ptr<5, wv, RK>(dir);
@@ -48,21 +51,24 @@ const void* pull_kernel_for(const RevView& rv) {
 // the 8-B records when the rhs has them (every weight an integer <= kRec8WMax)
 bool use_rec8(const RevView& rv) { return rv.rrec8 && !std::getenv("FSTAMD_NO_REC8"); }
 // FSTAMD_ROUTE_LOG: which records the pull kernel reads (0 RevRec / f64 cells, 1 rrec32,
-// 2 rrec8, 3 rrec4) and the weight scale 2^k of the integer records (tests)
+// 2 rrec8, 3 rrec4, 4 rrec4 with weight indices and f64 cells) and the weight scale 2^k of
+// the integer records (tests)
 int route_rk(const char* sem, int rk, const RevView& rv, bool log) {
   if (log && std::getenv("FSTAMD_ROUTE_LOG"))
     std::fprintf(stderr, "[libfst_amd route] %s pull: records %d, weight scale %g\n", sem, rk,
-                 rk ? 1.0 / rv.winv : 1.0);
+                 rk && rk != 4 ? 1.0 / rv.winv : 1.0);
   return rk;
 }
 int pull_rk(const DeviceFst& rhs, uint32_t max_len) {
-  if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64")) return 0;
+  if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64"))  // f64 cells
+    return rhs.rev.rrec4 && rhs.widx && !std::getenv("FSTAMD_NO_REC4") ? 4 : 0;
   if (rhs.rev.rrec4 && use_rec8(rhs.rev) && !std::getenv("FSTAMD_NO_REC4")) return 3;
   return use_rec8(rhs.rev) ? 2 : 1;
 }
 const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len, bool log = false) {
   switch (route_rk("eager", pull_rk(rhs, max_len), rhs.rev, log)) {
     case 0: return pull_kernel_for<0>(rhs.rev);
+    case 4: return pull_kernel_for<4>(rhs.rev);
     case 3: return pull_kernel_for<3>(rhs.rev);
     case 2: return pull_kernel_for<2>(rhs.rev);
     default: return pull_kernel_for<1>(rhs.rev);
@@ -107,6 +113,7 @@ void free_reverse_mirror(DeviceFst* d) {
   }
   d->rev = RevView{};
   d->pull_ok = false;
+  d->widx = false;
 }
 
 bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
@@ -286,10 +293,41 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   // 4-B records for tier P: {8 * (t - source + bias) << 16 | j << 13 | m << 9 | pos << 8 |
   // weight} -- the source as an offset from the target (every arc stays within the rhs's
   // jump range), the key bits in the low half.  Padding: 0xFFFF0000 (an offset past every
-  // window).  Only with the 8-B records' weights (integers <= 7) and offsets below 2^13.
+  // window).  Only with the 8-B records' weights (integers <= 7) or the weight table's
+  // indices (< kPullWt), and offsets below 2^13.
+  // Weights that are not dyadic (0.1, ln 3): with at most kPullWt distinct values the 4-B
+  // records hold the value's index in a table instead (RK 4: tier P with f64 cells adds
+  // the table's f64 value, the very value the reference adds; FSTAMD_NO_WIDX: off)
+  std::vector<double> wtab;
+  std::unordered_map<uint64_t, uint32_t> widx_of;
+  if (d->int_wmax < 0.0 && !std::getenv("FSTAMD_NO_WIDX")) {
+    bool ok = true;
+    for (uint32_t a = 0; a < na && ok; ++a) {
+      const double w = pa[a].weight;
+      uint64_t bits;
+      std::memcpy(&bits, &w, 8);
+      if (widx_of.count(bits)) continue;
+      if (!(w >= 0.0) || !std::isfinite(w) || wtab.size() == kPullWt) ok = false;
+      else {
+        widx_of.emplace(bits, (uint32_t)wtab.size());
+        wtab.push_back(w);
+      }
+    }
+    if (!ok) {
+      wtab.clear();
+      widx_of.clear();
+    }
+  }
+  const bool widx = !wtab.empty();
+  auto low_weight = [&](double w) -> uint32_t {  // the 4-B record's low byte
+    if (!widx) return wsc(w);
+    uint64_t bits;
+    std::memcpy(&bits, &w, 8);
+    return widx_of.at(bits);
+  };
   std::vector<uint32_t> rrec4;
   uint32_t rbias8 = 0;
-  if (!rrec8.empty()) {
+  if (!rrec8.empty() || widx) {
     int64_t dlo = 0, dhi = 0;
     for (size_t r = 0; r < rrec.size(); ++r) {
       if (rrec[r].src == 0xFFFFFFF8u) continue;
@@ -312,11 +350,11 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       rrec4.resize(rrec.size());
       for (size_t r = 0; r < rrec.size(); ++r) {
         const uint32_t y = rrec[r].y;
-        const uint32_t low = (((y >> 17) & 7u) << 13) | (((y >> 13) & 15u) << 9) |
-                             (((y >> 12) & 1u) << 8) | wsc(rrec[r].weight);
         if (rrec[r].src == 0xFFFFFFF8u) {
           rrec4[r] = 0xFFFF0000u;
         } else {
+          const uint32_t low = (((y >> 17) & 7u) << 13) | (((y >> 13) & 15u) << 9) |
+                               (((y >> 12) & 1u) << 8) | low_weight(rrec[r].weight);
           const int64_t dl = (int64_t)rtgt[r] - (int64_t)(rrec[r].src >> 3);
           rrec4[r] = ((uint32_t)((dl - dlo) * 8) << 16) | low;
         }
@@ -328,6 +366,15 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     for (size_t r = 0; r < rrec.size(); ++r)  // the weight: an integer below 2^24
       rrec32[r] = make_uint4(rrec[r].src, rrec[r].y, wsc(rrec[r].weight), rolab[r]);
   }
+  if (rrec4.empty()) wtab.clear();  // (the table serves the 4-B records only)
+  if (!wtab.empty()) {  // appended to the records (rv_weight_table)
+    wtab.resize(kPullWt, 0.0);
+    rrec4.resize((rrec4.size() + 1) & ~(size_t)1, 0xFFFF0000u);
+    const size_t at = rrec4.size();
+    rrec4.resize(at + 2 * kPullWt);
+    std::memcpy(rrec4.data() + at, wtab.data(), kPullWt * sizeof(double));
+  }
+  d->widx = !wtab.empty();
   auto up = [&](int i, const void* src_p, size_t bytes) -> bool {
     if (bytes == 0) bytes = 16;
     if (hipMalloc(&d->rev_bufs[i], bytes) != hipSuccess) return false;

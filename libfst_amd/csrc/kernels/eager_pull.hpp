@@ -85,6 +85,7 @@ struct PullLds {
   unsigned long long best;
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
+  double wt[kPullWt];              // RK 4: the rhs's distinct arc weights (rv_weight_table)
 };
 // integer cells (every distance an integer below 2^24; round 3 kept them as f32, round 4 as
 // u32, whose add takes the 8-B record's weight byte as an SDWA operand): one 8-B cell
@@ -139,6 +140,21 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec
   // times(d, times(One, w)) for w >= +0 (compose.zig:104, shortest-path.zig:72); +inf
   // stays +inf
   nd = d + r.weight;
+}
+// The same on tier P's 4-B records whose low byte indexes the rhs's table of distinct
+// weights (RK 4: weights that no power-of-two scale makes integers; the cells stay f64):
+// the source's offset as in the integer RK 3 below, the weight read from the LDS table --
+// the same f64 value the reference adds
+template <int W>
+__device__ __forceinline__ void pull_candidate(const PullLds<W, false>& S, const uint32_t& r,
+                                               uint32_t base8, uint32_t& pk, double& nd,
+                                               uint32_t& rank_word) {
+  const uint32_t off = min(base8 - (r >> 16), 8u * W);
+  const double d = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(S.d) + FB(off, 8 * (W + 1), 150));
+  const uint32_t rw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S.rk) + FB(off, 8 * (W + 1), 151));
+  pk = rw | (r & 0xFFFFu);
+  rank_word = rw;
+  nd = d + S.wt[FB(r & (kPullWt - 1u), kPullWt, 149)];
 }
 // The same on integer cells and the integer record copy {src, y, weight, olabel}: the
 // distances are integers below 2^24, so the u32 sum, min and compare equal the f64 ones.
@@ -231,15 +247,16 @@ __global__ void __launch_bounds__(64, WAVES_PER_EU)
 eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                   unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
-  constexpr bool F32 = RK != 0;
+  constexpr bool F32 = RK != 0 && RK != 4;
+  constexpr bool REC4 = RK == 3 || RK == 4;  // tier P's 4-B records (RK 4: f64 cells)
   using DT = typename std::conditional<F32, uint32_t, double>::type;  // (F32: integer cells)
   using RT = typename std::conditional<
-      RK == 3, uint32_t,
+      REC4, uint32_t,
       typename std::conditional<RK == 2, uint2,
                                 typename std::conditional<F32, uint4, RevRec>::type>::type>::type;
   // key layout: rank word rank << 20 over y = j << 17 | m << 13 (RK 3: rank << 16 over
   // j << 13 | m << 9): the first key (rank << 3 | j) and m sit at these shifts
-  constexpr uint32_t kRankShift = RK == 3 ? 16 : 20;
+  constexpr uint32_t kRankShift = REC4 ? 16 : 20;
   constexpr uint32_t kFirstShift = kRankShift - 3;
   constexpr uint32_t kMShift = kFirstShift - 4;
   constexpr int kWords = PullLds<W, F32>::kWords;
@@ -258,7 +275,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
     }
   };
   auto rec = [&](uint32_t r) -> RT {
-    if constexpr (RK == 3) return rv.rrec4[r];
+    if constexpr (REC4) return rv.rrec4[r];
     else if constexpr (RK == 2) return rv.rrec8[r];
     else if constexpr (F32) return rv.rrec32[r];
     else return rv.rrec[r];
@@ -288,7 +305,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
         uint32_t b;
-        if constexpr (RK == 3) {  // the byte x * KP + m of the tuple at slab position id,
+        if constexpr (REC4) {  // the byte x * KP + m of the tuple at slab position id,
                                   // whose state is tcur: block 0 at tcur * KP, blocks 1.. at
                                   // rxrec[tcur].x (eager_pull.hip)
           const uint32_t v = reinterpret_cast<const uint8_t*>(sl)[FB(id, lp.back_cap, 60)];
@@ -299,10 +316,13 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         const uint2 h = hdr[k];
         if (!out.host_ol) out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
-        if constexpr (RK == 3) {
+        if constexpr (REC4) {
           const uint32_t r = rv.rrec4[b];
           out.out_ol[jb.o + k] = rv.rolab[b];
-          out.out_w[jb.o + k] = (double)(r & 0xFFu) * rv.winv;  // exact: the f64 weight
+          if constexpr (RK == 4)
+            out.out_w[jb.o + k] = rv_weight_table(rv)[r & (kPullWt - 1u)];  // the f64 weight
+          else
+            out.out_w[jb.o + k] = (double)(r & 0xFFu) * rv.winv;  // exact: the f64 weight
           tcur -= (uint32_t)(((int32_t)(r >> 16) - (int32_t)rv.rbias8) >> 3);  // the source
           src8 = tcur << 3;
         } else if constexpr (RK == 2) {
@@ -353,6 +373,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) set_cell(i, kInf, kPullAbsent);
   if (lane < (uint32_t)kWords) S.bits[FB(lane, kWords, 157)] = 0;
+  if constexpr (RK == 4) S.wt[lane & (kPullWt - 1u)] = rv_weight_table(rv)[lane & (kPullWt - 1u)];
   wave_lds_sync();
   uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
 
@@ -449,12 +470,12 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         }
         // RK 3: the records hold the source relative to the target, so the lane's base is
         // 8 * (t - window origin) + rbias8 (the 2^31 shift of a miss applies the same)
-        if constexpr (RK == 3) tmin8 = (t << 3) - (tmin << 3) + rv.rbias8 + (tmin8 - (tmin << 3));
+        if constexpr (REC4) tmin8 = (t << 3) - (tmin << 3) + rv.rbias8 + (tmin8 - (tmin << 3));
         RT rr[KP];
         // one base address, the records at immediate offsets
         const RT* R;
         // (RK 2, 3: the byte offset in 32 bits -- fewer than 2^28 records, eager_pull.hip)
-        if constexpr (RK == 3) R = at_byte(rv.rrec4, rec0 * 4u);
+        if constexpr (REC4) R = at_byte(rv.rrec4, rec0 * 4u);
         else if constexpr (RK == 2) R = at_byte(rv.rrec8, rec0 * 8u);
         else if constexpr (F32) R = rv.rrec32 + rec0;
         else R = rv.rrec + rec0;
@@ -494,7 +515,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         // the back record: RK 3 (direct layout) keeps one byte, the in-arc's position
         // x * KP + m in its target's group (block x, slot m; the chase re-derives the record
         // from the target state); the other kinds the record index itself
-        uint32_t ra = (RK == 3 ? 0u : rec0) + ((c >> kMShift) & 15u);
+        uint32_t ra = (REC4 ? 0u : rec0) + ((c >> kMShift) & 15u);
         // groups of more than KP in-arcs: the further blocks, rare (a hub state)
         if (__ballot(nb > 1)) {
           if constexpr (DIRECT) {  // block 1's record; the true count past 255 blocks
@@ -518,7 +539,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
                 c = p2;
-                ra = RK == 3 ? x * KP + m : rx + m;
+                ra = REC4 ? x * KP + m : rx + m;
               }
               if (want_work()) relax += (uint32_t)__popcll(__ballot(w2 < kPullAbsent));
             }
@@ -590,7 +611,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          if constexpr (RK == 3)
+          if constexpr (REC4)
             reinterpret_cast<uint8_t*>(back)[FB(nbase + i, lp.back_cap, 61)] = (uint8_t)bra[e];
           else
             *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 61) * 4u)) = bra[e];
@@ -599,7 +620,7 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 62)];
             if (!w_is_zero((double)bd[e]) && !w_is_zero(fw2)) {
               // times(d, times(One, fw2)), in f64 (f32 cells hold d exactly, scaled by 2^k)
-              const unsigned long long kk = okey((double)bd[e] * (RK ? rv.winv : 1.0) + fw2);
+              const unsigned long long kk = okey((double)bd[e] * (F32 ? rv.winv : 1.0) + fw2);
               const uint32_t pp = (rank << 9) | i;
               if (kk < mykey || (kk == mykey && pp < myp)) {
                 mykey = kk;

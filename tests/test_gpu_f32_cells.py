@@ -223,7 +223,54 @@ def test_non_dyadic_weights_take_the_f64_cells(sem, den, monkeypatch, capfd):
     seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 40)))] for _ in range(200)]
     capfd.readouterr()
     check(blob, *csr(seqs), sem)
-    assert routed_records(capfd.readouterr().err, sem) == {(0, 1.0)}
+    # eager: tier P's 4-B records with indices into the table of distinct weights (RK 4,
+    # f64 cells) when the rhs has the direct layout, else the f64 records
+    got = routed_records(capfd.readouterr().err, sem)
+    assert got <= ({(4, 1.0), (0, 1.0)} if sem == EAGER else {(0, 1.0)}) and len(got) == 1, got
+
+
+def metric_like_rhs(T, B, delta):
+    """bench.fractional_ambiguous at a small T: the metric's chain, every weight + delta"""
+    f = O.Fst()
+    for _ in range(T + 1):
+        f.add_state(0.0)
+    f.start = 0
+    for i in range(T + 1):
+        f.add_arc(i, 1, 1, 0.0 + delta, i)
+        for b in range(max(1, min(B, 4))):
+            f.add_arc(i, 1, ((i + b) % 255) + 1, float(b) + delta, min(i + b + 1, T))
+    return f
+
+
+@pytest.mark.parametrize("delta", [0.1, 1.0 / 3.0])
+def test_weight_table_records_on_the_metric_shape(delta, monkeypatch, capfd):
+    # non-dyadic weights on the metric's chain: tier P reads 4-B records whose low byte
+    # indexes the weight table (RK 4), f64 cells; bit-exact with the oracle, and with the
+    # f64 records (FSTAMD_NO_REC4) -- ties on purpose (every string is 1^L)
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    blob = O.freeze(metric_like_rhs(512, 12, delta))
+    rng = np.random.default_rng(99)
+    seqs = [[1] * int(L) for L in rng.integers(0, 65, 400)] + [[1] * 64] * 8
+    capfd.readouterr()
+    check(blob, *csr(seqs), EAGER)
+    assert routed_records(capfd.readouterr().err, EAGER) == {(4, 1.0)}
+    monkeypatch.setenv("FSTAMD_NO_REC4", "1")
+    check(blob, *csr(seqs), EAGER)
+    assert routed_records(capfd.readouterr().err, EAGER) == {(0, 1.0)}
+
+
+def test_more_distinct_weights_than_the_table_holds(monkeypatch, capfd):
+    # 65 distinct non-dyadic weights: one more than the table holds, so the f64 records
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    f = metric_like_rhs(512, 12, 0.1)
+    for i in range(65):
+        f.add_arc(i, 2, 1, 0.1 + i / 7.0, i + 1)
+    blob = O.freeze(f)
+    rng = np.random.default_rng(100)
+    seqs = [[int(x) for x in rng.choice([1, 1, 1, 2], int(L))] for L in rng.integers(0, 65, 300)]
+    capfd.readouterr()
+    check(blob, *csr(seqs), EAGER)
+    assert routed_records(capfd.readouterr().err, EAGER) == {(0, 1.0)}
 
 
 @pytest.mark.parametrize("sem", [EAGER, LAZY])
