@@ -10,8 +10,10 @@ N GPUs: one process per GPU (torchrun); the frozen rhs blob is built on rank 0 a
 broadcast once over xGMI with RCCL (torch.distributed "nccl"), then adopted by every
 rank (fst_device_adopt_blob).  No per-step collectives: each rank runs its own shard;
 timing is barrier + synchronize on both sides, max over ranks.  The metric's form is
-"batch=1M, 1/2/4/8 GPU": by default the 1M strings of a step are split over the ranks
-(--scaling strong, --global-batch); --scaling weak gives every rank --batch strings.
+"batch=1M, 1/2/4/8 GPU".  By default (--scaling weak) every rank gets --batch strings
+(1M) per step, so an N-GPU step processes N x 1M strings and `value` is their sum over the
+max-over-ranks time; --scaling strong splits --global-batch strings (1M) of a step over
+the ranks instead.
 """
 import argparse
 import ctypes as C
@@ -591,7 +593,7 @@ def main():
             lplen = lb.plen.cpu().numpy().astype(np.int64)
             extra["lazy"]["roofline"] = roofline_block(
                 args, F.FST_SEM_LAZY, float(np.mean(lk)), b_alg_bytes(lwork, lengths, lplen),
-                lwork, lengths, lplen, None, None)
+                lwork, lengths, lplen, *measured_traffic(args, F.FST_SEM_LAZY))
         del lb
         if rank == 0 and not args.no_cpu and world == 1:  # the CPU port beside it (~3 s)
             extra["lazy"]["cpu_baseline"] = cpu_baseline(args, blob_check, 0, seconds=3.0)

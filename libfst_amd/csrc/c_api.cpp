@@ -149,6 +149,14 @@ int current_device() {
   return dev;
 }
 
+// Tests only: FSTAMD_FAULT_INJECT=<site> makes the named error branch fire after its work
+// is in flight on the GPU (tests/test_gpu_error_paths.py: the buffers a failing call hands
+// back to the pools must not still be in use by its copies or kernels).
+bool fault_inject(const char* site) {
+  const char* e = std::getenv("FSTAMD_FAULT_INJECT");
+  return e && std::strcmp(e, site) == 0;
+}
+
 bool gpu_available() {
   static int ok = -1;
   static std::mutex mu;
@@ -189,18 +197,27 @@ BufPool& buf_pool() {
 // thread's current device is restored.
 void pool_release(int dev) {
   BufPool& P = buf_pool();
-  std::lock_guard<std::mutex> g(P.mu);
+  // the blocks leave the pool under the lock; hipFree (it synchronises the device) runs
+  // after it, so other threads' DevBuf allocations never wait for a running kernel here
+  std::vector<std::pair<int, void*>> drop;
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    for (auto it = P.free.begin(); it != P.free.end();) {
+      if (dev >= 0 && it->first.first != dev) {
+        ++it;
+        continue;
+      }
+      drop.emplace_back(it->first.first, it->second);
+      P.held -= it->first.second;
+      it = P.free.erase(it);
+    }
+  }
+  if (drop.empty()) return;
   int cur = 0;
   const bool have_cur = hipGetDevice(&cur) == hipSuccess;
-  for (auto it = P.free.begin(); it != P.free.end();) {
-    if (dev >= 0 && it->first.first != dev) {
-      ++it;
-      continue;
-    }
-    (void)hipSetDevice(it->first.first);
-    (void)hipFree(it->second);
-    P.held -= it->first.second;
-    it = P.free.erase(it);
+  for (auto& [d, p] : drop) {
+    (void)hipSetDevice(d);
+    (void)hipFree(p);
   }
   if (have_cur) (void)hipSetDevice(cur);
 }
@@ -647,6 +664,16 @@ int run_small_batch(DeviceEngine::Lease& E, DeviceFst& D, const uint32_t* labels
   DevBuf blk(end);
   PinnedVec<uint8_t> hin(in_bytes), hout(end - o_st);
   if (!blk.p) return FST_OOM;
+  // every return before the final synchronisation drains the stream first: `blk`, `hin`
+  // and `hout` go back to their pools on return, and an upload, a kernel (run_chain can
+  // fail after launching some) or the download may still be using them
+  struct Drain {
+    hipStream_t s;
+    bool done = false;
+    ~Drain() {
+      if (!done) (void)hipStreamSynchronize(s);
+    }
+  } drain{stream};
   uint64_t* ho = (uint64_t*)(hin.data() + o_off);
   for (uint32_t i = 0; i <= num; ++i) ho[i] = offsets[i] - offsets[0];
   if (total) std::memcpy(hin.data() + o_lab, labels + offsets[0], total * 4);
@@ -660,11 +687,14 @@ int run_small_batch(DeviceEngine::Lease& E, DeviceFst& D, const uint32_t* labels
   if (t_prof) t_prof->lap(0);
   LaunchStats st;
   st.defer = true;  // (kernel time read after the download's synchronisation)
-  if (E->run_chain(D, in, n, semantics, v, stream, &st) != hipSuccess ||
+  const bool launched = E->run_chain(D, in, n, semantics, v, stream, &st) == hipSuccess &&
+                        !fault_inject("small_after_launch");
+  if (!launched ||
       hipMemcpyAsync(hout.data(), p + o_st, end - o_st, hipMemcpyDeviceToHost, stream) !=
           hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return FST_OOM;
+  drain.done = true;
   (void)E->finish_deferred(&st);
   t_last_stats = st;
   if (t_prof) {
@@ -1018,27 +1048,89 @@ struct StreamKit {  // per calling thread and device: the upload stream and its 
     }
     return true;
   }
-  // (never destroyed: thread exit may come after the runtime's teardown)
 };
 
-int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* offsets,
-                 uint32_t num, uint32_t n, int semantics, FstBatchResult* out) {
-  if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
-  DeviceFst* D = b.device(dev);
-  if (!D) return FST_OOM;
-  if (D->has_eps || !DeviceEngine::pull_first(*D, semantics)) return kStreamNotApplicable;
-  thread_local std::map<int, StreamKit> kits;
-  StreamKit& K = kits[dev];
-  if (!K.init(dev)) return kStreamNotApplicable;
-  const hipStream_t up = K.up;
-  const uint64_t base0 = offsets[0], total = offsets[num] - base0;
-  if (!alloc_result(out, num, total)) return FST_OOM;
-  if (!pin_is_pinned(out->ilabels) || !pin_is_pinned(out->olabels) ||
-      !pin_is_pinned(out->weights) || !pin_is_pinned(out->path_offsets)) {
-    fst_batch_result_free(out);
-    return kStreamNotApplicable;
+// StreamKits are leased per call from a process-wide pool per device (a kit per calling
+// thread leaked a stream and its events for every thread that ever entered the batch
+// API): the pool holds at most as many kits as calls ever ran at once on the device.
+// (Never destroyed: the process may exit after the runtime's teardown.)
+class KitLease {
+ public:
+  explicit KitLease(int dev) : dev_(dev) {
+    Pool& P = pool();
+    {
+      std::lock_guard<std::mutex> g(P.mu);
+      auto& v = P.free[dev];
+      if (!v.empty()) {
+        k_ = v.back();
+        v.pop_back();
+      }
+    }
+    if (!k_) k_ = new StreamKit;
+    if (!k_->init(dev)) {
+      give_back();
+      k_ = nullptr;
+    }
   }
-  const uint32_t* src = labels ? labels + base0 : nullptr;
+  ~KitLease() { give_back(); }
+  StreamKit* operator->() const { return k_; }
+  explicit operator bool() const { return k_ != nullptr; }
+  KitLease(const KitLease&) = delete;
+  KitLease& operator=(const KitLease&) = delete;
+
+ private:
+  struct Pool {
+    std::mutex mu;
+    std::map<int, std::vector<StreamKit*>> free;
+  };
+  static Pool& pool() {
+    static Pool* p = new Pool;
+    return *p;
+  }
+  void give_back() {
+    if (!k_) return;
+    Pool& P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    P.free[dev_].push_back(k_);
+    k_ = nullptr;
+  }
+  int dev_;
+  StreamKit* k_ = nullptr;
+};
+
+// One shard of a streamed batch: strings [s0, s1) on device `dev`, everything but the
+// result's final CSR compaction.  The result is already allocated and its offsets `poff`
+// (the batch's rebased input offsets) filled; the shard's paths sit at those offsets (its
+// labels at poff[s0] and up, its device buffers indexed from there), its statuses, final
+// weights and pull-tier statuses at string s0 and up.
+struct StreamShard {
+  int dev = 0;
+  uint32_t s0 = 0, s1 = 0;
+  FstError err = FST_OK;
+  double wall_ms = 0;
+  uint32_t launches = 0;
+};
+
+FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const uint64_t* poff,
+                      uint32_t max_len, uint32_t n, int semantics, FstBatchResult* out,
+                      int32_t* first_all) {
+  const int dev = S.dev;
+  if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
+  const uint32_t num = S.s1 - S.s0;
+  const uint64_t lbase = poff[S.s0], total = poff[S.s1] - lbase;
+  if (num == 0) return FST_OK;
+  KitLease K(dev);
+  if (!K) return FST_OOM;
+  const hipStream_t up = K->up;
+  // the shard's offsets from its first label (shard 0 of the batch: poff itself)
+  PinnedVec<uint64_t> loff_own(lbase ? num + 1 : 0);
+  const uint64_t* loff = poff + S.s0;
+  if (lbase) {
+    for (uint32_t i = 0; i <= num; ++i) loff_own[i] = poff[S.s0 + i] - lbase;
+    loff = loff_own.data();
+  }
+  const uint32_t* lsrc = src ? src + lbase : nullptr;
+  uint32_t* const il_out = out->ilabels + lbase;
   struct Threads {  // joined on every return (declared after what they use)
     std::vector<std::thread> th;
     void join() {
@@ -1048,30 +1140,8 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     ~Threads() { join(); }
   };
 
-  // ---- the result's CSR offsets (= the rebased input offsets) and max_len ----
-  uint64_t* const poff = out->path_offsets;
-  uint32_t max_len = 0;
-  {
-    const uint32_t nt = num >= (1u << 18) ? 4 : 1;
-    std::vector<uint32_t> mx(nt, 0);
-    auto rebase = [&](uint32_t t) {
-      uint32_t m = 0;
-      for (uint64_t i = (uint64_t)num * t / nt, e = (uint64_t)num * (t + 1) / nt; i < e; ++i) {
-        poff[i] = offsets[i] - base0;
-        m = std::max<uint32_t>(m, (uint32_t)(offsets[i + 1] - offsets[i]));
-      }
-      mx[t] = m;
-    };
-    Threads R;
-    for (uint32_t t = 1; t < nt; ++t) R.th.emplace_back(rebase, t);
-    rebase(0);
-    R.join();
-    for (uint32_t m : mx) max_len = std::max(max_len, m);
-    poff[num] = total;
-  }
-
   // ---- parts: string ranges cut at these fractions of the labels (per mille; small
-  // batches: one part): 1/43 and 7/43, so each part's upload fits in the previous part's
+  // shards: one part): 1/43 and 7/43, so each part's upload fits in the previous part's
   // compute.  FSTAMD_STREAM_CUTS overrides (A/B, one box: "23,163" 30.9 ms per 1M metric
   // strings, "167" 31.2, "100,400" 31.0, "125" 31.5) ----
   std::vector<uint32_t> cut{0};
@@ -1089,16 +1159,13 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     }
     for (uint64_t f : pm) {
       const uint64_t want = total * f / 1000;
-      const uint32_t i = (uint32_t)(std::upper_bound(poff, poff + num, want) - poff);
+      const uint32_t i = (uint32_t)(std::upper_bound(loff, loff + num, want) - loff);
       if (i > cut.back() && i < num) cut.push_back(i);
     }
   }
   cut.push_back(num);
   const size_t parts = cut.size() - 1;
-  if (parts > 64 || !K.events(parts)) {  // one upload event a part
-    fst_batch_result_free(out);
-    return kStreamNotApplicable;
-  }
+  if (parts > 64 || !K->events(parts)) return FST_OOM;  // one upload event a part
 
   // ---- engines and device buffers ----
   DeviceEngine::Lease EA = DeviceEngine::acquire(dev);
@@ -1110,7 +1177,6 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
       d_first(std::max<size_t>(num, 1) * 4ull), d_ctr(64 * 4);  // item counter per part
   DevOut o(num, std::max<uint64_t>(total, 1));
   if (!d_lab.p || !d_off.p || !d_first.p || !d_ctr.p || !o.ok()) return FST_OOM;
-  PinnedVec<int32_t> first(num);
   struct SyncAll {  // every return: no kernel or copy still uses the buffers or the result
     hipStream_t s[3];
     ~SyncAll() {
@@ -1120,6 +1186,12 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   } sync_all{{up, sA, sB}};
 
   // ---- uploads (offsets, then each part's labels: one event per part) ----
+  // Two ways to move the labels (FSTAMD_STREAM_STAGE): 0 = the runtime stages the pageable
+  // source itself while other threads copy it into the result's ilabels (the labels cross
+  // host DRAM twice); 1 = threads copy each chunk into the result's (pinned) ilabels and
+  // the chunk's DMA reads it from there (once).
+  const char* stage_env = std::getenv("FSTAMD_STREAM_STAGE");
+  const int stage_mode = stage_env ? std::atoi(stage_env) : 0;
   struct Ready {
     std::mutex mu;
     std::condition_variable cv;
@@ -1134,14 +1206,32 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
               hipMemsetD32Async((hipDeviceptr_t)o.status.p, kPathInternal, num, up) == hipSuccess &&
               hipMemsetD32Async((hipDeviceptr_t)d_first.p, kPathInternal, num, up) == hipSuccess &&
               hipMemsetAsync(d_ctr.p, 0, 64 * 4, up) == hipSuccess &&
-              hipMemcpyAsync(d_off.p, poff, (num + 1) * 8ull, hipMemcpyHostToDevice, up) ==
+              hipMemcpyAsync(d_off.p, loff, (num + 1) * 8ull, hipMemcpyHostToDevice, up) ==
                   hipSuccess;
+    constexpr uint64_t kChunk = 1ull << 21;  // labels per staged chunk (8 MB)
     for (size_t p = 0; p < parts && ok; ++p) {
-      const uint64_t a = poff[cut[p]], z = poff[cut[p + 1]];
-      // (a pageable source is staged through pinned memory before this returns)
-      ok = (z == a || hipMemcpyAsync((uint32_t*)d_lab.p + a, src + a, (z - a) * 4,
-                                     hipMemcpyHostToDevice, up) == hipSuccess) &&
-           hipEventRecord(K.ev[p], up) == hipSuccess;
+      const uint64_t a = loff[cut[p]], z = loff[cut[p + 1]];
+      if (stage_mode == 1) {
+        for (uint64_t c = a; c < z && ok; c += kChunk) {
+          const uint64_t e = std::min(z, c + kChunk), w = e - c;
+          const uint64_t T = w >= (1u << 19) ? 4 : 1;
+          std::vector<std::thread> cp;
+          for (uint64_t t = 1; t < T; ++t)
+            cp.emplace_back([&, t, T] {
+              std::memcpy(il_out + c + w * t / T, lsrc + c + w * t / T,
+                          (w * (t + 1) / T - w * t / T) * 4);
+            });
+          std::memcpy(il_out + c, lsrc + c, (w / T) * 4);
+          for (auto& x : cp) x.join();
+          ok = hipMemcpyAsync((uint32_t*)d_lab.p + c, il_out + c, w * 4, hipMemcpyHostToDevice,
+                              up) == hipSuccess;
+        }
+      } else {
+        // (a pageable source is staged through pinned memory before this returns)
+        ok = z == a || hipMemcpyAsync((uint32_t*)d_lab.p + a, lsrc + a, (z - a) * 4,
+                                      hipMemcpyHostToDevice, up) == hipSuccess;
+      }
+      ok = ok && hipEventRecord(K->ev[p], up) == hipSuccess;
       std::lock_guard<std::mutex> g(R.mu);
       if (ok) R.n = p + 1;
       R.cv.notify_all();
@@ -1150,7 +1240,7 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
     if (!ok) R.failed = true;
     R.cv.notify_all();
   });
-  {
+  if (stage_mode != 1) {
     // the result's ilabels, once the uploads are staged: the runtime's staging copies of
     // a pageable source read the same pages, and the kernels wait for them, not for these
     const uint64_t T = total >= (1u << 20) ? 3 : 1;
@@ -1161,21 +1251,18 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
           R.cv.wait(g, [&] { return R.failed || R.n == parts; });
         }
         const uint64_t a = total * t / T, z = total * (t + 1) / T;
-        if (z > a) std::memcpy(out->ilabels + a, src + a, (z - a) * 4);
+        if (z > a) std::memcpy(il_out + a, lsrc + a, (z - a) * 4);
       });
   }
 
   // ---- the parts: engine A takes parts 0, 2, .., engine B 1, 3, .. (A all without B) ----
-  struct PartRun {
-    FstError err = FST_OK;
-  };
-  std::vector<PartRun> pr(parts);
+  std::vector<FstError> perr(parts, FST_OK);
   // (A/B timing only: FSTAMD_STREAM_AB=1 drops the copy-out; the result then lacks paths)
   const char* abe = std::getenv("FSTAMD_STREAM_AB");
   const bool ab_nocopy = abe && std::atoi(abe) == 1;
   auto drive = [&](DeviceEngine::Lease& E, hipStream_t s, size_t p0, size_t step) {
     if (hipSetDevice(dev) != hipSuccess) {
-      pr[p0].err = FST_INVALID_ARG;
+      perr[p0] = FST_INVALID_ARG;
       return;
     }
     for (size_t p = p0; p < parts; p += step) {
@@ -1183,7 +1270,7 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
         std::unique_lock<std::mutex> g(R.mu);
         R.cv.wait(g, [&] { return R.failed || R.n > p; });
         if (R.n <= p) {
-          pr[p].err = FST_OOM;
+          perr[p] = FST_OOM;
           return;
         }
       }
@@ -1195,23 +1282,22 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
       v.path_off += s0;
       v.final_w += s0;
       v.slots = (const uint64_t*)d_off.p + s0;
-      v.host_ol = out->olabels;
-      v.host_w = out->weights;
+      v.host_ol = out->olabels + lbase;
+      v.host_w = out->weights + lbase;
       if (ab_nocopy) v.host_ol = nullptr, v.host_w = nullptr;
       v.first_status = (int32_t*)d_first.p + s0;
       // the pull tier alone: no fill, copy or host synchronisation between parts (a fill
       // or copy is a blit kernel that waits for CU slots behind the other engine's
       // persistent kernel, and had held this engine's next part back); the later tiers
       // and the downloads come after the last part
-      if (hipStreamWaitEvent(s, K.ev[p], 0) != hipSuccess ||
-          E->launch_pull_part(*D, in, n, semantics, v, s, (unsigned int*)d_ctr.p + p) !=
+      if (hipStreamWaitEvent(s, K->ev[p], 0) != hipSuccess ||
+          E->launch_pull_part(D, in, n, semantics, v, s, (unsigned int*)d_ctr.p + p) !=
               hipSuccess) {
-        pr[p].err = FST_OOM;
+        perr[p] = FST_OOM;
         return;
       }
     }
   };
-  if (t_prof) t_prof->lap(0);
   const auto tk0 = std::chrono::steady_clock::now();
   {
     Threads P;
@@ -1222,68 +1308,183 @@ int run_streamed(int dev, FrozenFst& b, const uint32_t* labels, const uint64_t* 
   for (hipStream_t x : {up, sA, sB})
     if (x && hipStreamSynchronize(x) != hipSuccess) return FST_OOM;
   for (size_t p = 0; p < parts; ++p)
-    if (pr[p].err != FST_OK) return pr[p].err;
+    if (perr[p] != FST_OK) return perr[p];
+  int32_t* const st_out = out->status + S.s0;
+  double* const fin_out = out->final_weights + S.s0;
+  int32_t* const first = first_all + S.s0;
   // statuses, final weights and the pull tier's statuses in one download each
   auto download = [&](bool with_first) {
-    return num == 0 ||
-           (hipMemcpyAsync(out->status, o.status.p, num * 4ull, hipMemcpyDeviceToHost, sA) ==
+    return (hipMemcpyAsync(st_out, o.status.p, num * 4ull, hipMemcpyDeviceToHost, sA) ==
                 hipSuccess &&
-            hipMemcpyAsync(out->final_weights, o.fin.p, num * 8ull, hipMemcpyDeviceToHost, sA) ==
+            hipMemcpyAsync(fin_out, o.fin.p, num * 8ull, hipMemcpyDeviceToHost, sA) ==
                 hipSuccess &&
-            (!with_first || hipMemcpyAsync(first.data(), d_first.p, num * 4ull,
-                                           hipMemcpyDeviceToHost, sA) == hipSuccess) &&
+            (!with_first || hipMemcpyAsync(first, d_first.p, num * 4ull, hipMemcpyDeviceToHost,
+                                           sA) == hipSuccess) &&
             hipStreamSynchronize(sA) == hipSuccess);
   };
-  if (!download(true)) return FST_OOM;
+  if (!download(true) || fault_inject("stream_after_pull")) return FST_OOM;
   // the later tiers, once, over the strings the pull tier handed on (in the device arena,
   // the same slots) -- only when it handed some on (the metric: none), then the statuses
   // and final weights again
   bool handed = false;
   for (uint32_t i = 0; i < num && !handed; ++i) handed = first[i] != kPathOk && first[i] != kPathEmpty;
+  uint32_t launches = (uint32_t)parts;
   if (handed) {
     ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
     BatchOutDev v = o.v;
     v.slots = (const uint64_t*)d_off.p;
     EA->set_after_pull(true);
-    const hipError_t e = EA->run_chain(*D, in, n, semantics, v, sA, nullptr);
+    const hipError_t e = EA->run_chain(D, in, n, semantics, v, sA, nullptr);
     EA->set_after_pull(false);
     if (e != hipSuccess || !download(false)) return FST_OOM;
+    ++launches;
+  }
+
+  // ---- paths the later tiers wrote (device arena, same slots) ----
+  uint64_t nfix = 0;
+  for (uint32_t i = 0; i < num; ++i) nfix += st_out[i] == kPathOk && first[i] != kPathOk;
+  if (nfix) {
+    const auto d2h = [&](void* dst, const void* s, size_t bytes) {
+      return bytes == 0 || hipMemcpyAsync(dst, s, bytes, hipMemcpyDeviceToHost, sA) == hipSuccess;
+    };
+    bool ok = true;
+    const char* few_env = std::getenv("FSTAMD_STREAM_FIX_FEW");  // (tests: 0 = bulk copy)
+    const uint64_t few = few_env ? std::strtoull(few_env, nullptr, 10) : 4096ull;
+    if (nfix <= few) {
+      for (uint32_t i = 0; i < num && ok; ++i)
+        if (st_out[i] == kPathOk && first[i] != kPathOk) {
+          const uint64_t a = loff[i], L = loff[i + 1] - a;
+          ok = d2h(out->olabels + lbase + a, (uint32_t*)o.ol.p + a, L * 4) &&
+               d2h(out->weights + lbase + a, (double*)o.w.p + a, L * 8);
+        }
+    } else {  // many: the whole arena (every pull-tier chase writes its path there too)
+      ok = d2h(out->olabels + lbase, o.ol.p, total * 4) &&
+           d2h(out->weights + lbase, o.w.p, total * 8);
+    }
+    if (!ok || hipStreamSynchronize(sA) != hipSuccess) return FST_OOM;
   }
   Th.join();
+  S.launches = launches;
+  S.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tk0)
+                  .count();
+  return FST_OK;
+}
+
+// The streamed host batch over `devices` (one shard per device, or `nsh` shards round
+// robin: FST_BATCH_DEVICES): the result is allocated once, every shard streams into its own
+// slice of it (fixed slots: no compaction between shards, no gather), then strings without
+// a path are compacted out on the host.  Shards are contiguous string ranges of equal
+// estimated cost (FrozenFst::chain_cost), as in run_sharded.
+int run_streamed(const std::vector<int>& devices, uint32_t nsh, FrozenFst& b,
+                 const uint32_t* labels, const uint64_t* offsets, uint32_t num, uint32_t n,
+                 int semantics, FstBatchResult* out) {
+  DeviceRestore_ restore;
+  std::vector<DeviceFst*> Ds(devices.size(), nullptr);
+  for (size_t d = 0; d < devices.size(); ++d) {  // (the rhs goes to every device first)
+    if (hipSetDevice(devices[d]) != hipSuccess) return FST_INVALID_ARG;
+    Ds[d] = b.device(devices[d]);
+    if (!Ds[d]) return FST_OOM;
+    if (Ds[d]->has_eps || !DeviceEngine::pull_first(*Ds[d], semantics))
+      return kStreamNotApplicable;
+  }
+  const uint64_t base0 = offsets[0], total = offsets[num] - base0;
+  if (!alloc_result(out, num, total)) return FST_OOM;
+  if (!pin_is_pinned(out->ilabels) || !pin_is_pinned(out->olabels) ||
+      !pin_is_pinned(out->weights) || !pin_is_pinned(out->path_offsets) ||
+      !pin_is_pinned(out->status) || !pin_is_pinned(out->final_weights)) {
+    fst_batch_result_free(out);
+    return kStreamNotApplicable;
+  }
+  const uint32_t* src = labels ? labels + base0 : nullptr;
+
+  // ---- the result's CSR offsets (= the rebased input offsets) and max_len ----
+  uint64_t* const poff = out->path_offsets;
+  uint32_t max_len = 0;
+  {
+    const uint32_t nt = num >= (1u << 18) ? 4 : 1;
+    std::vector<uint32_t> mx(nt, 0);
+    auto rebase = [&](uint32_t t) {
+      uint32_t m = 0;
+      for (uint64_t i = (uint64_t)num * t / nt, e = (uint64_t)num * (t + 1) / nt; i < e; ++i) {
+        poff[i] = offsets[i] - base0;
+        m = std::max<uint32_t>(m, (uint32_t)(offsets[i + 1] - offsets[i]));
+      }
+      mx[t] = m;
+    };
+    std::vector<std::thread> R;
+    for (uint32_t t = 1; t < nt; ++t) R.emplace_back(rebase, t);
+    rebase(0);
+    for (auto& t : R) t.join();
+    for (uint32_t m : mx) max_len = std::max(max_len, m);
+    poff[num] = total;
+  }
+
+  // ---- shards: contiguous string ranges of equal estimated cost ----
+  nsh = std::max<uint32_t>(1, std::min<uint32_t>(nsh, num));
+  std::vector<StreamShard> sh(nsh);
+  const bool shard_log = std::getenv("FSTAMD_SHARD_LOG") != nullptr;
+  std::vector<double> pre;  // cost of strings [0, i) (chain_cost per distinct length)
+  if (nsh > 1 || shard_log) {
+    std::vector<double> cl(max_len + 1, -1.0);
+    pre.assign(num + 1, 0.0);
+    for (uint32_t i = 0; i < num; ++i) {
+      const uint32_t L = (uint32_t)(poff[i + 1] - poff[i]);
+      if (cl[L] < 0) cl[L] = b.chain_cost(L);
+      pre[i + 1] = pre[i] + cl[L];
+    }
+  }
+  {
+    std::vector<uint32_t> cuts{0};
+    if (nsh > 1) {
+      for (uint32_t j = 1; j < nsh; ++j) {
+        const double goal = pre[num] * j / nsh;
+        uint32_t i = (uint32_t)(std::lower_bound(pre.begin(), pre.end(), goal) - pre.begin());
+        i = std::max(i, cuts.back() + 1);          // never empty
+        i = std::min(i, num - (nsh - j));           // at least one string for each later one
+        cuts.push_back(i);
+      }
+    }
+    cuts.push_back(num);
+    for (uint32_t j = 0; j < nsh; ++j) {
+      sh[j].dev = devices[j % devices.size()];
+      sh[j].s0 = cuts[j];
+      sh[j].s1 = cuts[j + 1];
+    }
+  }
+  if (shard_log)  // tests: the shard plan and the route
+    for (uint32_t j = 0; j < nsh; ++j)
+      std::fprintf(stderr, "[libfst_amd shard] %u dev %d strings %u..%u cost %.6g route streamed\n",
+                   j, sh[j].dev, sh[j].s0, sh[j].s1, pre[sh[j].s1] - pre[sh[j].s0]);
+
+  PinnedVec<int32_t> first(std::max<uint32_t>(num, 1));
+  if (t_prof) t_prof->lap(0);
+  const auto tk0 = std::chrono::steady_clock::now();
+  {
+    auto run = [&](uint32_t j) {
+      StreamShard& S = sh[j];
+      const size_t d = (size_t)(j % devices.size());
+      S.err = stream_shard(S, *Ds[d], src, poff, max_len, n, semantics, out, first.data());
+    };
+    std::vector<std::thread> th;
+    for (uint32_t j = 1; j < nsh; ++j) th.emplace_back(run, j);
+    run(0);
+    for (auto& t : th) t.join();
+  }
   LaunchStats agg{};  // (the parts overlap on two streams: their wall time, not a sum)
   agg.engine = semantics == 1 ? 0 : 7;
-  agg.launches = (uint32_t)parts + 1;
+  for (const StreamShard& S : sh) {
+    if (S.err != FST_OK) return S.err;
+    agg.launches += S.launches;
+  }
   agg.kernel_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tk0).count();
   t_last_stats = agg;
   if (t_prof) t_prof->lap(2);
-  const hipStream_t stream = sA;
 
-  // ---- fix-ups: paths the later tiers wrote (device arena, same slots), then the CSR ----
-  uint64_t nfix = 0, nbad = 0;
-  for (uint32_t i = 0; i < num; ++i) {
-    nbad += out->status[i] != kPathOk;
-    nfix += out->status[i] == kPathOk && first[i] != kPathOk;
-  }
-  if (nfix) {
-    const auto d2h = [&](void* dst, const void* s, size_t bytes) {
-      return bytes == 0 ||
-             hipMemcpyAsync(dst, s, bytes, hipMemcpyDeviceToHost, stream) == hipSuccess;
-    };
-    bool ok = true;
-    if (nfix <= 4096) {
-      for (uint32_t i = 0; i < num && ok; ++i)
-        if (out->status[i] == kPathOk && first[i] != kPathOk) {
-          const uint64_t a = poff[i], L = poff[i + 1] - a;
-          ok = d2h(out->olabels + a, (uint32_t*)o.ol.p + a, L * 4) &&
-               d2h(out->weights + a, (double*)o.w.p + a, L * 8);
-        }
-    } else {  // many: the whole arena (the pull tier's paths are in it too)
-      ok = d2h(out->olabels, o.ol.p, total * 4) && d2h(out->weights, o.w.p, total * 8);
-    }
-    if (!ok || hipStreamSynchronize(stream) != hipSuccess) return FST_OOM;
-  }
-  if (nbad) {  // drop the slots of strings without a path (in order, moving left)
+  // ---- strings without a path: their slots dropped (in order, moving left) ----
+  uint64_t nbad = 0;
+  for (uint32_t i = 0; i < num; ++i) nbad += out->status[i] != kPathOk;
+  if (nbad) {
     uint64_t dst = 0;
     for (uint32_t i = 0; i < num; ++i) {
       const uint64_t a = poff[i], L = poff[i + 1] - a;
@@ -1344,7 +1545,7 @@ FstError run_sharded(const std::vector<int>& devices, uint32_t nsh, uint32_t num
     for (uint32_t j = 0; j < nsh; ++j) {
       double c = 0;
       for (uint32_t i = sh[j].s0; i < sh[j].s1 && i < cost.size(); ++i) c += cost[i];
-      std::fprintf(stderr, "[libfst_amd shard] %u dev %d strings %u..%u cost %.6g\n", j,
+      std::fprintf(stderr, "[libfst_amd shard] %u dev %d strings %u..%u cost %.6g route sharded\n", j,
                    sh[j].dev, sh[j].s0, sh[j].s1, c);
     }
   auto phase1 = [&](Shard& S) {
@@ -2150,13 +2351,12 @@ FstError fst_compose_frozen_shortest_path_batch(FstHandle b_handle, const uint32
   struct ProfScope {
     ~ProfScope() { t_prof = nullptr; }
   } prof_scope;
-  // one device, an rhs without input epsilons and a pull tier first: the streamed batch
-  // (FSTAMD_STREAM=0 turns it off)
-  if (devices.size() == 1 && nsh == 1 && num_strings > 0) {
+  // an rhs without input epsilons and a pull tier first: the streamed batch, on one device
+  // or sharded over several (FSTAMD_STREAM=0 turns it off)
+  if (num_strings > 0) {
     const char* se = std::getenv("FSTAMD_STREAM");
     if (!(se && std::strcmp(se, "0") == 0)) {
-      DeviceRestore_ restore;
-      const int e = run_streamed(devices[0], *b, labels, offsets, num_strings, n, semantics, out);
+      const int e = run_streamed(devices, nsh, *b, labels, offsets, num_strings, n, semantics, out);
       if (e != kStreamNotApplicable) {
         if (e != FST_OK) {
           fst_batch_result_free(out);

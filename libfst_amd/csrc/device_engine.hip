@@ -518,17 +518,26 @@ DeviceEngine::DeviceEngine(int dev) : dev_(dev) {
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) stream_ = nullptr;
 }
 
-void DeviceEngine::trim_idle(int dev) {
+// The idle engines' workspaces leave them under the pool lock; hipFree (it waits for the
+// device's work, other engines' running kernels included) runs after the lock is released,
+// so acquire / try_acquire on this device never wait behind it.
+void DeviceEngine::trim_idle(int dev, const DeviceEngine* except) {
   if (dev < 0) return;
   EnginePool& P = engine_pool(dev);
-  std::lock_guard<std::mutex> g(P.mu);
-  for (DeviceEngine* e : P.idle) e->free_scratch();
+  std::vector<void*> drop;
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    for (DeviceEngine* e : P.idle)
+      if (e != except) e->take_scratch(&drop);
+  }
+  if (drop.empty()) return;
+  (void)hipSetDevice(dev);
+  for (void* p : drop) (void)hipFree(p);
 }
 
-void DeviceEngine::free_scratch() {
-  (void)hipSetDevice(dev_);
+void DeviceEngine::take_scratch(std::vector<void*>* out) {
   for (size_t i = 0; i < bufs_.size(); ++i) {
-    if (bufs_[i]) (void)hipFree(bufs_[i]);  // (hipFree waits for the device's work)
+    if (bufs_[i]) out->push_back(bufs_[i]);
     bufs_[i] = nullptr;
     sizes_[i] = 0;
   }
@@ -545,12 +554,7 @@ void* DeviceEngine::scratch(size_t idx, size_t bytes) {
     // per engine, so up to max_engines() sets of them) and the cached pool blocks go back,
     // then once more (this engine's own buffers may be in use by this call's launches)
     (void)hipGetLastError();
-    {
-      EnginePool& P = engine_pool(dev_);
-      std::lock_guard<std::mutex> g(P.mu);
-      for (DeviceEngine* e : P.idle)
-        if (e != this) e->free_scratch();
-    }
+    trim_idle(dev_, this);
     device_pool_release(dev_);
     (void)hipSetDevice(dev_);
     if (hipMalloc(&bufs_[idx], bytes) != hipSuccess) {

@@ -351,8 +351,8 @@ class DeviceEngine {
   // no pull launch); the later tiers take the strings it handed on.
   void set_after_pull(bool v) { after_pull_ = v; }
   // Out of HBM: the workspaces of the device's idle engines (kept per engine between calls)
-  // go back to the device.
-  static void trim_idle(int dev);
+  // go back to the device (all but `except`'s; hipFree outside the pool lock).
+  static void trim_idle(int dev, const DeviceEngine* except = nullptr);
   hipError_t run_graph(const DeviceFst& rhs, const GraphInput& in, uint32_t n, int semantics,
                        const BatchOutDev& out, hipStream_t stream, LaunchStats* stats);
   // fst_compose_frozen: the whole lattice of one general lhs (kernels/eager_bfs.hpp), on
@@ -392,7 +392,7 @@ class DeviceEngine {
   explicit DeviceEngine(int dev);
   hipStream_t stream_ = nullptr;   // the engine's own stream (non-blocking)
   bool after_pull_ = false;        // run_chain: the pull tier already ran (set_after_pull)
-  void free_scratch();             // every workspace back to the device (an idle engine)
+  void take_scratch(std::vector<void*>* out);  // an idle engine's workspaces, to be freed
   hipEvent_t done_ = nullptr;      // recorded when a lease ends (on the stream it used)
   hipStream_t done_stream_ = nullptr;
   bool done_valid_ = false;

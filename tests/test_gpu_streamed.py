@@ -89,3 +89,100 @@ def test_streamed_batch(metric, sem, cuts, monkeypatch):
     assert np.array_equal(got.olabels, ref.olabels)
     assert np.array_equal(bits(got.weights), bits(ref.weights))
     assert np.array_equal(bits(got.finals), bits(ref.finals))
+
+
+def handed_on_batch(rng, num=48000, every=5):
+    """Metric strings with a label-0 arc in every `every`-th one (short, so the general
+    engine finishes them quickly): > 4096 strings handed on by the pull tier."""
+    seqs = []
+    for i in range(num):
+        if i % every == 0:
+            L = int(rng.integers(8, 24))
+            q = np.ones(L, np.uint32)
+            q[int(rng.integers(0, L))] = 0
+        else:
+            L = int(rng.integers(100, 130))
+            q = np.where(rng.random(L) < 0.9, 1, 2).astype(np.uint32)
+        seqs.append(q)
+    offsets = np.concatenate([[0], np.cumsum([len(q) for q in seqs])]).astype(np.uint64)
+    return np.concatenate(seqs).astype(np.uint32), offsets
+
+
+def same_result(a, b):
+    assert np.array_equal(a.status, b.status)
+    assert np.array_equal(a.offsets, b.offsets)
+    assert np.array_equal(a.ilabels, b.ilabels)
+    assert np.array_equal(a.olabels, b.olabels)
+    assert np.array_equal(bits(a.weights), bits(b.weights))
+    assert np.array_equal(bits(a.finals), bits(b.finals))
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_streamed_bulk_fixup(metric, sem, monkeypatch):
+    # more than 4096 strings handed on: the fix-up copies the whole device arena over the
+    # paths the pull tier already wrote into the result (ADVICE round 5)
+    rhs, blob = metric
+    rng = np.random.default_rng(777 + sem)
+    labels, offsets = handed_on_batch(rng)
+    assert offsets[-1] >= (1 << 22)
+    monkeypatch.setenv("FSTAMD_SHARD_LOG", "1")
+    got = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+    num = len(offsets) - 1
+    idx = np.unique(np.concatenate([rng.choice(num, 120, replace=False),
+                                    np.arange(0, num, 997), [num - 1]])).astype(np.int64)
+    compare_sample(got, blob, labels, offsets, sem, idx)
+    monkeypatch.setenv("FSTAMD_STREAM", "0")
+    same_result(got, F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem))
+    # and the per-string fix-up on the same batch gives the same bytes
+    monkeypatch.delenv("FSTAMD_STREAM")
+    monkeypatch.setenv("FSTAMD_STREAM_FIX_FEW", "1000000")
+    same_result(got, F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem))
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+def test_streamed_label_staging_modes(metric, sem, monkeypatch):
+    # FSTAMD_STREAM_STAGE=1: the labels copied into the result's pinned ilabels chunk by
+    # chunk and uploaded from there (one host-DRAM pass) -- the same result as the
+    # runtime-staged upload
+    rhs, blob = metric
+    rng = np.random.default_rng(31337 + sem)
+    labels, offsets = mixed_batch(rng)
+    monkeypatch.setenv("FSTAMD_STREAM_STAGE", "0")
+    a = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+    monkeypatch.setenv("FSTAMD_STREAM_STAGE", "1")
+    b = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+    same_result(a, b)
+    num = len(offsets) - 1
+    compare_sample(b, blob, labels, offsets, sem,
+                   np.unique(np.concatenate([rng.choice(num, 80, replace=False), [0, num - 1]])))
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
+@pytest.mark.parametrize("shards", [2, 3])
+def test_streamed_shards_on_one_gpu(metric, sem, shards, monkeypatch, capfd):
+    # FST_BATCH_DEVICES through the streamed entry: each shard streams into its own slice
+    # of the one pinned result (fixed slots), strings without a path compacted out after
+    # the last shard; 2 and 3 logical shards on device 0 equal the one-shard run and the
+    # oracle bit for bit
+    rhs, blob = metric
+    rng = np.random.default_rng(4040 + 10 * shards + sem)
+    labels, offsets = mixed_batch(rng, num=90000)
+    one = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
+    capfd.readouterr()
+    monkeypatch.setenv("FSTAMD_SHARD_LOG", "1")
+    many = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem, devices=[0],
+                                                shards=shards)
+    err = capfd.readouterr().err
+    plan = [ln.split() for ln in err.splitlines() if ln.startswith("[libfst_amd shard]")]
+    assert len(plan) == shards and all(p[-1] == "streamed" for p in plan), err[-2000:]
+    spans = [tuple(int(x) for x in p[6].split("..")) for p in plan]
+    num = len(offsets) - 1
+    assert spans[0][0] == 0 and spans[-1][1] == num
+    assert all(spans[j][1] == spans[j + 1][0] for j in range(shards - 1))
+    costs = [float(p[8]) for p in plan]
+    assert max(costs) / min(costs) < 1.2
+    same_result(many, one)
+    # strings on both sides of every shard boundary, against the oracle
+    edges = np.asarray([s for sp in spans for s in (sp[0], sp[1] - 1)])
+    idx = np.unique(np.concatenate([edges, rng.choice(num, 100, replace=False)])).astype(np.int64)
+    compare_sample(many, blob, labels, offsets, sem, idx)
