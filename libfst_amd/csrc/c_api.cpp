@@ -1113,7 +1113,11 @@ struct StreamShard {
 
 FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const uint64_t* poff,
                       uint32_t max_len, uint32_t n, int semantics, FstBatchResult* out,
-                      int32_t* first_all) {
+                      int32_t* first_all, std::mutex* later_mu) {
+  // the later tiers of the shards of one device run one shard at a time, each to the end of
+  // its leases (declared after this lock, so released before it): the heavy replays size
+  // their workspaces from the free HBM, which a concurrent shard's would have taken
+  std::unique_lock<std::mutex> later_lock(*later_mu, std::defer_lock);
   const int dev = S.dev;
   if (hipSetDevice(dev) != hipSuccess) return FST_INVALID_ARG;
   const uint32_t num = S.s1 - S.s0;
@@ -1330,6 +1334,7 @@ FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const u
   for (uint32_t i = 0; i < num && !handed; ++i) handed = first[i] != kPathOk && first[i] != kPathEmpty;
   uint32_t launches = (uint32_t)parts;
   if (handed) {
+    later_lock.lock();
     ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
     BatchOutDev v = o.v;
     v.slots = (const uint64_t*)d_off.p;
@@ -1457,13 +1462,15 @@ int run_streamed(const std::vector<int>& devices, uint32_t nsh, FrozenFst& b,
                    j, sh[j].dev, sh[j].s0, sh[j].s1, pre[sh[j].s1] - pre[sh[j].s0]);
 
   PinnedVec<int32_t> first(std::max<uint32_t>(num, 1));
+  std::vector<std::mutex> later_mu(devices.size());  // (stream_shard: per device)
   if (t_prof) t_prof->lap(0);
   const auto tk0 = std::chrono::steady_clock::now();
   {
     auto run = [&](uint32_t j) {
       StreamShard& S = sh[j];
       const size_t d = (size_t)(j % devices.size());
-      S.err = stream_shard(S, *Ds[d], src, poff, max_len, n, semantics, out, first.data());
+      S.err = stream_shard(S, *Ds[d], src, poff, max_len, n, semantics, out, first.data(),
+                           &later_mu[d]);
     };
     std::vector<std::thread> th;
     for (uint32_t j = 1; j < nsh; ++j) th.emplace_back(run, j);

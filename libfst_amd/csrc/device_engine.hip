@@ -486,12 +486,32 @@ hipStream_t DeviceEngine::Lease::use(hipStream_t s) {
   return s;
 }
 
+// Workspaces above this many bytes (96 GB: the dense and band replays size theirs from the free
+// HBM) go back to the device when the lease ends: kept by an idle engine, they would leave
+// the next heavy plan on this device -- another engine's, maybe another shard's of the same
+// streamed call -- only the reserve to size itself from.  FSTAMD_RETAIN_GB overrides.
+static size_t retain_bytes() {
+  static const size_t b = [] {
+    const char* e = std::getenv("FSTAMD_RETAIN_GB");
+    return (size_t)(e ? std::max(0, std::atoi(e)) : 96) << 30;
+  }();
+  return b;
+}
+
 void DeviceEngine::Lease::release() {
   if (!e_) return;
   if (used_) {
     (void)hipSetDevice(e_->dev_);
     e_->done_valid_ = hipEventRecord(e_->done_, s_) == hipSuccess;
     e_->done_stream_ = s_;
+  }
+  size_t held = 0;
+  for (size_t b : e_->sizes_) held += b;
+  if (held > retain_bytes()) {  // (hipFree waits for the device's work, this lease's too)
+    std::vector<void*> drop;
+    e_->take_scratch(&drop);
+    (void)hipSetDevice(e_->dev_);
+    for (void* q : drop) (void)hipFree(q);
   }
   EnginePool& P = engine_pool(e_->dev_);
   {
@@ -541,6 +561,10 @@ void DeviceEngine::take_scratch(std::vector<void*>* out) {
     bufs_[i] = nullptr;
     sizes_[i] = 0;
   }
+  // the arrays that are initialised once per allocation must be initialised again: a new
+  // allocation of the same size may come back at the same address, dirty
+  ll_clean_ = ld_clean_ = ld_leaf_ = lb_clean_ = nullptr;
+  ll_clean_bytes_ = ld_clean_bytes_ = ld_leaf_bytes_ = lb_clean_bytes_ = 0;
 }
 
 void* DeviceEngine::scratch(size_t idx, size_t bytes) {

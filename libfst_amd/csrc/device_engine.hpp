@@ -143,6 +143,10 @@ struct DeviceFst {
   double int_wmax = -1.0;    // largest arc weight times RevView::winv^-1 when every scaled
                              // weight is an integer >= 0 below 2^24, else -1
   bool widx = false;         // rrec4 holds weight-table indices (RK 4; rv_weight_table)
+  // the direct layout with every in-arc group within 255 / kp blocks: a back record can be
+  // one byte, the in-arc's position x * kp + m in its target's group (the chases re-derive
+  // the record from the target state: tier P with rrec4, the lazy pull with any records)
+  bool byte_back = false;
   // Routing hints learnt from earlier batches on this rhs: a small-lattice (LDS) tier that
   // handed on nearly every string is skipped next time (config 3's lattices never fit).
   mutable std::atomic<int> skip_tiny_lazy{0}, skip_tiny_eager{0};

@@ -80,28 +80,33 @@ const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len, bool log = f
 #define FSTAMD_LP_WAVES_F32 5
 #endif
 constexpr int kLazyPullWaves = 3;
+// B1: 1-B back records (DeviceFst::byte_back; the direct layout only)
 template <int KP, int RK>
-const void* lazy_pull_ptr(bool direct) {
+const void* lazy_pull_ptr(bool direct, bool b1) {
   constexpr int wv = (RK && KP <= 5) ? FSTAMD_LP_WAVES_F32 : kLazyPullWaves;  // 8-record
                                                                           // blocks spill at 4
-  return direct ? (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, RK>
-                : (const void*)lazy_pull_kernel<kPullRows, KP, false, wv, RK>;
+  if (!direct) return (const void*)lazy_pull_kernel<kPullRows, KP, false, wv, RK, false>;
+  return b1 ? (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, RK, true>
+            : (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, RK, false>;
 }
 template <int RK>
-const void* lazy_pull_kernel_for(const RevView& rv) {
-  const bool dir = rv.direct != 0;
-  switch (rv.kp) {
-    case 4: return lazy_pull_ptr<4, RK>(dir);
-    case 5: return lazy_pull_ptr<5, RK>(dir);
-    default: return lazy_pull_ptr<8, RK>(dir);
+const void* lazy_pull_kernel_for(const DeviceFst& rhs) {
+  const bool dir = rhs.rev.direct != 0, b1 = dir && rhs.byte_back;
+  switch (rhs.rev.kp) {
+    case 4: return lazy_pull_ptr<4, RK>(dir, b1);
+    case 5: return lazy_pull_ptr<5, RK>(dir, b1);
+    default: return lazy_pull_ptr<8, RK>(dir, b1);
   }
 }
 const void* lazy_pull_kernel_for(const DeviceFst& rhs, uint32_t max_len, bool log = false) {
   const int rk = !lazy_pull_f32(rhs, max_len) ? 0 : use_rec8(rhs.rev) ? 2 : 1;
+  if (log && std::getenv("FSTAMD_ROUTE_LOG"))
+    std::fprintf(stderr, "[libfst_amd route] lazy pull: back records %d B\n",
+                 rhs.rev.direct && rhs.byte_back ? 1 : 4);
   switch (route_rk("lazy", rk, rhs.rev, log)) {
-    case 0: return lazy_pull_kernel_for<0>(rhs.rev);
-    case 2: return lazy_pull_kernel_for<2>(rhs.rev);
-    default: return lazy_pull_kernel_for<1>(rhs.rev);
+    case 0: return lazy_pull_kernel_for<0>(rhs);
+    case 2: return lazy_pull_kernel_for<2>(rhs);
+    default: return lazy_pull_kernel_for<1>(rhs);
   }
 }
 }  // namespace
@@ -283,6 +288,11 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       rxrec[t] = make_uint2(rspan[t].x, rspan[t].y);
     }
   }
+  // 1-B back records: the direct layout, every in-arc group within 255 / kp blocks
+  uint64_t max_nb = 0;
+  for (const uint4& r : rspan)
+    if (r.z != kSpanMixed) max_nb = std::max<uint64_t>(max_nb, r.y);
+  const bool byte_back = direct && max_nb * kp <= 255 && !std::getenv("FSTAMD_NO_BYTE_BACK");
   std::vector<uint4> rrec32;
   std::vector<uint2> rrec8;
   if (d->int_wmax >= 0.0 && d->int_wmax <= kRec8WMax) {
@@ -339,13 +349,8 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
     // of a window, 8 * (kPullW - 1) + rbias8, stays below a padding record's 0xFFFF, so
     // base - 0xFFFF always wraps past slot W (a backward jump of ~7,900 states would
     // otherwise turn padding into an in-window cell)
-    // Tier P then keeps 1-B back records (x * kp + m, eager_pull.hpp): the direct layout
-    // only, every in-arc group within 255 / kp blocks
-    uint64_t max_nb = 0;
-    for (const uint4& r : rspan)
-      if (r.z != kSpanMixed) max_nb = std::max<uint64_t>(max_nb, r.y);
-    if ((dhi - dlo) * 8 < 0xFFF0 && -dlo * 8 + 8 * (int64_t)kPullW <= 0xFFFF && direct &&
-        max_nb * kp <= 255) {
+    // Tier P then keeps 1-B back records (x * kp + m, eager_pull.hpp): byte_back below
+    if ((dhi - dlo) * 8 < 0xFFF0 && -dlo * 8 + 8 * (int64_t)kPullW <= 0xFFFF && byte_back) {
       rbias8 = (uint32_t)(-dlo * 8);
       rrec4.resize(rrec.size());
       for (size_t r = 0; r < rrec.size(); ++r) {
@@ -400,6 +405,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
                    (const uint32_t*)d->rev_bufs[6], (const uint2*)d->rev_bufs[7],
                    (uint32_t)(nblocks * kp), (const uint32_t*)d->rev_bufs[8], rbias8,
                    1.0 / wscale};
+  d->byte_back = byte_back;
   d->pull_ok = true;
   d->lazy_pull_ok = ol_ordered && d->finite && !std::getenv("FSTAMD_NO_LAZY_PULL");
   return true;

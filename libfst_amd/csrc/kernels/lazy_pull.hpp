@@ -145,8 +145,12 @@ struct LazyPullLds {
   ChaseJob job[kLpChase];
 };
 
-// RK: the records, as in eager_pull_kernel (0 RevRec, 1 rrec32, 2 rrec8)
-template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, int RK>
+// RK: the records, as in eager_pull_kernel (0 RevRec, 1 rrec32, 2 rrec8).  B1 (direct
+// layout, DeviceFst::byte_back): 1-B back records, the back arc's position x * KP + m in its
+// target's in-arc group (block x, slot m), as tier P's; the chase walks the states back from
+// the best final's and re-derives each record from its target (block 0 at t * KP, blocks
+// 1.. from rxrec[t].x).  Else 4-B records: the reverse record's index.
+template <int EW, int KP, bool DIRECT, int WAVES_PER_EU, int RK, bool B1 = false>
 __global__ void __launch_bounds__(64, WAVES_PER_EU)
 lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                  unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
@@ -176,6 +180,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   };
   constexpr int kWords = LazyPullLds<W, DT>::kWords;
   static_assert(KP <= 16 && W < 512, "key layout as in eager_pull.hpp");
+  static_assert(!B1 || DIRECT, "byte back records need the direct layout");
   __shared__ LazyPullLds<W, DT> S;
   auto& CL = S.c;
 #ifdef FSTAMD_LP_PAD  // occupancy experiment only: LDS padding to cut waves per SIMD
@@ -200,16 +205,23 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       maxL = jb.L;
     }
     maxL = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_u32(maxL));
-    // slab: 4-B back records (the reverse record of each tuple's back arc) in its first
-    // half, per layer k {slab base, window origin} of layer k in its second half: the
-    // record's source state gives the source's slab position
+    // slab: back records (B1: 1 B, else the 4-B reverse record index of each tuple's back
+    // arc) in its first half, per layer k {slab base, window origin} of layer k in its
+    // second half: the record's source state gives the source's slab position
     const uint32_t* sl = reinterpret_cast<const uint32_t*>(slabs + (size_t)lane * lp.back_cap);
     const uint2* hdr = slabs + (size_t)lane * lp.back_cap + lp.back_cap / 2;
     uint32_t id = jb.id;
+    uint32_t tcur = jb.pad;  // B1: the state of the tuple at slab position id
     for (uint32_t t = 0; t < maxL; ++t) {  // uniform trip count; lanes mask themselves
       if (lane < njobs && t < jb.L) {
         const uint32_t k = jb.L - 1 - t;
-        const uint32_t b = FB(sl[FB(id, lp.back_cap, 70)], rv.nrec, 73);
+        uint32_t b;
+        if constexpr (B1) {
+          const uint32_t v = reinterpret_cast<const uint8_t*>(sl)[FB(id, lp.back_cap, 70)];
+          b = FB(v < (uint32_t)KP ? tcur * KP + v : rv.rxrec[tcur].x + v - KP, rv.nrec, 73);
+        } else {
+          b = FB(sl[FB(id, lp.back_cap, 70)], rv.nrec, 73);
+        }
         const uint2 h = hdr[k];
         if (!out.host_ol) out.out_il[jb.o + k] = in.labels[jb.off + k];
         uint32_t src8;
@@ -229,7 +241,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           out.out_w[jb.o + k] = r.weight;  // times(One, w) == w for w >= +0
           src8 = r.src;
         }
-        id = h.x + ((src8 >> 3) - h.y);
+        tcur = src8 >> 3;
+        id = h.x + (tcur - h.y);
       }
     }
     if (lane < njobs) {
@@ -422,7 +435,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #else
         c = tight_min<KP>(nd, b, bpk);
 #endif
-        uint32_t ra = rec0 + ((c >> 13) & 15u);
+        uint32_t ra = (B1 ? 0u : rec0) + ((c >> 13) & 15u);
         if (hubs) {  // the further blocks: first toucher, distance, back-pointer
           // (block 1's record, loaded here: a branch before the row's record loads would
           // hold them behind the label load)
@@ -445,7 +458,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
               if (n2 < b || (n2 == b && p2 < c)) {
                 b = n2;
                 c = p2;
-                ra = rxx + m;
+                ra = B1 ? x * KP + m : rxx + m;
               }
               if (want_work()) relax += (uint32_t)__popcll(__ballot(iw < kLpAbsent));
             }
@@ -628,7 +641,10 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           hi_slot = max(hi_slot, (uint32_t)e * 64 + 63u - (uint32_t)__builtin_clzll(pm));
         }
         if (pres) {
-          *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 71) * 4u)) = bra[e];
+          if constexpr (B1)
+            reinterpret_cast<uint8_t*>(back)[FB(nbase + i, lp.back_cap, 71)] = (uint8_t)bra[e];
+          else
+            *const_cast<uint32_t*>(at_byte(back, FB(nbase + i, lp.back_cap, 71) * 4u)) = bra[e];
           if (last) {  // best final: lexmin (total, id) (compose-shortest-path.zig:165-179)
             const uint32_t t = tn + i;
             const double fw2 = rhs.final_w[FB(t, rhs.num_states, 72)];
@@ -912,6 +928,7 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       j.si = si;
       j.L = L;
       j.id = base + (bp & 511u);
+      j.pad = tmin + (bp & 511u);  // (its state: B1's chase walks the states back from it)
       j.tuples = tuples;
       j.relax = relax;
       j.o = o;

@@ -166,7 +166,7 @@ def test_streamed_shards_on_one_gpu(metric, sem, shards, monkeypatch, capfd):
     # oracle bit for bit
     rhs, blob = metric
     rng = np.random.default_rng(4040 + 10 * shards + sem)
-    labels, offsets = mixed_batch(rng, num=90000)
+    labels, offsets = mixed_batch(rng, num=60000)
     one = F.compose_frozen_shortest_path_batch(rhs, labels, offsets, 1, sem)
     capfd.readouterr()
     monkeypatch.setenv("FSTAMD_SHARD_LOG", "1")
@@ -184,5 +184,5 @@ def test_streamed_shards_on_one_gpu(metric, sem, shards, monkeypatch, capfd):
     same_result(many, one)
     # strings on both sides of every shard boundary, against the oracle
     edges = np.asarray([s for sp in spans for s in (sp[0], sp[1] - 1)])
-    idx = np.unique(np.concatenate([edges, rng.choice(num, 100, replace=False)])).astype(np.int64)
+    idx = np.unique(np.concatenate([edges, rng.choice(num, 40, replace=False)])).astype(np.int64)
     compare_sample(many, blob, labels, offsets, sem, idx)
