@@ -111,7 +111,10 @@ struct RevView {
   // table of the rhs's distinct arc weights stored after the records, rv_weight_table)
 };
 constexpr uint32_t kPullWt = 64;  // (a power of two: the kernels mask the index)
-// the weight table of an rhs with DeviceFst::widx: kPullWt doubles right after the
+// rhs with 65..256 distinct weights: tier P's RK 5 (the same records, a 256-entry LDS
+// table, 4 waves per SIMD instead of 5); the global copy always holds kPullWtMax entries
+constexpr uint32_t kPullWtMax = 256;
+// the weight table of an rhs with DeviceFst::widx: kPullWtMax doubles right after the
 // rrec4 records (their count rounded up to 8-B alignment)
 __host__ __device__ inline const double* rv_weight_table(const RevView& rv) {
   return reinterpret_cast<const double*>(rv.rrec4 + ((rv.nrec + 1u) & ~1u));
@@ -142,7 +145,8 @@ struct DeviceFst {
   bool lazy_pull_ok = false;
   double int_wmax = -1.0;    // largest arc weight times RevView::winv^-1 when every scaled
                              // weight is an integer >= 0 below 2^24, else -1
-  bool widx = false;         // rrec4 holds weight-table indices (RK 4; rv_weight_table)
+  bool widx = false;         // rrec4 holds weight-table indices (RK 4 / 5; rv_weight_table)
+  uint32_t wt_n = 0;         // distinct arc weights in that table (<= kPullWtMax)
   // the direct layout with every in-arc group within 255 / kp blocks: a back record can be
   // one byte, the in-arc's position x * kp + m in its target's group (the chases re-derive
   // the record from the target state: tier P with rrec4, the lazy pull with any records)

@@ -40,7 +40,8 @@ const void* pull_kernel_ptr(bool direct) {
 template <int RK>
 const void* pull_kernel_for(const RevView& rv) {
   const bool dir = rv.direct != 0;
-  constexpr int wv = RK == 4 ? FSTAMD_PULL_WAVES_SMALL  // (f64 cells)
+  constexpr int wv = RK == 5 ? 4  // (f64 cells and a 2 KB weight table: 8.9 KB of LDS)
+                   : RK == 4 ? FSTAMD_PULL_WAVES_SMALL  // (f64 cells)
                    : RK >= 2 ? FSTAMD_PULL_WAVES_R8 : RK ? FSTAMD_PULL_WAVES_F32 : FSTAMD_PULL_WAVES_SMALL;
   switch (rv.kp) {
     case 4: return pull_kernel_ptr<4, wv, RK>(dir);
@@ -51,40 +52,48 @@ const void* pull_kernel_for(const RevView& rv) {
 // the 8-B records when the rhs has them (every weight an integer <= kRec8WMax)
 bool use_rec8(const RevView& rv) { return rv.rrec8 && !std::getenv("FSTAMD_NO_REC8"); }
 // FSTAMD_ROUTE_LOG: which records the pull kernel reads (0 RevRec / f64 cells, 1 rrec32,
-// 2 rrec8, 3 rrec4, 4 rrec4 with weight indices and f64 cells) and the weight scale 2^k of
+// 2 rrec8, 3 rrec4, 4 rrec4 with weight indices and f64 cells, 5 the same with a 256-entry
+// table) and the weight scale 2^k of
 // the integer records (tests)
 int route_rk(const char* sem, int rk, const RevView& rv, bool log) {
   if (log && std::getenv("FSTAMD_ROUTE_LOG"))
     std::fprintf(stderr, "[libfst_amd route] %s pull: records %d, weight scale %g\n", sem, rk,
-                 rk && rk != 4 ? 1.0 / rv.winv : 1.0);
+                 rk && rk < 4 ? 1.0 / rv.winv : 1.0);
   return rk;
 }
 int pull_rk(const DeviceFst& rhs, uint32_t max_len) {
   if (!pull_f32(rhs, max_len) || std::getenv("FSTAMD_P_F64"))  // f64 cells
-    return rhs.rev.rrec4 && rhs.widx && !std::getenv("FSTAMD_NO_REC4") ? 4 : 0;
+    return rhs.rev.rrec4 && rhs.widx && !std::getenv("FSTAMD_NO_REC4")
+               ? (rhs.wt_n <= kPullWt ? 4 : 5)
+               : 0;
   if (rhs.rev.rrec4 && use_rec8(rhs.rev) && !std::getenv("FSTAMD_NO_REC4")) return 3;
   return use_rec8(rhs.rev) ? 2 : 1;
 }
 const void* pull_kernel_for(const DeviceFst& rhs, uint32_t max_len, bool log = false) {
   switch (route_rk("eager", pull_rk(rhs, max_len), rhs.rev, log)) {
     case 0: return pull_kernel_for<0>(rhs.rev);
+    case 5: return pull_kernel_for<5>(rhs.rev);
     case 4: return pull_kernel_for<4>(rhs.rev);
     case 3: return pull_kernel_for<3>(rhs.rev);
     case 2: return pull_kernel_for<2>(rhs.rev);
     default: return pull_kernel_for<1>(rhs.rev);
   }
 }
-// Lazy pull: 3 waves per SIMD with f64 cells (12.8 KB of LDS), 5 with f32 cells (7.4 KB;
-// round 3: 4 at 10.2 KB) when every distance is an integer below 2^24.
+// Lazy pull: 4 waves per SIMD with f64 cells (10.0 KB of LDS; round 5: 3 at 12.8 KB), 5
+// with f32 cells (7.4 KB; round 3: 4 at 10.2 KB) when every distance is an integer below
+// 2^24.
 #ifndef FSTAMD_LP_WAVES_F32  // A/B builds
 #define FSTAMD_LP_WAVES_F32 5
+#endif
+#ifndef FSTAMD_LP_WAVES_F64
+#define FSTAMD_LP_WAVES_F64 4
 #endif
 constexpr int kLazyPullWaves = 3;
 // B1: 1-B back records (DeviceFst::byte_back; the direct layout only)
 template <int KP, int RK>
 const void* lazy_pull_ptr(bool direct, bool b1) {
-  constexpr int wv = (RK && KP <= 5) ? FSTAMD_LP_WAVES_F32 : kLazyPullWaves;  // 8-record
-                                                                          // blocks spill at 4
+  constexpr int wv = KP > 5 ? kLazyPullWaves  // (8-record blocks spill at 4)
+                   : RK ? FSTAMD_LP_WAVES_F32 : FSTAMD_LP_WAVES_F64;
   if (!direct) return (const void*)lazy_pull_kernel<kPullRows, KP, false, wv, RK, false>;
   return b1 ? (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, RK, true>
             : (const void*)lazy_pull_kernel<kPullRows, KP, true, wv, RK, false>;
@@ -119,6 +128,7 @@ void free_reverse_mirror(DeviceFst* d) {
   d->rev = RevView{};
   d->pull_ok = false;
   d->widx = false;
+  d->wt_n = 0;
 }
 
 bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
@@ -304,10 +314,11 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   // weight} -- the source as an offset from the target (every arc stays within the rhs's
   // jump range), the key bits in the low half.  Padding: 0xFFFF0000 (an offset past every
   // window).  Only with the 8-B records' weights (integers <= 7) or the weight table's
-  // indices (< kPullWt), and offsets below 2^13.
-  // Weights that are not dyadic (0.1, ln 3): with at most kPullWt distinct values the 4-B
-  // records hold the value's index in a table instead (RK 4: tier P with f64 cells adds
-  // the table's f64 value, the very value the reference adds; FSTAMD_NO_WIDX: off)
+  // indices (< kPullWtMax), and offsets below 2^13.
+  // Weights that are not dyadic (0.1, ln 3): with at most kPullWtMax distinct values the
+  // 4-B records hold the value's index in a table instead (RK 4 up to kPullWt = 64 values,
+  // RK 5 up to 256: tier P with f64 cells adds the table's f64 value, the very value the
+  // reference adds; FSTAMD_NO_WIDX: off)
   std::vector<double> wtab;
   std::unordered_map<uint64_t, uint32_t> widx_of;
   if (d->int_wmax < 0.0 && !std::getenv("FSTAMD_NO_WIDX")) {
@@ -317,7 +328,7 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
       uint64_t bits;
       std::memcpy(&bits, &w, 8);
       if (widx_of.count(bits)) continue;
-      if (!(w >= 0.0) || !std::isfinite(w) || wtab.size() == kPullWt) ok = false;
+      if (!(w >= 0.0) || !std::isfinite(w) || wtab.size() == kPullWtMax) ok = false;
       else {
         widx_of.emplace(bits, (uint32_t)wtab.size());
         wtab.push_back(w);
@@ -373,11 +384,12 @@ bool build_reverse_mirror(DeviceFst* d, const FrozenFst& f) {
   }
   if (rrec4.empty()) wtab.clear();  // (the table serves the 4-B records only)
   if (!wtab.empty()) {  // appended to the records (rv_weight_table)
-    wtab.resize(kPullWt, 0.0);
+    d->wt_n = (uint32_t)wtab.size();
+    wtab.resize(kPullWtMax, 0.0);
     rrec4.resize((rrec4.size() + 1) & ~(size_t)1, 0xFFFF0000u);
     const size_t at = rrec4.size();
-    rrec4.resize(at + 2 * kPullWt);
-    std::memcpy(rrec4.data() + at, wtab.data(), kPullWt * sizeof(double));
+    rrec4.resize(at + 2 * kPullWtMax);
+    std::memcpy(rrec4.data() + at, wtab.data(), kPullWtMax * sizeof(double));
   }
   d->widx = !wtab.empty();
   auto up = [&](int i, const void* src_p, size_t bytes) -> bool {

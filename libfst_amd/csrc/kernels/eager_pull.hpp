@@ -72,7 +72,7 @@ __device__ __forceinline__ DT dist_min(DT a, DT b) {
 }
 
 
-template <int W, bool F32 = false>
+template <int W, bool F32 = false, int WT = kPullWt>
 struct PullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys rank << 3 | j < 8 W
   // the current layer's cells, slot W never holds a tuple.  Two arrays of 8-B entries
@@ -85,7 +85,7 @@ struct PullLds {
   unsigned long long best;
   uint32_t bestp;
   ChaseJob job[kChaseBatch];
-  double wt[kPullWt];              // RK 4: the rhs's distinct arc weights (rv_weight_table)
+  double wt[WT];                   // RK 4 / 5: the rhs's distinct arc weights (rv_weight_table)
 };
 // integer cells (every distance an integer below 2^24; round 3 kept them as f32, round 4 as
 // u32, whose add takes the 8-B record's weight byte as an SDWA operand): one 8-B cell
@@ -145,8 +145,8 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W>& S, const RevRec
 // weights (RK 4: weights that no power-of-two scale makes integers; the cells stay f64):
 // the source's offset as in the integer RK 3 below, the weight read from the LDS table --
 // the same f64 value the reference adds
-template <int W>
-__device__ __forceinline__ void pull_candidate(const PullLds<W, false>& S, const uint32_t& r,
+template <int W, int WT>
+__device__ __forceinline__ void pull_candidate(const PullLds<W, false, WT>& S, const uint32_t& r,
                                                uint32_t base8, uint32_t& pk, double& nd,
                                                uint32_t& rank_word) {
   const uint32_t off = min(base8 - (r >> 16), 8u * W);
@@ -154,7 +154,7 @@ __device__ __forceinline__ void pull_candidate(const PullLds<W, false>& S, const
   const uint32_t rw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S.rk) + FB(off, 8 * (W + 1), 151));
   pk = rw | (r & 0xFFFFu);
   rank_word = rw;
-  nd = d + S.wt[FB(r & (kPullWt - 1u), kPullWt, 149)];
+  nd = d + S.wt[FB(r & (WT - 1u), WT, 149)];
 }
 // The same on integer cells and the integer record copy {src, y, weight, olabel}: the
 // distances are integers below 2^24, so the u32 sum, min and compare equal the f64 ones.
@@ -247,8 +247,9 @@ __global__ void __launch_bounds__(64, WAVES_PER_EU)
 eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
                   unsigned int* next_item, EagerLaunch lp, BatchOutDev out) {
   constexpr int W = 64 * EW;
-  constexpr bool F32 = RK != 0 && RK != 4;
-  constexpr bool REC4 = RK == 3 || RK == 4;  // tier P's 4-B records (RK 4: f64 cells)
+  constexpr bool F32 = RK != 0 && RK != 4 && RK != 5;
+  constexpr bool REC4 = RK >= 3;  // tier P's 4-B records (RK 4 / 5: f64 cells)
+  constexpr int WT = RK == 5 ? (int)kPullWtMax : (int)kPullWt;  // weight-table entries
   using DT = typename std::conditional<F32, uint32_t, double>::type;  // (F32: integer cells)
   using RT = typename std::conditional<
       REC4, uint32_t,
@@ -259,10 +260,10 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
   constexpr uint32_t kRankShift = REC4 ? 16 : 20;
   constexpr uint32_t kFirstShift = kRankShift - 3;
   constexpr uint32_t kMShift = kFirstShift - 4;
-  constexpr int kWords = PullLds<W, F32>::kWords;
+  constexpr int kWords = PullLds<W, F32, WT>::kWords;
   static_assert(KP <= 16, "m is 4 bits of the key");
   static_assert(W < 512, "8 * slot is 12 bits of the key, ranks 9 bits");
-  __shared__ PullLds<W, F32> S;
+  __shared__ PullLds<W, F32, WT> S;
   const uint32_t lane = threadIdx.x;
   const DT kInf = dist_inf<DT>();
   // a cell: {distance, rank word}
@@ -319,8 +320,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         if constexpr (REC4) {
           const uint32_t r = rv.rrec4[b];
           out.out_ol[jb.o + k] = rv.rolab[b];
-          if constexpr (RK == 4)
-            out.out_w[jb.o + k] = rv_weight_table(rv)[r & (kPullWt - 1u)];  // the f64 weight
+          if constexpr (RK >= 4)
+            out.out_w[jb.o + k] = rv_weight_table(rv)[r & (WT - 1u)];  // the f64 weight
           else
             out.out_w[jb.o + k] = (double)(r & 0xFFu) * rv.winv;  // exact: the f64 weight
           tcur -= (uint32_t)(((int32_t)(r >> 16) - (int32_t)rv.rbias8) >> 3);  // the source
@@ -373,7 +374,8 @@ eager_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #pragma unroll 1
   for (uint32_t i = lane; i < (uint32_t)W + 1; i += 64) set_cell(i, kInf, kPullAbsent);
   if (lane < (uint32_t)kWords) S.bits[FB(lane, kWords, 157)] = 0;
-  if constexpr (RK == 4) S.wt[lane & (kPullWt - 1u)] = rv_weight_table(rv)[lane & (kPullWt - 1u)];
+  if constexpr (RK >= 4)
+    for (uint32_t i = lane; i < (uint32_t)WT; i += 64) S.wt[i] = rv_weight_table(rv)[i];
   wave_lds_sync();
   uint32_t wlast = 0;  // uniform: cells [wlast, W] hold no tuple
 

@@ -42,10 +42,10 @@ namespace fstamd {
 constexpr uint32_t kLpAbsent = 0xFFF00000u;  // rank words of a slot that holds no tuple
 constexpr uint32_t kLpRunMask = 0xFFFu;      // run (<= 4095 layers) below the pop rank
 constexpr uint32_t kLpMaxLen = 4095;
-// counting sort of the pop order: integer keys d - dmin below this (f64 cells: 256; f32
-// cells: 128, so that 5 waves' LDS fits a CU)
+// counting sort of the pop order: integer keys d - dmin below this (f32 cells: 128, so that
+// 5 waves' LDS fits a CU; f64 cells: 64, so that 4 do -- round 6, was 256 at 3 waves)
 template <typename DT>
-constexpr int lp_bins() { return sizeof(DT) == 4 ? 128 : 256; }
+constexpr int lp_bins() { return sizeof(DT) == 4 ? 128 : 64; }
 // f32 cells keep d - tb (the first toucher's distance) in 8 bits of the pop word: the lazy
 // pull takes f32 cells only when every arc weight is at most this
 constexpr double kLpF32WMax = 255.0;
@@ -124,8 +124,12 @@ struct LazyPullCells<W, uint32_t> {
 template <int W, typename DT>
 struct LazyPullLds {
   static constexpr int kWords = W * 8 / 64;  // first keys p << 3 | j < 8 W
+  // the sort buffers' entries: f64 cells keep slots (and counting keys < 64 above them) in
+  // 16 bits, their split sort reads its keys from the cells: 10.0 KB of LDS per wave, so 4
+  // waves per SIMD fit a CU (round 6; 32-bit entries and 256 bins were 12.8 KB, 3 waves)
+  using OrdT = typename std::conditional<sizeof(DT) == 4, uint32_t, uint16_t>::type;
   LazyPullCells<W, DT> c;
-  uint32_t ord0[W];                // (key << 9 |) slot in id order (f32 cells: first d)
+  OrdT ord0[W];                    // (key << 9 |) slot in id order (f32 cells: first d)
   // P1-P3 use {bits, pre}; the sorts (P4, after P3 read pre) overlay the split sort's
   // second buffer ord1 or the counting sort's {mask, hist} on them.  bits must be all zero
   // when P1 starts: the counting sort leaves mask zero, the split sort re-zeroes bits.
@@ -134,7 +138,7 @@ struct LazyPullLds {
       unsigned long long bits[kWords];
       uint4 pre[kWords];
     };
-    uint32_t ord1[W];              // split sort: the other buffer
+    OrdT ord1[W];                  // split sort: the other buffer
     struct {
       unsigned long long mask[lp_bins<DT>()];  // lanes of the current 64-chunk holding key b
       uint32_t hist[lp_bins<DT>()];            // running count of key b, then its prefix
@@ -726,7 +730,11 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
           mn = __ockl_wfred_min_f64(mn);
           mx = __ockl_wfred_max_f64(mx);
         }
-        const bool ik = __ballot(nonint) == 0 && (double)mx - (double)mn < 8388608.0;
+        // (f64 cells: integer keys only where the counting sort takes them -- their 16-bit
+        // sort entries hold key << 9 | slot for keys < 64; the split sort reads f64 bit
+        // patterns from the cells otherwise)
+        const bool ik = __ballot(nonint) == 0 &&
+                        (double)mx - (double)mn < (F32 ? 8388608.0 : (double)lp_bins<DT>());
         const unsigned long long mnb = (unsigned long long)__double_as_longlong((double)mn);
         uint32_t kacc = 0;            // OR of the integer keys
         unsigned long long diff = 0;  // OR of the f64 patterns' differences from dmin's
@@ -793,11 +801,15 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
             }
             wave_lds_sync();
           }
-          // exclusive prefix of the counts: lane l holds keys 4l .. 4l+3 (256 bins) or
-          // 2l, 2l+1 (128 bins, f32 cells) -- never past hist, which ends the union: the
-          // pending chase jobs follow it
-          static_assert(lp_bins<DT>() == 256 || lp_bins<DT>() == 128, "bins per lane");
-          if constexpr (lp_bins<DT>() == 256) {
+          // exclusive prefix of the counts: lane l holds keys 4l .. 4l+3 (256 bins), 2l,
+          // 2l+1 (128 bins, f32 cells) or l (64 bins, f64 cells) -- never past hist, which
+          // ends the union: the pending chase jobs follow it
+          static_assert(lp_bins<DT>() == 256 || lp_bins<DT>() == 128 || lp_bins<DT>() == 64,
+                        "bins per lane");
+          if constexpr (lp_bins<DT>() == 64) {
+            const uint32_t h = S.hist[FB(lane, lp_bins<DT>(), 142)];
+            S.hist[FB(lane, lp_bins<DT>(), 143)] = wave_incl_scan_dpp(h) - h;
+          } else if constexpr (lp_bins<DT>() == 256) {
             static_assert(4 * 64 == lp_bins<DT>(), "4 bins per lane cover hist exactly");
             const uint4 h = reinterpret_cast<const uint4*>(S.hist)[FB(lane, lp_bins<DT>() / 4, 132)];
             const uint32_t s4 = h.x + h.y + h.z + h.w;

@@ -278,6 +278,37 @@ def test_more_distinct_weights_than_the_table_holds(sem, monkeypatch, capfd):
 
 
 @pytest.mark.parametrize("sem", [EAGER, LAZY])
+@pytest.mark.parametrize("nw", [64, 65, 200, 256, 257])
+def test_wide_weight_tables(sem, nw, monkeypatch, capfd):
+    # nw distinct non-dyadic weights on the metric's chain (the direct layout): up to 64
+    # tier P's 4-B records index the 64-entry table (RK 4), up to 256 the 256-entry one
+    # (RK 5, round 6), beyond that the f64 records; the lazy pull reads its f64 records.
+    # Bit-exact with the oracle and with the f64 records (FSTAMD_NO_REC4)
+    monkeypatch.setenv("FSTAMD_ROUTE_LOG", "1")
+    vals = [0.1 + k / 7.0 for k in range(nw)]
+    T = 600
+    f = O.Fst()
+    for _ in range(T + 1):
+        f.add_state(0.0)
+    f.start = 0
+    for i in range(T + 1):
+        f.add_arc(i, 1, 1, vals[(5 * i) % nw], i)
+        for b in range(4):
+            f.add_arc(i, 1, ((i + b) % 255) + 1, vals[(5 * i + b + 1) % nw], min(i + b + 1, T))
+    blob = O.freeze(f)
+    assert len({w for al in f.arcs for (_, _, w, _) in al}) == nw
+    rng = np.random.default_rng(101 + nw)
+    seqs = [[1] * int(L) for L in rng.integers(0, 65, 300)] + [[1] * 64] * 8
+    capfd.readouterr()
+    check(blob, *csr(seqs), sem)
+    want = (4 if nw <= 64 else 5 if nw <= 256 else 0) if sem == EAGER else 0
+    assert routed_records(capfd.readouterr().err, sem) == {(want, 1.0)}
+    monkeypatch.setenv("FSTAMD_NO_REC4", "1")
+    check(blob, *csr(seqs), sem)
+    assert routed_records(capfd.readouterr().err, sem) == {(0, 1.0)}
+
+
+@pytest.mark.parametrize("sem", [EAGER, LAZY])
 def test_dyadic_weights_with_non_dyadic_finals(sem, monkeypatch, capfd):
     # the best final adds a final weight of 0.1 to the unscaled distance in f64, as the
     # reference does; ties between finals broken by id

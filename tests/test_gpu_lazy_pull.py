@@ -22,14 +22,20 @@ pytestmark = pytest.mark.gpu
 LAZY = F.FST_SEM_LAZY
 
 
-@pytest.fixture(params=["direct", "indirect"])
+@pytest.fixture(params=["direct", "indirect", "f64"])
 def only_lp(request, monkeypatch):
+    # f64: the f64-cell kernel (FSTAMD_LP_F64) on the direct layout -- 16-bit sort entries,
+    # a 64-bin counting sort and the split sort on f64 bit patterns (round 6)
     monkeypatch.setenv("FSTAMD_LAZY_ONLY_FIRST", "1")
     monkeypatch.delenv("FSTAMD_LAZY_ENGINE", raising=False)
     if request.param == "indirect":
         monkeypatch.setenv("FSTAMD_PULL_INDIRECT", "1")
     else:
         monkeypatch.delenv("FSTAMD_PULL_INDIRECT", raising=False)
+    if request.param == "f64":
+        monkeypatch.setenv("FSTAMD_LP_F64", "1")
+    else:
+        monkeypatch.delenv("FSTAMD_LP_F64", raising=False)
 
 
 def run_lp(blob, seqs, expect_all=True):
