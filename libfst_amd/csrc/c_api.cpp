@@ -1179,8 +1179,14 @@ FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const u
   const hipStream_t sA = EA.stream(), sB = EB ? EB.stream() : nullptr;
   DevBuf d_lab(std::max<uint64_t>(total, 1) * 4), d_off((num + 1) * 8ull),
       d_first(std::max<size_t>(num, 1) * 4ull), d_ctr(64 * 4);  // item counter per part
-  DevOut o(num, std::max<uint64_t>(total, 1));
+  DevOut o(num, total + 4);
   if (!d_lab.p || !d_off.p || !d_first.p || !d_ctr.p || !o.ok()) return FST_OOM;
+  // the arena's path arrays shifted so that each element shares its host twin's address
+  // modulo 16 (the copy-out's 16-B units, kernels/device_common.hpp copy_out_paths)
+  BatchOutDev vb = o.v;
+  vb.out_il += lbase & 3u;
+  vb.out_ol += lbase & 3u;
+  vb.out_w += lbase & 1u;
   struct SyncAll {  // every return: no kernel or copy still uses the buffers or the result
     hipStream_t s[3];
     ~SyncAll() {
@@ -1280,7 +1286,7 @@ FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const u
       }
       const uint32_t s0 = cut[p], np = cut[p + 1] - cut[p];
       ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p + s0, np, max_len};
-      BatchOutDev v = o.v;
+      BatchOutDev v = vb;
       v.status += s0;
       v.path_len += s0;
       v.path_off += s0;
@@ -1336,7 +1342,7 @@ FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const u
   if (handed) {
     later_lock.lock();
     ChainInput in{(const uint32_t*)d_lab.p, (const uint64_t*)d_off.p, num, max_len};
-    BatchOutDev v = o.v;
+    BatchOutDev v = vb;
     v.slots = (const uint64_t*)d_off.p;
     EA->set_after_pull(true);
     const hipError_t e = EA->run_chain(D, in, n, semantics, v, sA, nullptr);
@@ -1359,12 +1365,12 @@ FstError stream_shard(StreamShard& S, DeviceFst& D, const uint32_t* src, const u
       for (uint32_t i = 0; i < num && ok; ++i)
         if (st_out[i] == kPathOk && first[i] != kPathOk) {
           const uint64_t a = loff[i], L = loff[i + 1] - a;
-          ok = d2h(out->olabels + lbase + a, (uint32_t*)o.ol.p + a, L * 4) &&
-               d2h(out->weights + lbase + a, (double*)o.w.p + a, L * 8);
+          ok = d2h(out->olabels + lbase + a, vb.out_ol + a, L * 4) &&
+               d2h(out->weights + lbase + a, vb.out_w + a, L * 8);
         }
     } else {  // many: the whole arena (every pull-tier chase writes its path there too)
-      ok = d2h(out->olabels + lbase, o.ol.p, total * 4) &&
-           d2h(out->weights + lbase, o.w.p, total * 8);
+      ok = d2h(out->olabels + lbase, vb.out_ol, total * 4) &&
+           d2h(out->weights + lbase, vb.out_w, total * 8);
     }
     if (!ok || hipStreamSynchronize(sA) != hipSuccess) return FST_OOM;
   }

@@ -68,28 +68,73 @@ __device__ __forceinline__ unsigned long long reserve_path(const BatchOutDev& ou
 // wave's vector memory operations go through one L1 in order).  Round 5 first used an
 // agent-scope acquire here -- s_waitcnt vmcnt(0) + buffer_inv sc1 per chase, a cache
 // invalidate every 16 strings on every wave.
+// Round 6, measured and not kept (FSTAMD_COPYOUT_WIDE builds): 16-B units.  A string's
+// olabels and weights (L = 64: 256 + 512 B) went out as 16-B lane stores -- 48 lanes, one
+// load and one store instruction per string -- instead of 4- and 8-B lane stores.  The
+// copy-out holds the pull tier back by ~1 ms per part of the streamed batch (its trace with
+// and without it): device-initiated writes over PCIe run at ~30 GB/s.  The
+// wide stores were slower still (A/B on one box, 1M metric strings through the host entry:
+// 31.0-31.3 vs 29.9-30.4 ms, profiles/r06/ab_copyout_wide.txt).  The head and tail elements
+// before / after the 16-B aligned middle go out one element per lane in the same pass; the
+// device arena and the host result share each element's address modulo 16 (run_streamed
+// shifts the arena's base pointers to match the shard's first label).
+#ifdef FSTAMD_COPYOUT_WIDE
 __device__ __forceinline__ void copy_out_paths(const BatchOutDev& out, uint32_t njobs,
                                                uint64_t my_o, uint32_t my_L, uint32_t lane) {
-#ifdef FSTAMD_COPYOUT_AGENT  // A/B builds: round 5's first fence
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#else
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-#endif
+  for (uint32_t j = 0; j < njobs; ++j) {  // uniform
+    const uint32_t Lj = __builtin_amdgcn_readlane(my_L, j);
+    const uint64_t oj = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_o >> 32), j) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((uint32_t)my_o, j);
+    const uint32_t* dol = out.out_ol + oj;
+    uint32_t* hol = out.host_ol + oj;
+    const double* dw = out.out_w + oj;
+    double* hw = out.host_w + oj;
+    // olabels: ha head elements, nq 16-B units, then the tail; weights: hb, nw, tail
+    const uint32_t ha = min(Lj, (4u - (uint32_t)(((uintptr_t)hol >> 2) & 3u)) & 3u);
+    const uint32_t nq = (Lj - ha) >> 2, ta = Lj - ha - 4 * nq;
+    const uint32_t hb = min(Lj, (uint32_t)(((uintptr_t)hw >> 3) & 1u));
+    const uint32_t nw = (Lj - hb) >> 1, tb = Lj - hb - 2 * nw;
+    const uint32_t units = nq + nw + ha + ta + hb + tb;
+    for (uint32_t u = lane; u < units; u += 64) {
+      if (u < nq) {
+        *reinterpret_cast<u32x4*>(hol + ha + 4 * u) =
+            *reinterpret_cast<const u32x4*>(dol + ha + 4 * u);
+      } else if (u < nq + nw) {
+        const uint32_t v = u - nq;
+        *reinterpret_cast<u32x4*>(hw + hb + 2 * v) =
+            *reinterpret_cast<const u32x4*>(dw + hb + 2 * v);
+      } else {  // single elements: olabel head, olabel tail, weight head, weight tail
+        uint32_t r = u - nq - nw;
+        if (r < ha) {
+          hol[r] = dol[r];
+        } else if ((r -= ha) < ta) {
+          hol[ha + 4 * nq + r] = dol[ha + 4 * nq + r];
+        } else if ((r -= ta) < hb) {
+          hw[0] = dw[0];
+        } else {
+          hw[hb + 2 * nw] = dw[hb + 2 * nw];
+        }
+      }
+    }
+  }
+}
+#else
+__device__ __forceinline__ void copy_out_paths(const BatchOutDev& out, uint32_t njobs,
+                                               uint64_t my_o, uint32_t my_L, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   for (uint32_t j = 0; j < njobs; ++j) {  // uniform
     const uint32_t Lj = __builtin_amdgcn_readlane(my_L, j);
     const uint64_t oj = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_o >> 32), j) << 32) |
                         (uint32_t)__builtin_amdgcn_readlane((uint32_t)my_o, j);
     for (uint32_t x = lane; x < Lj; x += 64) {
-#ifdef FSTAMD_COPYOUT_PLAIN  // A/B builds
-      out.host_ol[oj + x] = out.out_ol[oj + x];
-      out.host_w[oj + x] = out.out_w[oj + x];
-#else
       __builtin_nontemporal_store(out.out_ol[oj + x], out.host_ol + oj + x);
       __builtin_nontemporal_store(out.out_w[oj + x], out.host_w + oj + x);
-#endif
     }
   }
 }
+#endif
 
 // Fst.arcsByIlabel (src/fst.zig:112-136): global arc range [lo, hi) of the arcs of
 // state `s` whose ilabel == label.  Spans of <= 8 arcs are counted with independent
