@@ -522,7 +522,9 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
 #elif defined(FSTAMD_LP_FULLCERT)  // A/B: the full loop on every row that needs it
         if (check_c && __ballot(pres && (!(c & kRevPos) || nb > 1))) {
 #else
-        if (check_c && lanes_without(pres, c, pwb, ckx, fast)) {
+        uint32_t ff2 = ff;  // (a fresh compare for the ballot, as in P3 below)
+        asm volatile("" : "+v"(ff2));
+        if (check_c && lanes_without(ff2 < kLpAbsent, c, pwb, ckx, fast)) {
 #endif
 #ifdef FSTAMD_LP_FULLCERT
           bool cert = !pres || (c & kRevPos);
@@ -614,7 +616,11 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
       for (int e = 0; e < EW; ++e) {
         if ((uint32_t)e >= rows_w) continue;
         const uint32_t i = (uint32_t)e * 64 + lane;
-        const bool pres = (uint32_t)e < rows_n && fst[e] < kLpAbsent;
+        // a fresh compare (rows past rows_n keep fst = kEmptyKey): P1's mask, kept across P2,
+        // came back as a select and a compare per row (round 6: 43.0 -> 42.4 ms, A/B)
+        uint32_t fe = fst[e];
+        asm volatile("" : "+v"(fe));
+        const bool pres = fe < kLpAbsent;
         uint32_t rank = 0;
         if ((uint32_t)e < rows_n) {
           const uint32_t key = pres ? fst[e] >> 17 : 0u;
@@ -679,6 +685,8 @@ lazy_pull_kernel(RhsView rhs, RevView rv, ChainInput in, uint32_t n_best,
         // already in order (the metric's layers, every one of them): the id order is the
         // pop order and the identity ranks written in P3 stand; nothing below runs (no
         // reductions, no keys: the check compares the cells' distances in id order)
+        // (round 6: the check as SALU ORs of per-row ballots with a uniform lane bound
+        // measured 42.45 vs 42.37 ms, not kept)
         bool unsorted = false;
 #pragma unroll
         for (int e = 0; e < EW; ++e) {

@@ -6,10 +6,11 @@ set -e
 cd "$(dirname "$0")/../libfst_amd/csrc"
 make -s -j8
 name=$1; defs=$2
-mkdir -p ../variants build_var
+vdir=${VARIANT_DIR:-../variants}
+mkdir -p $vdir build_var
 HIPCC=/opt/rocm/bin/hipcc
 $HIPCC -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=off $defs --offload-arch=gfx950 \
   -c eager_pull.hip -o build_var/$name.o
-$HIPCC -shared -fPIC --offload-arch=gfx950 -o ../variants/$name.so \
+$HIPCC -shared -fPIC --offload-arch=gfx950 -o $vdir/$name.so \
   build/host_fst.cpp.o build/c_api.cpp.o build/device_engine.hip.o build_var/$name.o
-echo "built libfst_amd/variants/$name.so ($defs)"
+echo "built $vdir/$name.so ($defs)"
