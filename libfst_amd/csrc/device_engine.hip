@@ -15,6 +15,7 @@
 
 #include "host_fst.hpp"
 #include "kernels/eager_bfs.hpp"
+#include "kernels/eager_tiny.hpp"
 #include "kernels/lazy_dense.hpp"
 #include "kernels/lazy_band.hpp"
 #include "kernels/lazy_layered.hpp"
@@ -1437,6 +1438,17 @@ int lazy_tiny_per_cu() {  // resident LDS-replay waves per CU, asked of the runt
   }();
   return occ;
 }
+template <int N>
+int ctiny_per_cu() {
+  static const int occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void*)eager_tiny_kernel<N>, 64,
+                                                     0) != hipSuccess)
+      o = 1;
+    return std::max(o, 1);
+  }();
+  return occ;
+}
 }  // namespace
 
 hipError_t DeviceEngine::run_lazy_tiny(const DeviceFst& rhs, const ChainInput& in, uint32_t n,
@@ -2000,6 +2012,12 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
                     ((uint64_t)(in.max_len + 1) * rhs.view.num_states <= 16384 ||
                      rhs.skip_tiny_eager.load(std::memory_order_relaxed) == 0);
   const uint32_t count0 = count;
+  // Eager semantics on an rhs a one-word tuple key can name: the compact tiny tiers
+  // (kernels/eager_tiny.hpp, ~63 B per tuple instead of ~110: 18 / 9 workgroups per CU
+  // instead of 10 / 5).  FSTAMD_EAGER_CTINY=0 keeps eager_bfs_kernel's (A/B runs, tests).
+  const char* cte = std::getenv("FSTAMD_EAGER_CTINY");
+  const bool compact = tiny && !lazy && !(cte && std::strcmp(cte, "0") == 0) &&
+                       rhs.view.num_states < kCtMaxStates && rhs.view.num_arcs < kCtPhase3;
   // tier -2: the 128-tuple tiny size, tier -1: the 256-tuple one, then the HBM tiers.
   // The 128-tuple size is skipped on an rhs where it handed on over a third of an earlier
   // batch (DeviceFst::tiny_eager_256); FSTAMD_BFS_TINY_START=1|2 forces the first size.
@@ -2015,7 +2033,9 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     // barriers, 4x the strings in flight); FSTAMD_BFS_WG0=256 for A/B runs
     const char* wge = std::getenv("FSTAMD_BFS_WG0");
     const bool wave = tier == 0 && !(wge && std::strcmp(wge, "256") == 0);
-    const uint64_t per_cu = tier < 0 ? (uint64_t)(tier == -2 ? tiny_per_cu<1>() : tiny_per_cu<2>())
+    const uint64_t per_cu = tier < 0 ? (uint64_t)(compact ? (tier == -2 ? ctiny_per_cu<128>()
+                                                                        : ctiny_per_cu<256>())
+                                                 : tier == -2 ? tiny_per_cu<1>() : tiny_per_cu<2>())
                             : tier == 0 ? (wave ? 4 * FSTAMD_BFS_WAVES64 : kBfsWgPerCu0) : 1;
     const uint32_t grid =
         (uint32_t)std::min<uint64_t>({(uint64_t)count, (uint64_t)num_cus_ * per_cu, fit});
@@ -2041,7 +2061,14 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
     if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)grid * 64, stream));
     HIP_TRY(hipMemsetAsync(cnt + 1, 0, 8, stream));  // item counter + next list count
     GraphInput none{};
-    if (tier == -2)
+    if (tier < 0 && compact) {
+      if (tier == -2)
+        eager_tiny_kernel<128><<<grid, 64, 0, stream>>>(rhs.view, in, n, cnt + 1, list, cnt,
+                                                        ws.wd_ticks, out);
+      else
+        eager_tiny_kernel<256><<<grid, 64, 0, stream>>>(rhs.view, in, n, cnt + 1, list, cnt,
+                                                        ws.wd_ticks, out);
+    } else if (tier == -2)
       eager_bfs_kernel<64, false, 1><<<grid, 64, 0, stream>>>(rhs.view, in, none, n, cnt + 1,
                                                               list, cnt, 0, ws, out);
     else if (tier == -1)

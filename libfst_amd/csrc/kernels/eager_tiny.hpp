@@ -1,0 +1,432 @@
+// eager_tiny.hpp -- the compact LDS tier of the general engine's chain batch: eager
+// semantics (compose, src/ops/compose.zig:29-198, then shortestPath,
+// src/ops/shortest-path.zig:18-139) on lattices of up to 128 / 256 tuples, one wavefront
+// per string, every table in LDS.
+//
+// Same algorithm and same answers as eager_bfs_kernel's tiny tiers (kernels/eager_bfs.hpp:
+// level-synchronous BFS with ids in first-candidate order, the least fixpoint by sweeps
+// over the levels when an arc goes backwards, back-pointer = tight in-arc with the
+// smallest (source id, arc index), best final = lexmin (total, id)); only the tables are
+// narrower, because the utterances of a WeText-scale tagger (~140 tuples, 95 % under 256)
+// are latency-bound and their workgroups per CU were set by LDS: eager_bfs_kernel<64,
+// false, 2> holds ~110 B per tuple (28 KB at 256 tuples, 5 per CU); this one ~63 B
+// (16 KB, 9 per CU; 8.6 KB and 18 per CU at 128):
+//   - a tuple key is one word, (s2 << 9) | (s1 << 2) | filter: the lhs is a chain of at
+//     most 126 labels (s1 < 128) and the host sends only an rhs of fewer than 2^23 states;
+//   - ids, arc offsets and levels are 16-bit; a back-pointer is (source << 16) | arc index;
+//   - an arc keeps its weight (f64, relaxed every level) and a code for its labels (the rhs
+//     arc, flagged when it is phase 3's rhs-epsilon-alone arc, or kCtPhase2): ilabels and
+//     olabels are read back from the lhs labels and the rhs records for the path's arcs only;
+//   - final weights are recomputed for the tuples with s1 = L instead of being stored.
+#pragma once
+
+#include "eager_bfs.hpp"
+
+namespace fstamd {
+
+constexpr uint32_t kCtPhase2 = 0xFFFFFFFFu;  // arc code: the lhs epsilon-output arc alone
+constexpr uint32_t kCtPhase3 = 0x80000000u;  // arc code flag: the rhs epsilon-input arc alone
+constexpr uint32_t kCtLab = 128;             // lhs labels held in LDS (chains of <= 126)
+constexpr uint32_t kCtMaxStates = 1u << 23;  // rhs states a one-word key can name
+
+__host__ __device__ constexpr int ct_waves(int n) { return n <= 128 ? 5 : 3; }  // per SIMD
+
+__device__ __forceinline__ uint32_t ct_key(uint32_t s1, uint32_t s2, uint32_t f) {
+  return (s2 << 9) | (s1 << 2) | f;
+}
+__device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
+  k ^= k >> 16;
+  k *= 0x7feb352du;
+  k ^= k >> 15;
+  return k;
+}
+
+// bfs_expand (eager_bfs.hpp) for a chain lhs (label lab[s1] on arc s1 -> s1 + 1, weight One):
+// the same candidates in the same order, each as emit(code, weight, target key).
+template <class Emit>
+__device__ __forceinline__ void ct_expand(const RhsView& rhs, const uint32_t* lab, uint32_t L,
+                                          uint32_t s1, uint32_t s2, uint32_t f, Emit&& emit) {
+  const bool arc = s1 < L;
+  const uint32_t c = arc ? lab[s1] : 0u;
+  if (arc && c != kEpsilon) {  // phase 1 (compose.zig:95-121)
+    uint32_t lo, cnt;
+    span_summary<false>(rhs, s2, c, lo, cnt);
+    for (uint32_t a = lo; a < lo + cnt; ++a) {
+      const ArcRec r = rhs.rec[a];
+      emit(a, w_times(w_one(), r.weight), ct_key(s1 + 1, r.next, 0));
+    }
+  }
+  if (f != 1 && arc && c == kEpsilon)  // phase 2 (:124-134)
+    emit(kCtPhase2, w_one(), ct_key(s1 + 1, s2, f == 0 ? 2u : f));
+  uint32_t elo, ecnt;
+  span_summary<false>(rhs, s2, kEpsilon, elo, ecnt);
+  if (f != 2) {  // phase 3 (:136-157)
+    const uint32_t nf = f == 0 ? 1u : f;
+    for (uint32_t a = elo; a < elo + ecnt; ++a) {
+      const ArcRec r = rhs.rec[a];
+      emit(a | kCtPhase3, r.weight, ct_key(s1, r.next, nf));
+    }
+  }
+  if (f == 0 && ecnt && arc && c == kEpsilon) {  // phase 4 (:160-194)
+    for (uint32_t a = elo; a < elo + ecnt; ++a) {
+      const ArcRec r = rhs.rec[a];
+      emit(a, w_times(w_one(), r.weight), ct_key(s1 + 1, r.next, 0));
+    }
+  }
+}
+
+struct CtShared {
+  uint32_t item;
+  uint32_t flag;
+  uint32_t changed;
+  uint32_t bestid;
+  unsigned long long t_item;
+  unsigned long long best;
+  unsigned long long path_o;  // the path's arena offset (thread 0 -> the wave)
+  uint32_t hops;
+  int32_t verdict;            // kPathOk: write the path; else the status to report
+};
+
+// Final weight of tuple key k (compose.zig:69-74 with the chain's final(L) = One).
+__device__ __forceinline__ double ct_final(const RhsView& rhs, uint32_t k, uint32_t L) {
+  if (((k >> 2) & 127u) != L) return w_zero();
+  const double fw1 = w_one(), fw2 = rhs.final_w[k >> 9];
+  return (!w_is_zero(fw1) && !w_is_zero(fw2)) ? w_times(fw1, fw2) : w_zero();
+}
+
+template <int kN>
+__global__ void __launch_bounds__(64, ct_waves(kN))
+eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
+                  const uint32_t* items, const uint32_t* num_items_dev,
+                  unsigned long long wd_ticks, BatchOutDev out) {
+  constexpr uint32_t N = kN, A = kN * 3 / 2, H = 2 * kN, HM = H - 1;
+  static_assert((H & HM) == 0 && N <= 256 && A < 65536, "16-bit ids and offsets");
+  __shared__ CtShared SH;
+  __shared__ uint32_t hkey[H], hval[H], nkey[N], nback[N], acode[A], cslot[A], lab[kCtLab];
+  __shared__ unsigned long long nd[N];
+  __shared__ double aw[A];
+  __shared__ uint16_t aoff[N + 2], lvl[N + 2], anext[A];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t num_items = *num_items_dev;
+
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) {
+      SH.item = atomicAdd(next_item, 1u);
+      SH.t_item = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+    const uint32_t item = SH.item;
+    if (item >= num_items) break;
+    const unsigned long long t0 = SH.t_item;  // per-string watchdog, as eager_bfs_kernel
+    const uint32_t si = items[item];
+    const uint64_t off = in.offsets[si];
+    const uint32_t L = (uint32_t)(in.offsets[si + 1] - off);
+    if (L + 2 > kCtLab) {
+      if (tid == 0) write_status(out, si, kPathOverflow, 0, 0);
+      continue;
+    }
+    for (uint32_t i = tid; i < L; i += 64) lab[i] = in.labels[off + i];
+    if (rhs.start == kNoState || n_best != 1) {  // shortest-path.zig:21-24
+      if (tid == 0)
+        write_status(out, si, (rhs.start == kNoState || n_best == 0) ? kPathEmpty : kPathErrorN,
+                     0, 0);
+      continue;
+    }
+
+    // ---- compose: level-synchronous BFS (eager_bfs_kernel's phases A-E) ----
+    for (uint32_t i = tid; i < H; i += 64) {
+      hkey[i] = kEmptyKey;
+      hval[i] = ~0u;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t k0 = ct_key(0, rhs.start, 0), h = ct_hash(k0) & HM;
+      hkey[h] = k0;
+      hval[h] = 0;
+      nkey[0] = k0;
+      nd[0] = okey(w_one());
+      lvl[0] = 0;
+      lvl[1] = 1;
+      aoff[0] = 0;
+      SH.changed = 0;
+    }
+    __syncthreads();
+    uint32_t n_nodes = 1, n_arcs = 0, level = 0;
+    int32_t fail = kPathOk;
+    while (true) {
+      const uint32_t f0 = level == 0 ? 0u : lvl[level];
+      const uint32_t f1 = n_nodes;
+      if (f0 >= f1) break;
+      // (A) candidate counts -> arc offsets (written only while they fit: 16-bit)
+      uint32_t carry = 0;
+      for (uint32_t b = f0; b < f1; b += 64) {
+        const uint32_t p = b + tid;
+        uint32_t cnt = 0;
+        if (p < f1) {
+          const uint32_t k = nkey[p];
+          ct_expand(rhs, lab, L, (k >> 2) & 127u, k >> 9, k & 3u,
+                    [&](uint32_t, double, uint32_t) { ++cnt; });
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<64>(cnt, nullptr, tot);
+        if (p < f1 && n_arcs + carry + ex <= A) aoff[p] = (uint16_t)(n_arcs + carry + ex);
+        carry += tot;
+      }
+      if ((uint64_t)n_arcs + carry > A) {
+        fail = kPathOverflow;
+        break;
+      }
+      if (tid == 0) {
+        aoff[f1] = (uint16_t)(n_arcs + carry);
+        SH.flag = 0;
+      }
+      __syncthreads();
+      // (B) the level's arcs, then every candidate's target into the hash (the first
+      // candidate of a new key keeps the smallest arc index)
+      const uint32_t c0 = n_arcs, c1 = n_arcs + carry;
+      for (uint32_t p = f0 + tid; p < f1; p += 64) {
+        const uint32_t k = nkey[p];
+        uint32_t a = aoff[p];
+        ct_expand(rhs, lab, L, (k >> 2) & 127u, k >> 9, k & 3u,
+                  [&](uint32_t code, double w, uint32_t key) {
+                    acode[a] = code;
+                    aw[a] = w;
+                    cslot[a] = key;
+                    ++a;
+                  });
+      }
+      __syncthreads();
+      for (uint32_t a = c0 + tid; a < c1; a += 64) {
+        const uint32_t key = cslot[a];
+        uint32_t h = ct_hash(key) & HM, slot = kEmptyKey;
+        for (uint32_t probe = 0; probe <= HM; ++probe) {
+          const uint32_t old = atomicCAS(&hkey[h], kEmptyKey, key);
+          if (old == kEmptyKey || old == key) {
+            slot = h;
+            break;
+          }
+          h = (h + 1) & HM;
+        }
+        if (slot == kEmptyKey) SH.flag = 1;
+        else atomicMin(&hval[slot], 0x80000000u | a);
+        cslot[a] = slot;
+      }
+      __syncthreads();
+      if (SH.flag) {
+        fail = kPathOverflow;
+        break;
+      }
+      // (C) ids of first occurrences, in candidate order (4 candidates per lane per round)
+      constexpr uint32_t K = 4;
+      uint32_t newc = 0;
+      for (uint32_t b = c0; b < c1; b += 64 * K) {
+        const uint32_t a0 = b + tid * K;
+        uint32_t nf = 0, slots[K];
+        bool first[K];
+#pragma unroll
+        for (uint32_t q = 0; q < K; ++q) {
+          const uint32_t a = a0 + q;
+          slots[q] = a < c1 ? cslot[a] : 0u;
+          first[q] = a < c1 && hval[slots[q]] == (0x80000000u | a);
+          nf += first[q] ? 1u : 0u;
+        }
+        uint32_t tot;
+        uint32_t rank = block_excl_scan<64>(nf, nullptr, tot);
+        if (n_nodes + newc + tot <= N) {
+#pragma unroll
+          for (uint32_t q = 0; q < K; ++q) {
+            if (first[q]) {
+              const uint32_t id = n_nodes + newc + rank++;
+              hval[slots[q]] = id;
+              nkey[id] = hkey[slots[q]];
+              nd[id] = okey(w_zero());
+            }
+          }
+        }
+        newc += tot;
+        if (n_nodes + newc > N) break;
+      }
+      __syncthreads();
+      if (n_nodes + newc > N) {
+        fail = kPathOverflow;
+        break;
+      }
+      // (D) arc targets; (E) relax the level's arcs in level order (a backward arc leaves
+      // the rest to the fixpoint sweeps)
+      for (uint32_t a = c0 + tid; a < c1; a += 64) anext[a] = (uint16_t)hval[cslot[a]];
+      __syncthreads();
+      bool back = false;
+      for (uint32_t p = f0 + tid; p < f1; p += 64) {
+        const double ds = from_okey(nd[p]);
+        const uint32_t a1 = aoff[p + 1];
+        for (uint32_t a = aoff[p]; a < a1; ++a) {
+          const uint32_t x = anext[a];
+          back |= x < f1;
+          if (!w_is_zero(ds)) atomicMin(&nd[x], okey(w_times(ds, aw[a])));
+        }
+      }
+      if (back) SH.changed = 1;
+      n_arcs = c1;
+      n_nodes += newc;
+      ++level;
+      if (tid == 0) lvl[level + 1] = (uint16_t)n_nodes;
+      __syncthreads();
+      if ((level & 7u) == 0) {  // the watchdog every 8 levels
+        if (__builtin_amdgcn_s_memrealtime() - t0 > wd_ticks) {
+          if (tid == 0) SH.flag = 1;
+        }
+        __syncthreads();
+        if (SH.flag) {
+          fail = kPathInternal;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (fail != kPathOk) {
+      if (tid == 0) write_status(out, si, fail, n_nodes, n_arcs);
+      continue;
+    }
+    const uint32_t n_levels = level;
+    const bool dag = SH.changed == 0;
+    const unsigned long long deadline = t0 + wd_ticks;
+
+    // ---- shortestPath: the least fixpoint (bfs_fixpoint), nd already holds path sums ----
+    for (uint32_t i = tid; i < n_nodes; i += 64) nback[i] = ~0u;
+    __syncthreads();
+    bool ok = true;
+    if (!dag) {
+      for (uint32_t sweep = 0;; ++sweep) {
+        if (tid == 0) SH.changed = 0;
+        __syncthreads();
+        for (uint32_t l = 0; l < n_levels; ++l) {
+          const uint32_t b0 = lvl[l], b1 = lvl[l + 1];
+          for (uint32_t s = b0 + tid; s < b1; s += 64) {
+            const double ds = from_okey(nd[s]);
+            if (w_is_zero(ds)) continue;
+            for (uint32_t a = aoff[s]; a < aoff[s + 1]; ++a) {
+              const unsigned long long v = okey(w_times(ds, aw[a]));  // shortest-path.zig:72
+              const unsigned long long old = atomicMin(&nd[anext[a]], v);
+              if (v < old) SH.changed = 1;
+            }
+          }
+          __syncthreads();
+        }
+        if (tid == 0) SH.flag = __builtin_amdgcn_s_memrealtime() > deadline;
+        __syncthreads();
+        const bool changed = SH.changed != 0, expired = SH.flag != 0;
+        __syncthreads();
+        if (!changed) break;
+        if (expired || sweep > n_nodes) {  // sweep > n_nodes: impossible for w >= 0
+          ok = false;
+          break;
+        }
+      }
+    }
+    if (!ok) {
+      if (tid == 0) write_status(out, si, kPathInternal, n_nodes, n_arcs);
+      continue;
+    }
+    // back-pointers: the tight in-arc with the smallest (source, arc index)
+    for (uint32_t s = tid; s < n_nodes; s += 64) {
+      const double ds = from_okey(nd[s]);
+      if (w_is_zero(ds)) continue;
+      const uint32_t a0 = aoff[s], a1 = aoff[s + 1];
+      for (uint32_t a = a0; a < a1; ++a) {
+        const uint32_t x = anext[a];
+        if (okey(w_times(ds, aw[a])) == nd[x]) atomicMin(&nback[x], (s << 16) | (a - a0));
+      }
+    }
+    // best final: lexmin (total, id)
+    if (tid == 0) {
+      SH.best = kMaxU64;
+      SH.bestid = kEmptyKey;
+    }
+    __syncthreads();
+    unsigned long long mk = kMaxU64;
+    uint32_t mid = kEmptyKey;
+    for (uint32_t s = tid; s < n_nodes; s += 64) {
+      const double ds = from_okey(nd[s]);
+      const double fw = ct_final(rhs, nkey[s], L);
+      if (w_is_zero(ds) || w_is_zero(fw)) continue;
+      const unsigned long long k = okey(w_times(ds, fw));
+      if (k < mk) {  // s ascending per lane: equal keys keep the smaller id
+        mk = k;
+        mid = s;
+      }
+    }
+    if (mk != kMaxU64) atomicMin(&SH.best, mk);
+    __syncthreads();
+    if (mk != kMaxU64 && mk == SH.best) atomicMin(&SH.bestid, mid);
+    __syncthreads();
+    // backtrace: thread 0 walks the back-pointers in LDS (bounded: a cycle reports CYCLE)
+    // and parks the path's (source, arc) pairs in anext / cslot; the wave then writes the
+    // arcs, reading their olabels from the rhs records in parallel
+    const uint32_t best = SH.bestid;
+    if (tid == 0) {
+      int32_t verdict = kPathOk;
+      uint32_t hops = 0;
+      if (best == kEmptyKey) {
+        verdict = kPathEmpty;
+      } else {
+        uint32_t cur = best;
+        for (;;) {
+          const uint32_t b = nback[cur];
+          if (b == ~0u) break;
+          if (++hops > n_nodes) {
+            verdict = kPathCycle;
+            break;
+          }
+          cur = b >> 16;
+        }
+        if (verdict == kPathOk && cur != 0u) verdict = kPathEmpty;  // shortest-path.zig:120-122
+      }
+      if (verdict == kPathOk) {
+        const unsigned long long o = reserve_path(out, si, hops);
+        if (o + hops > out.arc_cap) {
+          verdict = kPathOutputFull;
+        } else {
+          uint32_t cur = best;
+          for (uint32_t k = hops; k > 0; --k) {
+            const uint32_t b = nback[cur], s = b >> 16;
+            anext[k - 1] = (uint16_t)s;
+            cslot[k - 1] = aoff[s] + (b & 0xFFFFu);
+            cur = s;
+          }
+          SH.path_o = o;
+        }
+      }
+      SH.hops = hops;
+      SH.verdict = verdict;
+    }
+    __syncthreads();
+    const int32_t verdict = SH.verdict;
+    if (verdict != kPathOk) {
+      if (tid == 0) write_status(out, si, verdict, n_nodes, n_arcs);
+      continue;
+    }
+    const uint32_t hops = SH.hops;
+    const unsigned long long o = SH.path_o;
+    for (uint32_t k = tid; k < hops; k += 64) {
+      const uint32_t a = cslot[k], code = acode[a];
+      const uint32_t s1 = (nkey[anext[k]] >> 2) & 127u;
+      const bool ph2 = code == kCtPhase2, ph3 = !ph2 && (code & kCtPhase3) != 0u;
+      out.out_il[o + k] = ph3 ? kEpsilon : lab[s1];
+      out.out_ol[o + k] = ph2 ? kEpsilon : rhs.rec[code & ~kCtPhase3].olabel;
+      out.out_w[o + k] = aw[a];
+    }
+    if (tid == 0) {
+      out.status[si] = kPathOk;
+      out.path_len[si] = hops;
+      out.path_off[si] = o;
+      out.final_w[si] = ct_final(rhs, nkey[best], L);
+      if (out.work) {
+        out.work[2 * si] = n_nodes;
+        out.work[2 * si + 1] = n_arcs;
+      }
+    }
+  }
+}
+
+}  // namespace fstamd

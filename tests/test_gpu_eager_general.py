@@ -245,32 +245,40 @@ def test_batch_eager_negative_weights(seed):
     assert F.last_launch_stats().engine == 6
 
 
-@pytest.mark.parametrize("sem", ["eager", "lazy_rounds"])
+@pytest.mark.parametrize("sem", ["eager", "eager_256", "eager_wide", "lazy_rounds"])
 @pytest.mark.parametrize("seed", range(6))
 def test_batch_tiny_tier_mixed_sizes(monkeypatch, sem, seed):
-    # the general engine's tiny tier (tables and labels in LDS: eager_bfs.hpp kTiny*) takes
-    # the short strings; strings past its label / node / arc caps report OVERFLOW there and
-    # finish in the HBM tiers.  Bit-exact against the oracle, for both semantics (lazy
-    # through the general rounds engine)
+    # the general engine's tiny tiers (tables and labels in LDS) take the short strings;
+    # strings past their label / node / arc / hash caps report OVERFLOW there and finish in
+    # the HBM tiers.  Bit-exact against the oracle, for both semantics (lazy through the
+    # general rounds engine).  Eager: the compact tables (eager_tiny.hpp) from 128 tuples,
+    # from 256 (FSTAMD_BFS_TINY_START=2), and eager_bfs.hpp's kTiny tables
+    # (FSTAMD_EAGER_CTINY=0)
     if sem == "lazy_rounds":
         monkeypatch.setenv("FSTAMD_LAZY_ENGINE", "rounds")
+    if sem == "eager_256":
+        monkeypatch.setenv("FSTAMD_BFS_TINY_START", "2")
+    if sem == "eager_wide":
+        monkeypatch.setenv("FSTAMD_EAGER_CTINY", "0")
     rng = np.random.default_rng(8100 + seed)
     f = random_rhs(rng, int(rng.integers(3, 24)), int(rng.integers(8, 80)), 4, eps=True,
                    frac=seed % 2 == 1)
     blob = O.freeze(f)
     lens = [int(x) for x in rng.integers(0, 24, 56)] + [100, 125, 126, 127, 140, 60, 90, 33]
     seqs = [[int(x) for x in rng.integers(1 if i % 5 else 0, 5, L)] for i, L in enumerate(lens)]
-    check(blob, *csr(seqs), EAGER if sem == "eager" else LAZY)
+    check(blob, *csr(seqs), LAZY if sem == "lazy_rounds" else EAGER)
 
 
-def test_batch_tiny_tier_off_matches(monkeypatch):
-    # FSTAMD_BFS_TINY=0 (HBM tiers only) gives the same bits as the default on config 4's
-    # stand-ins (the tiny tier with the rhs in LDS)
+@pytest.mark.parametrize("env", ["FSTAMD_BFS_TINY", "FSTAMD_EAGER_CTINY"])
+def test_batch_tiny_tier_off_matches(monkeypatch, env):
+    # FSTAMD_BFS_TINY=0 (HBM tiers only) and FSTAMD_EAGER_CTINY=0 (eager_bfs.hpp's kTiny
+    # tables instead of the compact ones) give the same bits as the default on config 4's
+    # stand-ins
     import libfst_amd.synthetic as SY
     stages = [SY.to_mutable(SY.tagger()).freeze(), SY.to_mutable(SY.verbalizer()).freeze()]
     labels, offsets = SY.to_labels(SY.utterances(np.random.default_rng(9), 512))
     a = F.pipeline_batch(stages, labels, offsets, 1, EAGER)
-    monkeypatch.setenv("FSTAMD_BFS_TINY", "0")
+    monkeypatch.setenv(env, "0")
     b = F.pipeline_batch(stages, labels, offsets, 1, EAGER)
     assert np.array_equal(a.status, b.status) and np.all(a.status == F.FST_PATH_OK)
     assert np.array_equal(a.offsets, b.offsets)

@@ -47,6 +47,19 @@ def test_tagger_stage_tiny_start(standin, sem, start, monkeypatch):
     assert (got.status == F.FST_PATH_OK).all()
 
 
+@pytest.mark.parametrize("ctiny", ["0", "1"])
+@pytest.mark.parametrize("start", ["1", "2"])
+def test_tagger_stage_eager_tables(standin, ctiny, start, monkeypatch):
+    # eager, both LDS table layouts (the compact one of kernels/eager_tiny.hpp, the default,
+    # and eager_bfs.hpp's kTiny ones), from either size: bit-exact against the oracle
+    monkeypatch.setenv("FSTAMD_EAGER_CTINY", ctiny)
+    monkeypatch.setenv("FSTAMD_BFS_TINY_START", start)
+    tb, _, _, _ = standin
+    labels, offsets = W.utterances(np.random.default_rng(91 + int(start)), 1000)
+    got, ref = check(tb, labels, offsets, EAGER)
+    assert (got.status == F.FST_PATH_OK).all()
+
+
 def oracle_pipeline(blobs, labels, offsets, sem):
     num = len(offsets) - 1
     fail = np.full(num, F.FST_PATH_OK, np.int32)
