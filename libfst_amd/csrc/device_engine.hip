@@ -2013,7 +2013,7 @@ hipError_t DeviceEngine::run_bfs_chain(const DeviceFst& rhs, const ChainInput& i
                      rhs.skip_tiny_eager.load(std::memory_order_relaxed) == 0);
   const uint32_t count0 = count;
   // Eager semantics on an rhs a one-word tuple key can name: the compact tiny tiers
-  // (kernels/eager_tiny.hpp, ~63 B per tuple instead of ~110: 18 / 9 workgroups per CU
+  // (kernels/eager_tiny.hpp, ~52 B per tuple instead of ~110: 23 / 12 workgroups per CU
   // instead of 10 / 5).  FSTAMD_EAGER_CTINY=0 keeps eager_bfs_kernel's (A/B runs, tests).
   const char* cte = std::getenv("FSTAMD_EAGER_CTINY");
   const bool compact = tiny && !lazy && !(cte && std::strcmp(cte, "0") == 0) &&

@@ -9,14 +9,14 @@
 // smallest (source id, arc index), best final = lexmin (total, id)); only the tables are
 // narrower, because the utterances of a WeText-scale tagger (~140 tuples, 95 % under 256)
 // are latency-bound and their workgroups per CU were set by LDS: eager_bfs_kernel<64,
-// false, 2> holds ~110 B per tuple (28 KB at 256 tuples, 5 per CU); this one ~63 B
-// (16 KB, 9 per CU; 8.6 KB and 18 per CU at 128):
+// false, 2> holds ~110 B per tuple (28 KB at 256 tuples, 5 per CU); this one ~52 B
+// (13.1 KB, 12 per CU; 6.8 KB and 23 per CU at 128):
 //   - a tuple key is one word, (s2 << 9) | (s1 << 2) | filter: the lhs is a chain of at
 //     most 126 labels (s1 < 128) and the host sends only an rhs of fewer than 2^23 states;
 //   - ids, arc offsets and levels are 16-bit; a back-pointer is (source << 16) | arc index;
-//   - an arc keeps its weight (f64, relaxed every level) and a code for its labels (the rhs
-//     arc, flagged when it is phase 3's rhs-epsilon-alone arc, or kCtPhase2): ilabels and
-//     olabels are read back from the lhs labels and the rhs records for the path's arcs only;
+//   - an arc keeps its target and weight (f64, relaxed every level), not its labels: the
+//     path's arcs read theirs back by expanding their source tuples again;
+//   - the hash has 1.5 slots per tuple (any size: multiply-shift home slots);
 //   - final weights are recomputed for the tuples with s1 = L instead of being stored.
 #pragma once
 
@@ -34,43 +34,78 @@ __host__ __device__ constexpr int ct_waves(int n) { return n <= 128 ? 5 : 3; }  
 __device__ __forceinline__ uint32_t ct_key(uint32_t s1, uint32_t s2, uint32_t f) {
   return (s2 << 9) | (s1 << 2) | f;
 }
-__device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
+// Home slot of key k in a table of H slots (any H: multiply-shift of a mixed hash).
+template <uint32_t H>
+__device__ __forceinline__ uint32_t ct_slot(uint32_t k) {
   k ^= k >> 16;
   k *= 0x7feb352du;
   k ^= k >> 15;
-  return k;
+  return (uint32_t)(((uint64_t)k * H) >> 32);
+}
+// Insert key into the hash (linear probing); its slot, or kEmptyKey when the table is full.
+template <uint32_t H>
+__device__ __forceinline__ uint32_t ct_insert(uint32_t* hkey, uint32_t key) {
+  uint32_t h = ct_slot<H>(key);
+  for (uint32_t probe = 0; probe < H; ++probe) {
+    const uint32_t old = atomicCAS(&hkey[h], kEmptyKey, key);
+    if (old == kEmptyKey || old == key) return h;
+    h = h + 1 < H ? h + 1 : 0u;
+  }
+  return kEmptyKey;
 }
 
-// bfs_expand (eager_bfs.hpp) for a chain lhs (label lab[s1] on arc s1 -> s1 + 1, weight One):
-// the same candidates in the same order, each as emit(code, weight, target key).
-template <class Emit>
-__device__ __forceinline__ void ct_expand(const RhsView& rhs, const uint32_t* lab, uint32_t L,
-                                          uint32_t s1, uint32_t s2, uint32_t f, Emit&& emit) {
-  const bool arc = s1 < L;
-  const uint32_t c = arc ? lab[s1] : 0u;
-  if (arc && c != kEpsilon) {  // phase 1 (compose.zig:95-121)
-    uint32_t lo, cnt;
-    span_summary<false>(rhs, s2, c, lo, cnt);
-    for (uint32_t a = lo; a < lo + cnt; ++a) {
-      const ArcRec r = rhs.rec[a];
-      emit(a, w_times(w_one(), r.weight), ct_key(s1 + 1, r.next, 0));
-    }
+// bfs_expand (eager_bfs.hpp) for a chain lhs (label lab[s1] on arc s1 -> s1 + 1, weight One),
+// in two steps: ct_spans finds the tuple's rhs spans (the dependent loads: the state
+// summary, a search on a multi-label state), ct_emit walks them and emits the same
+// candidates in the same order, each as emit(code, weight, target key, olabel).  The level loop
+// keeps a lane's spans from the count pass (A) for the arc pass (B).
+struct CtSpans {
+  uint32_t lo, cnt;    // phase 1's arcs (cnt = 0: none)
+  uint32_t elo, ecnt;  // the state's epsilon-input arcs
+  uint32_t s1, s2, f, c;
+  bool arc;            // s1 < L
+  __device__ uint32_t count() const {
+    const bool e = arc && c == kEpsilon;
+    return cnt + ((f != 1 && e) ? 1u : 0u) + (f != 2 ? ecnt : 0u) + ((f == 0 && e) ? ecnt : 0u);
   }
-  if (f != 1 && arc && c == kEpsilon)  // phase 2 (:124-134)
-    emit(kCtPhase2, w_one(), ct_key(s1 + 1, s2, f == 0 ? 2u : f));
-  uint32_t elo, ecnt;
-  span_summary<false>(rhs, s2, kEpsilon, elo, ecnt);
+};
+
+__device__ __forceinline__ CtSpans ct_spans(const RhsView& rhs, const uint32_t* lab, uint32_t L,
+                                            uint32_t k) {
+  CtSpans sp;
+  sp.s1 = (k >> 2) & 127u;
+  sp.s2 = k >> 9;
+  sp.f = k & 3u;
+  sp.arc = sp.s1 < L;
+  sp.c = sp.arc ? lab[sp.s1] : 0u;
+  sp.lo = 0;
+  sp.cnt = 0;
+  if (sp.arc && sp.c != kEpsilon) span_summary<false>(rhs, sp.s2, sp.c, sp.lo, sp.cnt);
+  span_summary<false>(rhs, sp.s2, kEpsilon, sp.elo, sp.ecnt);
+  return sp;
+}
+
+template <class Emit>
+__device__ __forceinline__ void ct_emit(const RhsView& rhs, const CtSpans& sp, Emit&& emit) {
+  const uint32_t s1 = sp.s1, s2 = sp.s2, f = sp.f;
+  for (uint32_t a = sp.lo; a < sp.lo + sp.cnt; ++a) {  // phase 1 (compose.zig:95-121)
+    const ArcRec r = rhs.rec[a];
+    emit(a, w_times(w_one(), r.weight), ct_key(s1 + 1, r.next, 0), r.olabel);
+  }
+  const bool e = sp.arc && sp.c == kEpsilon;
+  if (f != 1 && e)  // phase 2 (:124-134)
+    emit(kCtPhase2, w_one(), ct_key(s1 + 1, s2, f == 0 ? 2u : f), kEpsilon);
   if (f != 2) {  // phase 3 (:136-157)
     const uint32_t nf = f == 0 ? 1u : f;
-    for (uint32_t a = elo; a < elo + ecnt; ++a) {
+    for (uint32_t a = sp.elo; a < sp.elo + sp.ecnt; ++a) {
       const ArcRec r = rhs.rec[a];
-      emit(a | kCtPhase3, r.weight, ct_key(s1, r.next, nf));
+      emit(a | kCtPhase3, r.weight, ct_key(s1, r.next, nf), r.olabel);
     }
   }
-  if (f == 0 && ecnt && arc && c == kEpsilon) {  // phase 4 (:160-194)
-    for (uint32_t a = elo; a < elo + ecnt; ++a) {
+  if (f == 0 && e) {  // phase 4 (:160-194)
+    for (uint32_t a = sp.elo; a < sp.elo + sp.ecnt; ++a) {
       const ArcRec r = rhs.rec[a];
-      emit(a, w_times(w_one(), r.weight), ct_key(s1 + 1, r.next, 0));
+      emit(a, w_times(w_one(), r.weight), ct_key(s1 + 1, r.next, 0), r.olabel);
     }
   }
 }
@@ -99,13 +134,13 @@ __global__ void __launch_bounds__(64, ct_waves(kN))
 eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item,
                   const uint32_t* items, const uint32_t* num_items_dev,
                   unsigned long long wd_ticks, BatchOutDev out) {
-  constexpr uint32_t N = kN, A = kN * 3 / 2, H = 2 * kN, HM = H - 1;
-  static_assert((H & HM) == 0 && N <= 256 && A < 65536, "16-bit ids and offsets");
+  constexpr uint32_t N = kN, A = kN * 3 / 2, H = kN * 3 / 2;
+  static_assert(N <= 256 && A < 65536 && H < 65535, "16-bit ids, offsets and slots");
   __shared__ CtShared SH;
-  __shared__ uint32_t hkey[H], hval[H], nkey[N], nback[N], acode[A], cslot[A], lab[kCtLab];
+  __shared__ uint32_t hkey[H], hval[H], nkey[N], nback[N], lab[kCtLab];
   __shared__ unsigned long long nd[N];
   __shared__ double aw[A];
-  __shared__ uint16_t aoff[N + 2], lvl[N + 2], anext[A];
+  __shared__ uint16_t aoff[N + 2], lvl[N + 2], anext[A], cslot[A];
   const uint32_t tid = threadIdx.x;
   const uint32_t num_items = *num_items_dev;
 
@@ -141,7 +176,7 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     }
     __syncthreads();
     if (tid == 0) {
-      const uint32_t k0 = ct_key(0, rhs.start, 0), h = ct_hash(k0) & HM;
+      const uint32_t k0 = ct_key(0, rhs.start, 0), h = ct_slot<H>(k0);
       hkey[h] = k0;
       hval[h] = 0;
       nkey[0] = k0;
@@ -160,13 +195,14 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       if (f0 >= f1) break;
       // (A) candidate counts -> arc offsets (written only while they fit: 16-bit)
       uint32_t carry = 0;
+      CtSpans sp0;  // the lane's first tuple of the level (p = f0 + tid), kept for (B)
       for (uint32_t b = f0; b < f1; b += 64) {
         const uint32_t p = b + tid;
         uint32_t cnt = 0;
         if (p < f1) {
-          const uint32_t k = nkey[p];
-          ct_expand(rhs, lab, L, (k >> 2) & 127u, k >> 9, k & 3u,
-                    [&](uint32_t, double, uint32_t) { ++cnt; });
+          const CtSpans sp = ct_spans(rhs, lab, L, nkey[p]);
+          cnt = sp.count();
+          if (b == f0) sp0 = sp;
         }
         uint32_t tot;
         const uint32_t ex = block_excl_scan<64>(cnt, nullptr, tot);
@@ -182,35 +218,23 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
         SH.flag = 0;
       }
       __syncthreads();
-      // (B) the level's arcs, then every candidate's target into the hash (the first
-      // candidate of a new key keeps the smallest arc index)
+      // (B) the level's arcs (weights; their labels are read back for the path only), each
+      // candidate's target into the hash by the lane that emits it (the first candidate of
+      // a new key keeps the smallest arc index; a tagger level has a handful of tuples with
+      // one or two candidates each, so parking the keys for a parallel insert cost LDS and
+      // saved nothing)
       const uint32_t c0 = n_arcs, c1 = n_arcs + carry;
       for (uint32_t p = f0 + tid; p < f1; p += 64) {
-        const uint32_t k = nkey[p];
         uint32_t a = aoff[p];
-        ct_expand(rhs, lab, L, (k >> 2) & 127u, k >> 9, k & 3u,
-                  [&](uint32_t code, double w, uint32_t key) {
-                    acode[a] = code;
-                    aw[a] = w;
-                    cslot[a] = key;
-                    ++a;
-                  });
-      }
-      __syncthreads();
-      for (uint32_t a = c0 + tid; a < c1; a += 64) {
-        const uint32_t key = cslot[a];
-        uint32_t h = ct_hash(key) & HM, slot = kEmptyKey;
-        for (uint32_t probe = 0; probe <= HM; ++probe) {
-          const uint32_t old = atomicCAS(&hkey[h], kEmptyKey, key);
-          if (old == kEmptyKey || old == key) {
-            slot = h;
-            break;
-          }
-          h = (h + 1) & HM;
-        }
-        if (slot == kEmptyKey) SH.flag = 1;
-        else atomicMin(&hval[slot], 0x80000000u | a);
-        cslot[a] = slot;
+        ct_emit(rhs, p == f0 + tid ? sp0 : ct_spans(rhs, lab, L, nkey[p]),
+                [&](uint32_t, double w, uint32_t key, uint32_t) {
+                  aw[a] = w;
+                  const uint32_t slot = ct_insert<H>(hkey, key);
+                  if (slot == kEmptyKey) SH.flag = 1;
+                  else atomicMin(&hval[slot], 0x80000000u | a);
+                  cslot[a] = (uint16_t)slot;
+                  ++a;
+                });
       }
       __syncthreads();
       if (SH.flag) {
@@ -361,8 +385,9 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     if (mk != kMaxU64 && mk == SH.best) atomicMin(&SH.bestid, mid);
     __syncthreads();
     // backtrace: thread 0 walks the back-pointers in LDS (bounded: a cycle reports CYCLE)
-    // and parks the path's (source, arc) pairs in anext / cslot; the wave then writes the
-    // arcs, reading their olabels from the rhs records in parallel
+    // and parks the path's (source, arc index) pairs in anext / cslot; then one lane per
+    // path arc expands its source tuple again up to that arc for the arc's labels (the
+    // tables keep no labels), all in parallel
     const uint32_t best = SH.bestid;
     if (tid == 0) {
       int32_t verdict = kPathOk;
@@ -391,7 +416,7 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
           for (uint32_t k = hops; k > 0; --k) {
             const uint32_t b = nback[cur], s = b >> 16;
             anext[k - 1] = (uint16_t)s;
-            cslot[k - 1] = aoff[s] + (b & 0xFFFFu);
+            cslot[k - 1] = (uint16_t)b;
             cur = s;
           }
           SH.path_o = o;
@@ -409,12 +434,18 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     const uint32_t hops = SH.hops;
     const unsigned long long o = SH.path_o;
     for (uint32_t k = tid; k < hops; k += 64) {
-      const uint32_t a = cslot[k], code = acode[a];
-      const uint32_t s1 = (nkey[anext[k]] >> 2) & 127u;
-      const bool ph2 = code == kCtPhase2, ph3 = !ph2 && (code & kCtPhase3) != 0u;
-      out.out_il[o + k] = ph3 ? kEpsilon : lab[s1];
-      out.out_ol[o + k] = ph2 ? kEpsilon : rhs.rec[code & ~kCtPhase3].olabel;
-      out.out_w[o + k] = aw[a];
+      const uint32_t s = anext[k], ai = cslot[k], k1 = nkey[s];
+      uint32_t i = 0, code = 0, ol = 0;
+      ct_emit(rhs, ct_spans(rhs, lab, L, k1), [&](uint32_t c, double, uint32_t, uint32_t l) {
+        if (i++ == ai) {
+          code = c;
+          ol = l;
+        }
+      });
+      const bool ph3 = code != kCtPhase2 && (code & kCtPhase3) != 0u;
+      out.out_il[o + k] = ph3 ? kEpsilon : lab[(k1 >> 2) & 127u];
+      out.out_ol[o + k] = ol;
+      out.out_w[o + k] = aw[aoff[s] + ai];
     }
     if (tid == 0) {
       out.status[si] = kPathOk;
