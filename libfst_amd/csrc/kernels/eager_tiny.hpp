@@ -85,6 +85,90 @@ __device__ __forceinline__ CtSpans ct_spans(const RhsView& rhs, const uint32_t* 
   return sp;
 }
 
+// ct_spans for the whole wave (every lane calls it; `valid` lanes get their tuple's spans).
+// Phase 1's arcsByIlabel on a multi-label state of more than 8 arcs was a binary search per
+// lane: ~2 log2(n) dependent loads, 10-14 round trips on a WeText-scale tagger's lead-byte
+// and char-boundary states (17-110 arcs), every BFS level.  Here lanes in 16-lane groups
+// count the state's ilabels below / up to the label instead, 64 per round trip, four
+// lanes' searches at a time.
+__device__ __forceinline__ CtSpans ct_spans_wave(const RhsView& rhs, const uint32_t* lab,
+                                                 uint32_t L, uint32_t k, bool valid) {
+  CtSpans sp;
+  sp.s1 = (k >> 2) & 127u;
+  sp.s2 = k >> 9;
+  sp.f = k & 3u;
+  sp.arc = valid && sp.s1 < L;
+  sp.c = sp.arc ? lab[sp.s1] : 0u;
+  sp.lo = sp.cnt = sp.elo = sp.ecnt = 0;
+  uint4 ss = make_uint4(0, 0, 0, 0);
+  if (valid) {
+    ss = rhs.sspan[sp.s2];  // span_summary's cases, from one load
+    sp.elo = ss.x;
+    sp.ecnt = ss.z == kEpsilon ? ss.y : ss.z == kSpanMixed ? ss.w : 0u;
+  }
+  bool need = false;
+  if (sp.arc && sp.c != kEpsilon) {
+    sp.lo = ss.x;
+    if (ss.z == sp.c) {
+      sp.cnt = ss.y;
+    } else if (ss.z == kSpanMixed) {
+      if (ss.y <= 8) {  // span_by_ilabel's independent loads
+        uint32_t x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = (uint32_t)i < ss.y ? rhs.il[ss.x + i] : 0xFFFFFFFFu;
+        uint32_t cl = 0, ch = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool v = (uint32_t)i < ss.y;
+          cl += (v && x[i] < sp.c) ? 1u : 0u;
+          ch += (v && x[i] <= sp.c) ? 1u : 0u;
+        }
+        sp.lo = ss.x + cl;
+        sp.cnt = ch - cl;
+      } else {
+        need = true;
+      }
+    }
+  }
+  const uint32_t lane = threadIdx.x & 63, g = lane >> 4, sub = lane & 15;
+  uint64_t mask = __ballot(need);
+  while (mask) {  // uniform: up to four searches per round, one per 16-lane group
+    uint64_t m = mask;
+    for (uint32_t i = 0; i < g; ++i) m &= m - 1;
+    const bool has = m != 0;
+    const uint32_t t = has ? (uint32_t)__ffsll((long long)m) - 1 : 0u;
+    // (the shuffles run on every lane: a lane that skipped one would not provide its value)
+    const uint32_t off = __shfl(ss.x, t), nt = __shfl(ss.y, t), label = __shfl(sp.c, t);
+    const uint32_t n = has ? nt : 0u;
+    uint32_t lt = 0, le = 0;
+    for (uint32_t base = 0; __ballot(base < n); base += 64) {
+      uint32_t x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t i = base + sub + 16 * q;
+        x[q] = i < n ? rhs.il[off + i] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool v = base + sub + 16 * q < n;
+        lt += __popcll((__ballot(v && x[q] < label) >> (16 * g)) & 0xFFFFull);
+        le += __popcll((__ballot(v && x[q] <= label) >> (16 * g)) & 0xFFFFull);
+      }
+    }
+    // each searching lane takes its group's counts: job j = its rank among the set bits
+    const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    const bool mine = ((mask >> lane) & 1ull) && j < 4;
+    const uint32_t src = mine ? 16 * j : 0u;
+    const uint32_t mlt = __shfl(lt, src), mle = __shfl(le, src);
+    if (mine) {
+      sp.lo = ss.x + mlt;
+      sp.cnt = mle - mlt;
+    }
+    for (int i = 0; i < 4 && mask; ++i) mask &= mask - 1;
+  }
+  return sp;
+}
+
 template <class Emit>
 __device__ __forceinline__ void ct_emit(const RhsView& rhs, const CtSpans& sp, Emit&& emit) {
   const uint32_t s1 = sp.s1, s2 = sp.s2, f = sp.f;
@@ -198,12 +282,9 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
       CtSpans sp0;  // the lane's first tuple of the level (p = f0 + tid), kept for (B)
       for (uint32_t b = f0; b < f1; b += 64) {
         const uint32_t p = b + tid;
-        uint32_t cnt = 0;
-        if (p < f1) {
-          const CtSpans sp = ct_spans(rhs, lab, L, nkey[p]);
-          cnt = sp.count();
-          if (b == f0) sp0 = sp;
-        }
+        const CtSpans sp = ct_spans_wave(rhs, lab, L, p < f1 ? nkey[p] : 0u, p < f1);
+        const uint32_t cnt = p < f1 ? sp.count() : 0u;
+        if (b == f0) sp0 = sp;
         uint32_t tot;
         const uint32_t ex = block_excl_scan<64>(cnt, nullptr, tot);
         if (p < f1 && n_arcs + carry + ex <= A) aoff[p] = (uint16_t)(n_arcs + carry + ex);
@@ -433,10 +514,14 @@ eager_tiny_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* nex
     }
     const uint32_t hops = SH.hops;
     const unsigned long long o = SH.path_o;
-    for (uint32_t k = tid; k < hops; k += 64) {
-      const uint32_t s = anext[k], ai = cslot[k], k1 = nkey[s];
+    for (uint32_t kb = 0; kb < hops; kb += 64) {  // uniform (ct_spans_wave)
+      const uint32_t k = kb + tid;
+      const bool v = k < hops;
+      const uint32_t s = v ? anext[k] : 0u, ai = v ? cslot[k] : 0u, k1 = nkey[s];
+      const CtSpans sp = ct_spans_wave(rhs, lab, L, k1, v);
+      if (!v) continue;
       uint32_t i = 0, code = 0, ol = 0;
-      ct_emit(rhs, ct_spans(rhs, lab, L, k1), [&](uint32_t c, double, uint32_t, uint32_t l) {
+      ct_emit(rhs, sp, [&](uint32_t c, double, uint32_t, uint32_t l) {
         if (i++ == ai) {
           code = c;
           ol = l;
