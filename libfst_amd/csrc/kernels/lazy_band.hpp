@@ -72,6 +72,9 @@ struct LbWs {
 // The id -> window index map of the newest kLbRing ids also lives in LDS (the rest: the
 // per-wave HBM ring).  Small, so that 32 waves fit a CU's 160 KB of LDS (~5 KB each).
 constexpr uint32_t kLbRing = 256;
+#ifndef FSTAMD_BAND_ATTR
+#define FSTAMD_BAND_ATTR
+#endif
 
 struct LbLds {
   uint32_t ring[kLbRing];  // id -> window index for id >= nn - kLbRing
@@ -80,7 +83,10 @@ struct LbLds {
   uint32_t il[64];
   uint32_t ol[64];
   double w[64];      // arc weight as relaxed (W.times(lhs arc, rhs arc) for phase 1)
-  double nd[64];     // dist[curr] (x) w
+  union {
+    double nd[64];                // dist[curr] (x) w
+    unsigned long long key[64];   // the slot path: per slot min (distance bits | lane)
+  };
 };
 
 __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const ChainInput& in,
@@ -103,6 +109,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   const uint32_t LS = RING - 64;
   const uint32_t S0 = rhs.start;  // every reachable state is >= S0 (arcs go forward)
   const uint32_t SCAP = ws.scap;
+  const bool jf32 = rhs.jump_fwd < 32;  // a pop's targets fit 2 x 32 slots (the slot path)
   auto wix = [&](uint32_t k_, uint32_t s_) { return (s_ & wmask) * LC + k_; };  // x 2 + f
   // v / LC for window indices v < 2^26 (the host plan checks WS * LC < 2^26): one 64-bit
   // multiply instead of a ~35-instruction integer division, exact since 2^38 >= v * LC
@@ -387,6 +394,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     const bool small = na <= 64;
     // the targets' largest state only matters near the window's end (t - s <= jump_fwd)
     const bool near_end = (uint64_t)s + rhs.jump_fwd >= min((uint64_t)slo + WS, (uint64_t)S0 + SCAP);
+    // slot path (below): this lane's candidate, kept in registers
+    bool fast = false, fc = false, fp1 = false;
+    uint32_t fnext = 0;
+    double fnd = 0.0;
     if (small) {
       const bool v = lane < na;
       const uint32_t il = v ? rhs.il[aoff + lane] : 0xFFFFFFFFu;
@@ -397,7 +408,19 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       n1 = (uint32_t)__popcll(m1);
       C = n1 + (uint32_t)__popcll(m3);
       if (near_end) tmax = max(tmax, __ockl_wfred_max_u32((p1 || p3) ? r.next : 0u));
-      if (p1 || p3) {  // (a window index does not depend on slo: valid after any slide)
+      if (jf32) {
+        // the slot path takes the pop when every candidate distance is finite, >= +0 and
+        // has its 6 low mantissa bits clear (integer costs do): then (bits | lane) orders
+        // the candidates of one target exactly as (distance, relax order)
+        fnd = w_times(dcur, p1 ? w_times(w_one(), r.weight) : r.weight);
+        const unsigned long long b = (unsigned long long)__double_as_longlong(fnd);
+        const bool nice = (b & 0x800000000000003Full) == 0ull && b < 0x7FF0000000000000ull;
+        fast = __ballot((p1 || p3) && !nice) == 0ull;
+        fc = p1 || p3;
+        fp1 = p1;
+        fnext = r.next;
+      }
+      if ((p1 || p3) && !fast) {  // (a window index does not depend on slo: valid after any slide)
         const uint32_t rank = p1 ? (uint32_t)__popcll(m1 & lanemask_lt())
                                  : n1 + (uint32_t)__popcll(m3 & lanemask_lt());
         S.x[rank] = p1 ? 2 * wix(k + 1, r.next) : 2 * wix(k, r.next) + 1;
@@ -530,65 +553,118 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
           break;
         }
       }
-      const bool act = lane < cnt_c;
-      const uint32_t tx = act ? S.x[lane] : 0u;
-      // the target's tuple index (its state from the window slot: targets lie in the window)
-      const uint32_t tslot = div_lc(tx >> 1);
-      const uint32_t tstate = slo + ((tslot - slo) & wmask);
-      const uint32_t tg = 2 * gix((tx >> 1) - tslot * LC, tstate) + (tx & 1);
-      const double nd = act ? w_times(dcur, S.w[lane]) : 0.0;
-      S.nd[lane] = nd;
-      const uint4 rv = act ? R[tx] : make_uint4(0, 0, kLdUntouched, 0);
-      // group candidates by target: the group's first lane folds it in order
-      unsigned long long gmask = 0;
-      {
-        unsigned long long pend = __ballot(act);
-        while (pend) {
-          const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
-          const uint32_t xl = lane_read(tx, l);
-          const unsigned long long m = __ballot(act && tx == xl);
-          if (lane == l) gmask = m;
-          pend &= ~m;
+      // per target, one writer lane holds the folded relax (:99-141) of its candidates
+      uint32_t tx = 0, tg = 0, id = 0, bkw = 0;
+      uint4 rv;
+      bool took = false, fresh = false;
+      double cd, od;
+      if (fast) {
+        // slot path: a target's candidates share one slot (phase, t - s < 32); one LDS
+        // min of (distance bits | lane) per slot finds the fold's winner, the first in
+        // relax order among the least distances.  Its fold against the record is the
+        // whole group's: an earlier candidate at a larger distance is overtaken by it,
+        // a later one at the same distance has an olabel >= its own (arcs sort by
+        // (ilabel, olabel)) and loses the tie, and the record cannot hold this pop's id
+        // (each target is met by one phase of one pop).  A min of lanes finds the
+        // slot's first candidate, which numbers a new tuple (getOrCreate order).
+        const bool act = fc;
+        const uint32_t sl = (fp1 ? 0u : 32u) + (fnext - s);
+        const uint32_t kk = fp1 ? k + 1 : k;
+        tx = 2 * wix(kk, fnext) + (fp1 ? 0u : 1u);
+        tg = 2 * gix(kk, fnext) + (fp1 ? 0u : 1u);
+        rv = act ? R[tx] : make_uint4(0, 0, kLdUntouched, 0);
+        unsigned long long* K = S.key;
+        uint32_t* F = S.x;  // per slot: its first candidate's lane
+        const unsigned long long key =
+            (unsigned long long)__double_as_longlong(fnd) | (unsigned long long)lane;
+        K[lane] = ~0ull;
+        F[lane] = ~0u;
+        wave_fence();
+        if (act) {
+          atomicMin(&K[sl], key);
+          atomicMin(&F[sl], lane);
         }
-      }
-      wave_lds_sync();
-      const bool leader = gmask != 0ull;
-      const bool untouched = rv.z == kLdUntouched;
-      const double od = untouched ? w_zero() : ld_dist(rv);
-      double cd = od;
-      uint32_t bprev = untouched ? kLdNoPrev : rv.w;
-      uint32_t bil = 0, bol = 0, ba = 0;
-      bool took = false;
-      if (leader) {
-        if (!untouched && bprev == pid) {  // back set earlier in this pop: its labels
-          const uint32_t a0 = aoff + (bk_get(tg) >> (1 + dbits));
-          bil = rhs.il[a0];
-          bol = rhs.rec[a0].olabel;
-        }
-        unsigned long long m = gmask;
-        while (m) {  // relax (:99-141) in candidate order
-          const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
-          m &= m - 1;
-          const double cnd = S.nd[i];
-          const uint32_t cil = S.il[i], col = S.ol[i];
-          bool take = w_is_zero(cd) || cnd < cd;
-          if (!take && cnd == cd)
-            take = pid < bprev || (pid == bprev && (cil < bil || (cil == bil && col < bol)));
-          if (take) {
-            cd = cnd;
-            bprev = pid;
-            bil = cil;
-            bol = col;
-            ba = S.a[i];
-            took = true;
+        wave_fence();
+        const unsigned long long kmin = act ? K[sl] : 0ull;
+        const uint32_t first = act ? F[sl] : 64u;
+        wave_lds_sync();
+        const bool untouched = rv.z == kLdUntouched;
+        od = untouched ? w_zero() : ld_dist(rv);
+        const uint32_t bprev = untouched ? kLdNoPrev : rv.w;
+        const bool win = act && kmin == key;
+        took = win && (w_is_zero(od) || fnd < od || (fnd == od && pid < bprev));
+        cd = took ? fnd : od;
+        const bool ff = act && first == lane && untouched;
+        const unsigned long long fm1 = __ballot(ff && fp1), fm3 = __ballot(ff && !fp1);
+        const unsigned long long below = (1ull << (first & 63)) - 1;
+        fresh = win && untouched;
+        id = fresh ? nn + (fp1 ? (uint32_t)__popcll(fm1 & below)
+                               : (uint32_t)__popcll(fm1) + (uint32_t)__popcll(fm3 & below))
+                   : (rv.z & ~kLdSettled);
+        nn += (uint32_t)__popcll(fm1) + (uint32_t)__popcll(fm3);
+        bkw = (x & 1) | ((fnext - s) << 1) | (lane << (1 + dbits));
+      } else {
+        const bool act = lane < cnt_c;
+        tx = act ? S.x[lane] : 0u;
+        // the target's tuple index (its state from the window slot: targets lie in the window)
+        const uint32_t tslot = div_lc(tx >> 1);
+        const uint32_t tstate = slo + ((tslot - slo) & wmask);
+        tg = 2 * gix((tx >> 1) - tslot * LC, tstate) + (tx & 1);
+        const double nd = act ? w_times(dcur, S.w[lane]) : 0.0;
+        S.nd[lane] = nd;
+        rv = act ? R[tx] : make_uint4(0, 0, kLdUntouched, 0);
+        // group candidates by target: the group's first lane folds it in order
+        unsigned long long gmask = 0;
+        {
+          unsigned long long pend = __ballot(act);
+          while (pend) {
+            const uint32_t l = (uint32_t)__ffsll((long long)pend) - 1;
+            const uint32_t xl = lane_read(tx, l);
+            const unsigned long long m = __ballot(act && tx == xl);
+            if (lane == l) gmask = m;
+            pend &= ~m;
           }
         }
+        wave_lds_sync();
+        const bool leader = gmask != 0ull;
+        const bool untouched = rv.z == kLdUntouched;
+        od = untouched ? w_zero() : ld_dist(rv);
+        cd = od;
+        uint32_t bprev = untouched ? kLdNoPrev : rv.w;
+        uint32_t bil = 0, bol = 0, ba = 0;
+        if (leader) {
+          if (!untouched && bprev == pid) {  // back set earlier in this pop: its labels
+            const uint32_t a0 = aoff + (bk_get(tg) >> (1 + dbits));
+            bil = rhs.il[a0];
+            bol = rhs.rec[a0].olabel;
+          }
+          unsigned long long m = gmask;
+          while (m) {  // relax (:99-141) in candidate order
+            const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
+            m &= m - 1;
+            const double cnd = S.nd[i];
+            const uint32_t cil = S.il[i], col = S.ol[i];
+            bool take = w_is_zero(cd) || cnd < cd;
+            if (!take && cnd == cd)
+              take = pid < bprev || (pid == bprev && (cil < bil || (cil == bil && col < bol)));
+            if (take) {
+              cd = cnd;
+              bprev = pid;
+              bil = cil;
+              bol = col;
+              ba = S.a[i];
+              took = true;
+            }
+          }
+        }
+        // getOrCreate: new tuples numbered by first occurrence (leaders in lane order)
+        fresh = leader && untouched;
+        const unsigned long long fm = __ballot(fresh);
+        id = fresh ? nn + (uint32_t)__popcll(fm & lanemask_lt()) : (rv.z & ~kLdSettled);
+        nn += (uint32_t)__popcll(fm);
+        bkw = (x & 1) | ((tstate - s) << 1) | ((ba - aoff) << (1 + dbits));
       }
-      // getOrCreate: new tuples numbered by first occurrence (leaders in lane order)
-      const bool fresh = leader && untouched;
-      const unsigned long long fm = __ballot(fresh);
-      const uint32_t id = fresh ? nn + (uint32_t)__popcll(fm & lanemask_lt()) : (rv.z & ~kLdSettled);
-      nn += (uint32_t)__popcll(fm);
+      const bool untouched = rv.z == kLdUntouched;
       // the live span: every id open at dcur is >= pid (pops go in id order) or was
       // re-opened by this pop (checked below); one open above dcur is checked when it joins
       // the bitmap.  So the span holds while the newest id stays below pid + LS.
@@ -596,7 +672,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const bool settled = !untouched && (rv.z & kLdSettled);
       if (took) {
         R[tx] = ld_rec(cd, untouched ? id : rv.z, pid);
-        bk_put(tg, (x & 1) | ((tstate - s) << 1) | ((ba - aoff) << (1 + dbits)));
+        bk_put(tg, bkw);
         if (fresh) {
           idr[id & rmask] = tx;
           S.ring[id & (kLbRing - 1)] = tx;
@@ -713,7 +789,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   wave_lds_sync();
 }
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) FSTAMD_BAND_ATTR
 lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item, LbWs ws,
                  BatchOutDev out) {
   extern __shared__ unsigned long long lb_dyn[];
