@@ -1660,10 +1660,12 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     ws.items = d_order + p.first;
     ws.num_items = p.count;
     HIP_TRY(hipMemsetAsync(ctr + 36, 0, 4, stream));
+    // back pointers of 1, 2 or 4 B: one instance each
+    auto* kern = bkb == 1 ? lazy_band_kernel<1> : bkb == 2 ? lazy_band_kernel<2> : lazy_band_kernel<4>;
     if (p.lds > 64 * 1024)
-      HIP_TRY(hipFuncSetAttribute((const void*)lazy_band_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
-    lazy_band_kernel<<<p.grid, 64, p.lds, stream>>>(rhs.view, in, n, ctr + 36, ws, out);
+      HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)p.lds));
+    kern<<<p.grid, 64, p.lds, stream>>>(rhs.view, in, n, ctr + 36, ws, out);
     HIP_TRY(hipGetLastError());
   }
   *ran = true;

@@ -83,12 +83,14 @@ struct LbLds {
   uint32_t il[64];
   uint32_t ol[64];
   double w[64];      // arc weight as relaxed (W.times(lhs arc, rhs arc) for phase 1)
+  uint32_t fut_lb;   // <= every live future entry's id (LDS min per push; read when needed)
   union {
     double nd[64];                // dist[curr] (x) w
     unsigned long long key[64];   // the slot path: per slot min (distance bits | lane)
   };
 };
 
+template <uint32_t BKB>
 __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const ChainInput& in,
                                                  const LbWs& ws, const BatchOutDev& out,
                                                  uint4* R, void* bkv, uint32_t* idr, uint4* fut,
@@ -120,14 +122,16 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   uint8_t* bk8 = (uint8_t*)bkv;
   uint16_t* bk16 = (uint16_t*)bkv;
   uint32_t* bk32 = (uint32_t*)bkv;
-  const uint32_t bkb = ws.bkb;  // bytes per back pointer: 1, 2 or 4
+  constexpr uint32_t bkb = BKB;  // bytes per back pointer: 1, 2 or 4
   const uint32_t dbits = ws.dbits, dmask = (1u << dbits) - 1;
   auto bk_get = [&](uint32_t g_) -> uint32_t {
-    return bkb == 1 ? (uint32_t)bk8[g_] : bkb == 2 ? (uint32_t)bk16[g_] : bk32[g_];
+    if constexpr (bkb == 1) return (uint32_t)bk8[g_];
+    else if constexpr (bkb == 2) return (uint32_t)bk16[g_];
+    else return bk32[g_];
   };
   auto bk_put = [&](uint32_t g_, uint32_t c_) {
-    if (bkb == 1) bk8[g_] = (uint8_t)c_;
-    else if (bkb == 2) bk16[g_] = (uint16_t)c_;
+    if constexpr (bkb == 1) bk8[g_] = (uint8_t)c_;
+    else if constexpr (bkb == 2) bk16[g_] = (uint16_t)c_;
     else bk32[g_] = c_;
   };
   if (prof && lane == 0) prof[3] += 1;
@@ -160,7 +164,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   // tuple's back chain, no later pop can change the best or a back pointer on that chain
   const bool early = ws.early != 0;
   uint32_t emax = 0;       // the largest id on the back chain when last walked (grows)
-  uint32_t fut_lb = ~0u;   // <= every live future entry's id (min pushed since the last scan)
+  if (lane == 0) S.fut_lb = ~0u;  // (S.fut_lb: <= every live future entry's id)
   uint32_t nn_slid = 0;    // every tuple that left the window has an id < nn_slid
   uint32_t scan_gate = 0;  // pops before the next exact scan of the future list
   bool stop = false;       // early exit taken
@@ -177,8 +181,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   // cached word (one reduction when an id falls in it), lowp
   auto bucket_insert = [&](bool ins, uint32_t id) {
     if (ins) atomicOr(&bm[(id & rmask) >> 6], 1ull << (id & 63));
-    if (__ballot(ins && (id & ~63u) == cur_base))
-      cur_bits = uni64(cur_bits | wave_or_u64(ins && (id & ~63u) == cur_base ? 1ull << (id & 63) : 0ull));
+    if (__ballot(ins && (id & ~63u) == cur_base)) {  // the cached word: read back (LDS
+      wave_fence();                                   // operations of a wave run in order)
+      cur_bits = uni64(bm[(cur_base & rmask) >> 6]);
+    }
     if (__ballot(ins && id < cur_base)) cache = false;
     if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
   };
@@ -288,7 +294,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         cur_base + (uint32_t)__ffsll((long long)cur_bits) - 1 > emax) {
       // the next pop (the smallest open id at dcur) is past emax; the future list's live
       // ids (above dcur) must be too -- its bound first, an exact scan (amortised) if not
-      if (fut_lb <= emax && pops >= scan_gate) {
+      if (uni(S.fut_lb) <= emax && pops >= scan_gate) {
         uint32_t wpos = 0, mn = ~0u;
         for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
           const uint32_t e = e0 + lane;
@@ -304,10 +310,13 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         }
         wave_fence();
         fn = wpos;
-        fut_lb = uni(wave_min_u32d(mn));
+        mn = uni(wave_min_u32d(mn));
+        wave_lds_sync();
+        if (lane == 0) S.fut_lb = mn;
+        wave_lds_sync();
         scan_gate = pops + max(64u, fn / 16u);
       }
-      if (fut_lb > emax) {
+      if (uni(S.fut_lb) > emax) {
         // the chain's ids now (lane 0 walks it): a tuple still in the window holds its id
         // in its record; one that left it has an id < nn_slid
         uint32_t m = best_id;
@@ -687,7 +696,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const unsigned long long fmk = __ballot(tof);
       if (tof) fut[fn + (uint32_t)__popcll(fmk & lanemask_lt())] = ld_rec(cd, tx, id);
       fn += (uint32_t)__popcll(fmk);
-      if (fmk && early) fut_lb = min(fut_lb, uni(wave_min_u32d(tof ? id : ~0u)));
+      if (tof && early) atomicMin(&S.fut_lb, id);
       bucket_insert(tob, id);
       wave_fence();
       wave_lds_sync();
@@ -789,6 +798,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   wave_lds_sync();
 }
 
+template <uint32_t BKB>
 __global__ void __launch_bounds__(64) FSTAMD_BAND_ATTR
 lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item, LbWs ws,
                  BatchOutDev out) {
@@ -840,7 +850,7 @@ lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next
     if (pre != kPathOk) {
       if (lane == 0) write_status(out, si, pre, 0, 0);
     } else {
-      lazy_band_string(rhs, in, ws, out, R, bk, idr, fut, bm, lab, S, prof, si, L);
+      lazy_band_string<BKB>(rhs, in, ws, out, R, bk, idr, fut, bm, lab, S, prof, si, L);
     }
   }
 }
