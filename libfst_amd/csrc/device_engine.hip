@@ -1536,7 +1536,7 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   auto len = [&](uint32_t i) { return (uint32_t)std::min<uint64_t>(off[i + 1] - off[i], in.max_len); };
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len(a) < len(b); });
   const uint32_t NS = rhs.view.num_states;
-  constexpr uint32_t kRing = 4096, kFcap = 65536;
+  constexpr uint32_t kRing = kLbIdRing, kFcap = kLbFcap;  // the kernel's compile-time sizes
   // states past the start (every reachable state is: arcs go forward)
   const uint32_t srange = rhs.view.start < NS ? NS - rhs.view.start : NS;
   struct Plan {

@@ -72,8 +72,24 @@ struct LbWs {
 // The id -> window index map of the newest kLbRing ids also lives in LDS (the rest: the
 // per-wave HBM ring).  Small, so that 32 waves fit a CU's 160 KB of LDS (~5 KB each).
 constexpr uint32_t kLbRing = 256;
+// the per-wave id ring (HBM, power of two) and future list: compile-time sizes, so the
+// loop holds no registers for them
+constexpr uint32_t kLbIdRing = 4096;
+constexpr uint32_t kLbFcap = 65536;
+// FSTAMD_BAND_STATS (debug builds, implied by FSTAMD_BAND_DEBUG / _TIMING): advances, slides
+// and the failing state/id in the FSTAMD_BFS_PROF words (they cost the loop registers)
+#if defined(FSTAMD_BAND_DEBUG) || defined(FSTAMD_BAND_TIMING)
+#define FSTAMD_BAND_STATS 1
+#endif
+#ifdef FSTAMD_BAND_STATS
+#define LB_STAT(x) x
+#else
+#define LB_STAT(x) do { } while (0)
+#endif
+// 7 waves per SIMD (72 VGPRs): 42.1 K vs 39.5 K strings/s at the compiler's 73 VGPRs and 6
+// waves (config 3 sample, profiles/r06/band/ab_v5.txt)
 #ifndef FSTAMD_BAND_ATTR
-#define FSTAMD_BAND_ATTR
+#define FSTAMD_BAND_ATTR __attribute__((amdgpu_waves_per_eu(7)))
 #endif
 
 struct LbLds {
@@ -103,12 +119,12 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   const uint32_t NS = rhs.num_states;
   const uint32_t LC = L + 1;
   const uint32_t WS = ws.ws, wmask = WS - 1;
-  const uint32_t RING = ws.ring, rmask = RING - 1;
-  const uint32_t nbw = RING / 64;  // bitmap words
+  constexpr uint32_t RING = kLbIdRing, rmask = RING - 1;
+  constexpr uint32_t nbw = RING / 64;  // bitmap words
   // open ids stay within the newest LS = RING - 64 (an older one hands the string on):
   // then a scan over [nn - LS, nn) never meets one physical bitmap word twice, and the
   // ring slot of an open id is never reused
-  const uint32_t LS = RING - 64;
+  constexpr uint32_t LS = RING - 64;
   const uint32_t S0 = rhs.start;  // every reachable state is >= S0 (arcs go forward)
   const uint32_t SCAP = ws.scap;
   const bool jf32 = rhs.jump_fwd < 32;  // a pop's targets fit 2 x 32 slots (the slot path)
@@ -135,8 +151,8 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     else bk32[g_] = c_;
   };
   if (prof && lane == 0) prof[3] += 1;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  const unsigned long long wd = ws.wd_ticks + (uint64_t)LC * 2 * NS * ws.wd_tuple_ticks;
+  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + ws.wd_ticks +
+                                     (uint64_t)LC * 2 * NS * ws.wd_tuple_ticks;
 
   uint32_t slo = rhs.start;  // window: states [slo, slo + WS)
   const uint32_t x0 = 2 * wix(0, rhs.start);
@@ -147,7 +163,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     bm[0] = 1ull;
   }
   wave_lds_sync();
-  uint32_t nn = 1, fn = 0, pops = 0, advances = 0, slides = 0;
+  uint32_t nn = 1, fn = 0, pops = 0;
+#ifdef FSTAMD_BAND_STATS
+  uint32_t advances = 0, slides = 0;
+#endif
   uint32_t lowp = 0;                 // every open id at dcur is >= lowp
   uint32_t cur_base = 0;             // cached word: ids [cur_base, cur_base + 64)
   unsigned long long cur_bits = 1ull;
@@ -157,8 +176,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   double best_fw = w_zero(), best_total = w_zero();
   int32_t fail = kPathOk;
   uint32_t site = 0;  // INTERNAL / OVERFLOW: where it stopped (FSTAMD_BFS_PROF)
+#ifdef FSTAMD_BAND_STATS
   uint32_t dbg_s = 0, dbg_t = 0;
-  uint64_t relax = 0;
+#endif
+  uint32_t relax = 0;
   // exact early exit (ws.early): once the next pop is at dcur == best_total
   // and every tuple with an id <= emax is settled, where emax bounds the ids on the best
   // tuple's back chain, no later pop can change the best or a back pointer on that chain
@@ -200,7 +221,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     bool have = uni(cache && cur_bits != 0ull ? 1u : 0u) != 0u;
     if (cache && !have) lowp = max(lowp, cur_base + 64);  // the lowest word is exhausted
     if (!have) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > wd) {
+      if (__builtin_amdgcn_s_memrealtime() > deadline) {
         fail = kPathInternal;
         site = 1;
         break;
@@ -232,7 +253,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     }
     if (!have) {
       // ---- advance: smallest live distance in the future list (:159-163) ----
-      ++advances;
+      LB_STAT(++advances);
       double dmin = w_zero();
       bool any = false;
       uint32_t wpos = 0;
@@ -353,8 +374,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       if (!((wbits >> (pid & 63)) & 1ull) || zz != pid) {
         fail = kPathInternal;
         site = ((wbits >> (pid & 63)) & 1ull) ? 9 : 8;
-        dbg_s = zz;
-        dbg_t = pid;
+        LB_STAT((dbg_s = zz, dbg_t = pid));
         break;
       }
     }
@@ -364,7 +384,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       Rw[4 * (size_t)x + 2] = pid | kLdSettled;
     }
     ++pops;
-    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > wd) {
+    if ((pops & 255u) == 0 && __builtin_amdgcn_s_memrealtime() > deadline) {
       fail = kPathInternal;
       site = 2;
       break;
@@ -372,8 +392,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     if (k > L || s >= NS || pid >= nn) {  // invariant guard: never walk on garbage
       fail = kPathInternal;
       site = 3;
-      dbg_s = s;
-      dbg_t = pid;
+      LB_STAT((dbg_s = s, dbg_t = pid));
       break;
     }
 
@@ -409,8 +428,11 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     double fnd = 0.0;
     if (small) {
       const bool v = lane < na;
-      const uint32_t il = v ? rhs.il[aoff + lane] : 0xFFFFFFFFu;
-      const ArcRec r = v ? rhs.rec[aoff + lane] : ArcRec{0u, 0u, 0.0};
+      // unconditional loads: a lane past the span reads its last arc (or the padding
+      // record past the arc mirror's end when the span is empty) and is masked off
+      const uint32_t ai = aoff + min(lane, max(na, 1u) - 1u);
+      const uint32_t il = v ? rhs.il[ai] : 0xFFFFFFFFu;
+      const ArcRec r = rhs.rec[ai];
       const bool p1 = v && has1 && il == label;
       const bool p3 = v && il == kEpsilon;
       const unsigned long long m1 = __ballot(p1), m3 = __ballot(p3);
@@ -460,8 +482,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     if (tmax - S0 >= SCAP) {  // beyond the back pointers' states: the next launch's
       fail = kPathOverflow;
       site = 10;
-      dbg_s = s;
-      dbg_t = tmax;
+      LB_STAT((dbg_s = s, dbg_t = tmax));
       break;
     }
 
@@ -469,7 +490,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     // ---- the window must hold every target: slide it up to the lowest state with an
     // open tuple (a pop at state s only ever touches states >= s) ----
     if (tmax >= slo + WS) {
-      ++slides;
+      LB_STAT(++slides);
       // lowest state with an open tuple: the ids open at dcur (bitmap) and the live future
       // entries (compacted on the way); none below: the popped state s.  Slides are rare
       // (every ~Ws - L states), so the open set is walked rather than counted per pop.
@@ -507,8 +528,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       if (tmax >= smin + WS) {  // the open tuples span more than the window
         fail = kPathOverflow;
         site = 4;
-        dbg_s = s;
-        dbg_t = smin;
+        LB_STAT((dbg_s = s, dbg_t = smin));
         break;
       }
       // clear the leaving states' records (every tuple there is final)
@@ -541,7 +561,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         wave_lds_sync();
       }
       // room for this chunk's future entries: compact the list first if needed
-      if (fn + 64 > ws.fcap) {
+      if (fn + 64 > kLbFcap) {
         uint32_t wpos = 0;
         for (uint32_t e0 = 0; e0 < fn; e0 += 64) {
           const uint32_t e = e0 + lane;
@@ -556,7 +576,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         }
         wave_fence();
         fn = wpos;
-        if (fn + 64 > ws.fcap) {
+        if (fn + 64 > kLbFcap) {
           fail = kPathOverflow;
           site = 6;
           break;
@@ -577,11 +597,12 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         // (each target is met by one phase of one pop).  A min of lanes finds the
         // slot's first candidate, which numbers a new tuple (getOrCreate order).
         const bool act = fc;
-        const uint32_t sl = (fp1 ? 0u : 32u) + (fnext - s);
+        // (a lane without a candidate reads the popped tuple's record: no branch)
+        const uint32_t sl = ((fp1 ? 0u : 32u) + (fnext - s)) & 63u;
         const uint32_t kk = fp1 ? k + 1 : k;
-        tx = 2 * wix(kk, fnext) + (fp1 ? 0u : 1u);
+        tx = act ? 2 * wix(kk, fnext) + (fp1 ? 0u : 1u) : x;
         tg = 2 * gix(kk, fnext) + (fp1 ? 0u : 1u);
-        rv = act ? R[tx] : make_uint4(0, 0, kLdUntouched, 0);
+        rv = R[tx];
         unsigned long long* K = S.key;
         uint32_t* F = S.x;  // per slot: its first candidate's lane
         const unsigned long long key =
@@ -589,13 +610,13 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         K[lane] = ~0ull;
         F[lane] = ~0u;
         wave_fence();
-        if (act) {
+        if (act) {  // (LDS atomics of many lanes on one word serialise: candidates only)
           atomicMin(&K[sl], key);
           atomicMin(&F[sl], lane);
         }
         wave_fence();
-        const unsigned long long kmin = act ? K[sl] : 0ull;
-        const uint32_t first = act ? F[sl] : 64u;
+        const unsigned long long kmin = K[sl];
+        const uint32_t first = F[sl];
         wave_lds_sync();
         const bool untouched = rv.z == kLdUntouched;
         od = untouched ? w_zero() : ld_dist(rv);
@@ -703,8 +724,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       if (__ballot(clash)) {
         fail = kPathOverflow;
         site = 5;
-        dbg_s = s;
-        dbg_t = uni(wave_min_u32d(clash ? id : ~0u));
+        LB_STAT((dbg_s = s, dbg_t = uni(wave_min_u32d(clash ? id : ~0u))));
         break;
       }
     }
@@ -769,20 +789,24 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     out.final_w[si] = fin;
     if (out.work) {
       out.work[2 * si] = nn;
-      out.work[2 * si + 1] = (uint32_t)relax;
+      out.work[2 * si + 1] = relax;
     }
     if (prof) {
       if (stop) prof[16] += 1;
       prof[0] += pops;
+#ifdef FSTAMD_BAND_STATS
       prof[1] += advances;
       prof[2] += slides;
+#endif
       if (fail != kPathOk && site != 0) {
         if (site >= 4 && site < 8) prof[site] += 1;
         if (site == 10) prof[17] += 1;
         prof[8] = pops;  // the last failure of this wave
         prof[9] = site;
+#ifdef FSTAMD_BAND_STATS
         prof[10] = dbg_s;
         prof[11] = dbg_t;
+#endif
         prof[12] = slo;
         prof[13] = nn;
         prof[14] = fn;
@@ -805,16 +829,16 @@ lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next
   extern __shared__ unsigned long long lb_dyn[];
   __shared__ LbLds S;
   unsigned long long* bm = lb_dyn;                        // [ring / 64] open-at-dcur bitmap
-  uint32_t* lab = (uint32_t*)(lb_dyn + ws.ring / 64);     // [lcap] the string's labels
+  uint32_t* lab = (uint32_t*)(lb_dyn + kLbIdRing / 64);  // [lcap] the string's labels
   const uint32_t lane = threadIdx.x;
   const size_t w = blockIdx.x;
   uint4* R = ws.win + w * ws.wn;
   void* bk = (void*)((uint8_t*)ws.bk + w * ws.tn * ws.bkb);
-  uint32_t* idr = ws.idr + w * (size_t)ws.ring;
-  uint4* fut = ws.fut + w * (size_t)ws.fcap;
+  uint32_t* idr = ws.idr + w * (size_t)kLbIdRing;
+  uint4* fut = ws.fut + w * (size_t)kLbFcap;
   unsigned long long* prof = ws.prof ? ws.prof + w * kLbProf : nullptr;
 
-  for (uint32_t i = lane; i < ws.ring / 64; i += 64) bm[i] = 0ull;
+  for (uint32_t i = lane; i < kLbIdRing / 64; i += 64) bm[i] = 0ull;
   wave_lds_sync();
 
   const uint32_t num_items = ws.items ? ws.num_items : in.num_strings;

@@ -9,5 +9,6 @@ for r in $(seq 1 "$rounds"); do
     LIBFST_AMD_LIB=libfst_amd/variants/$v.so timeout -k 10 120 python -u scripts/band_profile.py --n "$n" \
       > "gpurun_out/abb_$v.$r.log" 2>&1 || exit 1
     echo "$v $r $(tail -1 gpurun_out/abb_$v.$r.log)"
+    sleep 2
   done
 done

@@ -5,7 +5,7 @@
 # usage: [SRC_DIR=dir] scripts/build_engine_variant.sh <name> "<-DFLAG ...>"
 set -e
 cd "$(dirname "$0")/../libfst_amd/csrc"
-make -s -j8
+[ -n "$SKIP_MAKE" ] || make -s -j8
 name=$1; defs=$2
 src=${SRC_DIR:-.}
 vdir=${VARIANT_DIR:-../variants}
