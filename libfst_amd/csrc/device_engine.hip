@@ -39,6 +39,21 @@ namespace fstamd {
 // ---------------------------------------------------------------------------------
 
 // perm (optional): the device's state numbering (old id -> new id, DeviceFst::perm).
+// The band replay's strided arc table: slot i of state s (device numbering) holds the
+// state's i-th arc, or padding past its last one.
+__global__ void build_band_table_kernel(const uint2* span, const uint32_t* il, const ArcRec* rec,
+                                        uint32_t ns, uint32_t sh, uint32_t* bil, ArcRec* brec) {
+  const uint64_t total = (uint64_t)ns << sh;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t st = (uint32_t)(i >> sh), j = (uint32_t)(i & ((1u << sh) - 1));
+    const uint2 sp = span[st];
+    const bool v = j < sp.y;
+    bil[i] = v ? il[sp.x + j] : 0xFFFFFFFFu;
+    brec[i] = v ? rec[sp.x + j] : ArcRec{0u, 0u, 0.0};
+  }
+}
+
 __global__ void build_mirror_kernel(const uint8_t* blob, uint32_t ns, uint32_t na,
                                     const uint32_t* perm, uint2* span, double* fin, uint32_t* il,
                                     ArcRec* rec, uint4* sspan, uint4* sspan2) {
@@ -202,6 +217,28 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
   d->nan = f.has_nan_weight();
   d->finite = f.arc_weights_finite();
   d->weight_type = f.weight_type();
+  // band replay's strided arc table (<= 1 GB; without it the band reads spans first)
+  if (d->has_eps && jb == 0 && max_span > 0 && max_span <= 64 && ns > 0 &&
+      !std::getenv("FSTAMD_NO_BAND_TABLE")) {
+    uint32_t sh = 0;
+    while ((1u << sh) < max_span) ++sh;
+    const uint64_t slots = (uint64_t)ns << sh;
+    if (slots * (4 + sizeof(ArcRec)) <= (1ull << 30)) {
+      if (hipMalloc(&d->band_il, slots * 4) != hipSuccess ||
+          hipMalloc(&d->band_rec, slots * sizeof(ArcRec)) != hipSuccess) {
+        DeviceFst::destroy(d);
+        return nullptr;
+      }
+      d->band_sh = sh;
+      const uint32_t bb = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 8192);
+      build_band_table_kernel<<<bb, 256>>>(d->span, d->il, d->rec, ns, sh, d->band_il,
+                                           d->band_rec);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) {
+        DeviceFst::destroy(d);
+        return nullptr;
+      }
+    }
+  }
   // pull tier (eager_pull.hip); false = device OOM.  Its uploads go to the null stream:
   // wait for them before engines on their own streams read the mirror
   if (!build_reverse_mirror(d, f) || hipStreamSynchronize(nullptr) != hipSuccess) {
@@ -248,6 +285,8 @@ void DeviceFst::destroy(DeviceFst* d) {
   if (d->il) (void)hipFree(d->il);
   if (d->rec) (void)hipFree(d->rec);
   if (d->sspan) (void)hipFree(d->sspan);
+  if (d->band_il) (void)hipFree(d->band_il);
+  if (d->band_rec) (void)hipFree(d->band_rec);
   free_reverse_mirror(d);
   (void)hipSetDevice(cur);
   delete d;
@@ -1646,6 +1685,9 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   if (ws.prof) HIP_TRY(hipMemsetAsync(ws.prof, 0, (size_t)gmax * kLbProf * 8, stream));
   ws.ring = kRing;
   ws.fcap = kFcap;
+  ws.sil = rhs.band_il;
+  ws.srec = rhs.band_rec;
+  ws.ssh = rhs.band_sh;
   // the exact early exit needs every arc and final weight >= +0, finite
   // arcs; FSTAMD_NO_EARLY=1 replays the whole product as the reference does (tests, A/B)
   ws.early = (rhs.nonneg && rhs.finite && !std::getenv("FSTAMD_NO_EARLY")) ? 1u : 0u;

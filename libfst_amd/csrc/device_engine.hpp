@@ -161,6 +161,13 @@ struct DeviceFst {
   mutable std::atomic<uint64_t> tiny_lazy_seen{0}, tiny_lazy_over{0};
   RevView rev{};
   void* rev_bufs[9] = {};
+  // band replay (kernels/lazy_band.hpp): the arcs at a fixed stride of 2^band_sh slots per
+  // state (device numbering), built when the rhs takes the band replay (arcs forward, input
+  // epsilon, <= 64 arcs per state) and the table stays small; padding slots: ilabel
+  // 0xFFFFFFFF, a zero record
+  uint32_t* band_il = nullptr;
+  ArcRec* band_rec = nullptr;
+  uint32_t band_sh = 0;
   // The device's state numbering (old id -> new id; empty = the blob's own ids): a
   // breadth-first renumbering of an rhs with scattered ids (device_engine.hip
   // bfs_renumbering).  Every device view (RhsView, RevView) uses it; results do not.

@@ -67,11 +67,20 @@ struct LbWs {
                               // (8..15), early exits (16), overflows past scap (17)
   const uint32_t* items;      // this launch's strings, or nullptr = all
   uint32_t num_items;
+  // the rhs's arcs at a fixed stride per state (DeviceFst::band_il / band_rec: 2^ssh slots,
+  // padding slots with ilabel 0xFFFFFFFF), or nullptr: a pop reads its state's arcs without
+  // first reading the state's span
+  const uint32_t* sil;
+  const ArcRec* srec;
+  uint32_t ssh;
 };
 
 // The id -> window index map of the newest kLbRing ids also lives in LDS (the rest: the
 // per-wave HBM ring).  Small, so that 32 waves fit a CU's 160 KB of LDS (~5 KB each).
-constexpr uint32_t kLbRing = 256;
+#ifndef FSTAMD_BAND_LDS_RING
+#define FSTAMD_BAND_LDS_RING 256
+#endif
+constexpr uint32_t kLbRing = FSTAMD_BAND_LDS_RING;
 // the per-wave id ring (HBM, power of two) and future list: compile-time sizes, so the
 // loop holds no registers for them
 constexpr uint32_t kLbIdRing = 4096;
@@ -416,7 +425,10 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     // ---- candidates: phase 1 (labels[k] arcs) then phase 3 (epsilon arcs) ----
     const bool has1 = k < L;
     const uint32_t label = has1 ? lab[k] : 0u;
-    const uint2 sp = rhs.span[s];
+    // with the strided table a state's arcs sit at s << ssh (aoff 0: every use of an arc
+    // index below is relative to the state's first arc), else behind its span
+    const bool tab = ws.sil != nullptr;
+    const uint2 sp = tab ? make_uint2(0u, 1u << ws.ssh) : rhs.span[s];
     const uint32_t aoff = sp.x, na = sp.y;
     uint32_t C = 0, lo1 = 0, n1 = 0, lo3 = 0, tmax = s;
     const bool small = na <= 64;
@@ -430,9 +442,9 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
       const bool v = lane < na;
       // unconditional loads: a lane past the span reads its last arc (or the padding
       // record past the arc mirror's end when the span is empty) and is masked off
-      const uint32_t ai = aoff + min(lane, max(na, 1u) - 1u);
-      const uint32_t il = v ? rhs.il[ai] : 0xFFFFFFFFu;
-      const ArcRec r = rhs.rec[ai];
+      const uint32_t ai = (tab ? s << ws.ssh : aoff) + min(lane, max(na, 1u) - 1u);
+      const uint32_t il = v ? (tab ? ws.sil[ai] : rhs.il[ai]) : 0xFFFFFFFFu;
+      const ArcRec r = tab ? ws.srec[ai] : rhs.rec[ai];
       const bool p1 = v && has1 && il == label;
       const bool p3 = v && il == kEpsilon;
       const unsigned long long m1 = __ballot(p1), m3 = __ballot(p3);
@@ -664,7 +676,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
         uint32_t bil = 0, bol = 0, ba = 0;
         if (leader) {
           if (!untouched && bprev == pid) {  // back set earlier in this pop: its labels
-            const uint32_t a0 = aoff + (bk_get(tg) >> (1 + dbits));
+            const uint32_t a0 = (tab ? rhs.span[s].x : aoff) + (bk_get(tg) >> (1 + dbits));
             bil = rhs.il[a0];
             bol = rhs.rec[a0].olabel;
           }
