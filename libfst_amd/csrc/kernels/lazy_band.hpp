@@ -211,12 +211,16 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   // cached word (one reduction when an id falls in it), lowp
   auto bucket_insert = [&](bool ins, uint32_t id) {
     if (ins) atomicOr(&bm[(id & rmask) >> 6], 1ull << (id & 63));
-    if (__ballot(ins && (id & ~63u) == cur_base)) {  // the cached word: read back (LDS
-      wave_fence();                                   // operations of a wave run in order)
-      cur_bits = uni64(bm[(cur_base & rmask) >> 6]);
+    // each case below has id < cur_base + 64 (lowp <= cur_base + 64): one test for the
+    // common insert above the cached word
+    if (__ballot(ins && id < cur_base + 64)) {
+      if (__ballot(ins && (id & ~63u) == cur_base)) {  // the cached word: read back (LDS
+        wave_fence();                                   // operations of a wave run in order)
+        cur_bits = uni64(bm[(cur_base & rmask) >> 6]);
+      }
+      if (__ballot(ins && id < cur_base)) cache = false;
+      if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
     }
-    if (__ballot(ins && id < cur_base)) cache = false;
-    if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
   };
 
 #ifdef FSTAMD_BAND_TIMING
