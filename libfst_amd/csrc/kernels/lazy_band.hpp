@@ -211,16 +211,17 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   // cached word (one reduction when an id falls in it), lowp
   auto bucket_insert = [&](bool ins, uint32_t id) {
     if (ins) atomicOr(&bm[(id & rmask) >> 6], 1ull << (id & 63));
-    // each case below has id < cur_base + 64 (lowp <= cur_base + 64): one test for the
-    // common insert above the cached word
+    // both cases relative to the cached word have id < cur_base + 64: one test for the
+    // common insert above it.  (lowp is not tied to cur_base: after an advance the cached
+    // word is stale and lowp = nn, so its test stays separate.)
     if (__ballot(ins && id < cur_base + 64)) {
       if (__ballot(ins && (id & ~63u) == cur_base)) {  // the cached word: read back (LDS
         wave_fence();                                   // operations of a wave run in order)
         cur_bits = uni64(bm[(cur_base & rmask) >> 6]);
       }
       if (__ballot(ins && id < cur_base)) cache = false;
-      if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
     }
+    if (__ballot(ins && id < lowp)) lowp = uni(wave_min_u32d(ins ? id : ~0u));
   };
 
 #ifdef FSTAMD_BAND_TIMING
