@@ -124,3 +124,38 @@ def test_negative_finals_no_early_exit(route, capfd, seed):
     seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 30)))] for _ in range(24)]
     check(blob, *csr(seqs), LAZY)
     assert handed_on(capfd.readouterr().err) == []  # not the band
+
+
+def test_without_arc_table(route, capfd, monkeypatch):
+    # the strided per-state arc table (DeviceFst::band_il / band_rec) is the default; the
+    # span-then-arcs reads without it must give the same answers
+    monkeypatch.setenv("FSTAMD_NO_BAND_TABLE", "1")
+    blob = O.freeze(O.gen("eps_dense", 1024, 12))
+    check(blob, *csr([[1] * L for L in (0, 1, 11, 64, 200)]), LAZY)
+    rng = np.random.default_rng(7400)
+    f = forward_rhs(rng, 300, 40, 5)
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(1, 4, int(rng.integers(0, 40)))] for _ in range(24)]
+    check(blob, *csr(seqs), LAZY)
+    assert handed_on(capfd.readouterr().err)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_slot_fold_mixed_pops(route, capfd, early_mode, seed):
+    # the slot fold takes a pop only when every candidate distance is a finite, >= +0 value
+    # with 6 clear low mantissa bits; integer and dyadic weights with a few 0.1 ones make
+    # pops of both kinds within one string, and states past 64 arcs (seeds 2, 3: no arc
+    # table, the wave-wide span search) take the old fold throughout
+    rng = np.random.default_rng(7500 + seed)
+    deg = 8 if seed < 2 else 90
+    f = forward_rhs(rng, int(rng.integers(40, 300)), deg, 6, labels=2)
+    for st in range(len(f.arcs)):
+        arcs = []
+        for il, ol, w, t in f.arcs[st]:
+            r = rng.random()
+            arcs.append((il, ol, w + (0.1 if r < 0.1 else 0.5 if r < 0.3 else 0.0), t))
+        f.arcs[st] = arcs
+    blob = O.freeze(f)
+    seqs = [[int(x) for x in rng.integers(1, 3, int(rng.integers(0, 40)))] for _ in range(32)]
+    check(blob, *csr(seqs), LAZY)
+    assert handed_on(capfd.readouterr().err)
