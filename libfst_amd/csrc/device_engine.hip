@@ -224,18 +224,23 @@ static DeviceFst* finish_device(DeviceFst* d, const FrozenFst& f) {
     while ((1u << sh) < max_span) ++sh;
     const uint64_t slots = (uint64_t)ns << sh;
     if (slots * (4 + sizeof(ArcRec)) <= (1ull << 30)) {
+      // (an optimisation only: without the HBM for it the band reads spans first)
       if (hipMalloc(&d->band_il, slots * 4) != hipSuccess ||
           hipMalloc(&d->band_rec, slots * sizeof(ArcRec)) != hipSuccess) {
-        DeviceFst::destroy(d);
-        return nullptr;
-      }
-      d->band_sh = sh;
-      const uint32_t bb = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 8192);
-      build_band_table_kernel<<<bb, 256>>>(d->span, d->il, d->rec, ns, sh, d->band_il,
-                                           d->band_rec);
-      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) {
-        DeviceFst::destroy(d);
-        return nullptr;
+        (void)hipGetLastError();  // clear the failed allocation's error
+        if (d->band_il) (void)hipFree(d->band_il);
+        if (d->band_rec) (void)hipFree(d->band_rec);
+        d->band_il = nullptr;
+        d->band_rec = nullptr;
+      } else {
+        d->band_sh = sh;
+        const uint32_t bb = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 8192);
+        build_band_table_kernel<<<bb, 256>>>(d->span, d->il, d->rec, ns, sh, d->band_il,
+                                             d->band_rec);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) {
+          DeviceFst::destroy(d);
+          return nullptr;
+        }
       }
     }
   }
