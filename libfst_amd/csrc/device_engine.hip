@@ -1693,6 +1693,11 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
   ws.sil = rhs.band_il;
   ws.srec = rhs.band_rec;
   ws.ssh = rhs.band_sh;
+  if (std::getenv("FSTAMD_ROUTE_LOG"))
+    for (const Plan& p : plans)
+      std::fprintf(stderr, "[libfst_amd route] band plan: %u strings, lcap %u, grid %u of %u waves "
+                   "(budget %.1f GB), window %u states, arc table %s\n", p.count, p.lcap, p.grid,
+                   max_waves, budget / 1e9, p.wstates, ws.sil ? "on" : "off");
   // the exact early exit needs every arc and final weight >= +0, finite
   // arcs; FSTAMD_NO_EARLY=1 replays the whole product as the reference does (tests, A/B)
   ws.early = (rhs.nonneg && rhs.finite && !std::getenv("FSTAMD_NO_EARLY")) ? 1u : 0u;
