@@ -1713,7 +1713,12 @@ hipError_t DeviceEngine::run_lazy_band(const DeviceFst& rhs, const ChainInput& i
     ws.num_items = p.count;
     HIP_TRY(hipMemsetAsync(ctr + 36, 0, 4, stream));
     // back pointers of 1, 2 or 4 B: one instance each
-    auto* kern = bkb == 1 ? lazy_band_kernel<1> : bkb == 2 ? lazy_band_kernel<2> : lazy_band_kernel<4>;
+    // (and the slot path's preconditions as a compile-time fact when they hold)
+    const bool fp = ws.sil != nullptr && rhs.view.jump_fwd < 32;
+    auto* kern = fp ? (bkb == 1 ? lazy_band_kernel<1, true> : bkb == 2 ? lazy_band_kernel<2, true>
+                                                                         : lazy_band_kernel<4, true>)
+                    : (bkb == 1 ? lazy_band_kernel<1, false> : bkb == 2 ? lazy_band_kernel<2, false>
+                                                                          : lazy_band_kernel<4, false>);
     if (p.lds > 64 * 1024)
       HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)p.lds));

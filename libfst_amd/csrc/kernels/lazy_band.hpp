@@ -115,7 +115,9 @@ struct LbLds {
   };
 };
 
-template <uint32_t BKB>
+// FP: the host guarantees the strided arc table and jump_fwd < 32 (the slot path's
+// preconditions), so neither is tested per pop
+template <uint32_t BKB, bool FP>
 __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const ChainInput& in,
                                                  const LbWs& ws, const BatchOutDev& out,
                                                  uint4* R, void* bkv, uint32_t* idr, uint4* fut,
@@ -136,7 +138,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   constexpr uint32_t LS = RING - 64;
   const uint32_t S0 = rhs.start;  // every reachable state is >= S0 (arcs go forward)
   const uint32_t SCAP = ws.scap;
-  const bool jf32 = rhs.jump_fwd < 32;  // a pop's targets fit 2 x 32 slots (the slot path)
+  const bool jf32 = FP || rhs.jump_fwd < 32;  // a pop's targets fit 2 x 32 slots (the slot path)
   auto wix = [&](uint32_t k_, uint32_t s_) { return (s_ & wmask) * LC + k_; };  // x 2 + f
   // v / LC for window indices v < 2^26 (the host plan checks WS * LC < 2^26): one 64-bit
   // multiply instead of a ~35-instruction integer division, exact since 2^38 >= v * LC
@@ -440,7 +442,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
     const uint32_t label = has1 ? lab[k] : 0u;
     // with the strided table a state's arcs sit at s << ssh (aoff 0: every use of an arc
     // index below is relative to the state's first arc), else behind its span
-    const bool tab = ws.sil != nullptr;
+    const bool tab = FP || ws.sil != nullptr;
     const uint2 sp = tab ? make_uint2(0u, 1u << ws.ssh) : rhs.span[s];
     const uint32_t aoff = sp.x, na = sp.y;
     uint32_t C = 0, lo1 = 0, n1 = 0, lo3 = 0, tmax = s;
@@ -848,7 +850,7 @@ __device__ __forceinline__ void lazy_band_string(const RhsView& rhs, const Chain
   wave_lds_sync();
 }
 
-template <uint32_t BKB>
+template <uint32_t BKB, bool FP>
 __global__ void __launch_bounds__(64) FSTAMD_BAND_ATTR
 lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next_item, LbWs ws,
                  BatchOutDev out) {
@@ -900,7 +902,7 @@ lazy_band_kernel(RhsView rhs, ChainInput in, uint32_t n_best, unsigned int* next
     if (pre != kPathOk) {
       if (lane == 0) write_status(out, si, pre, 0, 0);
     } else {
-      lazy_band_string<BKB>(rhs, in, ws, out, R, bk, idr, fut, bm, lab, S, prof, si, L);
+      lazy_band_string<BKB, FP>(rhs, in, ws, out, R, bk, idr, fut, bm, lab, S, prof, si, L);
     }
   }
 }
